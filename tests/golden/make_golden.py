@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REAL reference in the build container.
+
+Run from the repo root (needs ``/root/reference``, which does not exist on the GPU box)::
+
+    python tests/golden/make_golden.py
+
+What it does (harness only; nothing here ships):
+
+* registers a minimal ``omegaconf`` stand-in (``OmegaConf.merge/create`` returning an
+  attribute dict) and synthetic ``gluefactory`` / ``gluefactory.models`` /
+  ``gluefactory.models.matchers`` / ``gluefactory.models.utils`` package objects whose
+  ``__path__`` points into ``/root/reference`` so their training-stack ``__init__`` files are
+  skipped;
+* imports ``gluefactory.models.matchers.lightglue`` and ``gluefactory_nonfree.superglue``;
+* builds ``LightGlue(conf)``, loads the deterministic recipe weights
+  (``lightglue_amd.weights.synthetic_state_dict``) with ``strict=True``, runs the seeded
+  ``synthetic_pair`` inputs through ``forward`` in eval mode, and writes the outputs into
+  ``tests/golden/<case>.npz``.  Inputs and weights are NOT stored (they are regenerated from
+  the recipe); their SHA-256 is, so recipe drift is detected.
+
+Early-stop cases: the reference reads an undefined ``self.confidence_thresholds``
+(``lightglue.py:592,604``); the harness sets that attribute on the instance to
+``[confidence_threshold(i) for i in range(L)]``.  When the stop fires, the reference then fails
+in ``torch.stack([])`` (``:572``) after the matches were computed; the harness swaps the
+module's ``torch`` for a proxy whose ``stack`` returns an empty tensor for an empty list, and the
+fixture omits ``ref_descriptors*``.
+"""
+import hashlib
+import importlib
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+import lgamd  # noqa: E402,F401
+from lightglue_amd.weights import synthetic_pair, synthetic_state_dict  # noqa: E402
+
+
+class _ADict(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def _merge(*cfgs):
+    out = _ADict()
+    for c in cfgs:
+        for k, v in (c or {}).items():
+            if isinstance(v, dict):
+                out[k] = _merge(out.get(k, {}) if isinstance(out.get(k), dict) else {}, v)
+            else:
+                out[k] = v
+    return out
+
+
+def install_shim():
+    om = types.ModuleType("omegaconf")
+
+    class OmegaConf:
+        merge = staticmethod(_merge)
+        create = staticmethod(lambda d=None: _merge(d or {}))
+        to_container = staticmethod(lambda d: dict(d))
+
+    om.OmegaConf = OmegaConf
+    om.DictConfig = _ADict
+    sys.modules["omegaconf"] = om
+    for name, path in [
+        ("gluefactory", "gluefactory"),
+        ("gluefactory.models", "gluefactory/models"),
+        ("gluefactory.models.matchers", "gluefactory/models/matchers"),
+        ("gluefactory.models.utils", "gluefactory/models/utils"),
+        ("gluefactory_nonfree", "gluefactory_nonfree"),
+    ]:
+        m = types.ModuleType(name)
+        m.__path__ = [os.path.join(REF, path)]
+        sys.modules[name] = m
+    bm = types.ModuleType("gluefactory.models.base_model")
+    bm.BaseModel = torch.nn.Module
+    sys.modules["gluefactory.models.base_model"] = bm
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    lg = importlib.import_module("gluefactory.models.matchers.lightglue")
+    sg = importlib.import_module("gluefactory_nonfree.superglue")
+    return lg, sg
+
+
+class _TorchProxy:
+    def __init__(self, real):
+        self._real = real
+
+    def __getattr__(self, k):
+        return getattr(self._real, k)
+
+    def stack(self, ts, *a, **kw):
+        if len(ts) == 0:
+            return self._real.empty(0)
+        return self._real.stack(ts, *a, **kw)
+
+
+def sha(arrs):
+    h = hashlib.sha256()
+    for k in sorted(arrs):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(arrs[k]).tobytes())
+    return h.hexdigest()
+
+
+# Per-layer matchability biases that prune ~10 % of the points per layer under the seed-6
+# recipe (keep iff sigmoid(z) > 1 - 0.95, i.e. z > -2.944; offsets from the 10 % quantile of the
+# unpruned logits).
+PRUNE_BIAS = [-2.97, -2.32, -2.90, -2.29, -3.00, -2.80, -2.14, -2.37]
+
+# name -> (conf overrides, pair kwargs, weight kwargs, weight overrides, store_full)
+CASES = {
+    "tiny_ragged_b2": ({"filter_threshold": 0.1}, dict(B=2, M=48, N=40, seed=11), dict(seed=0), {}, True),
+    "tiny_b1_n64": ({"filter_threshold": 0.0}, dict(B=1, M=64, N=64, seed=12), dict(seed=3), {}, True),
+    "n512": ({"filter_threshold": 0.1}, dict(B=1, M=512, seed=1), dict(seed=0), {}, False),
+    "n1024": ({"filter_threshold": 0.1}, dict(B=1, M=1024, seed=1), dict(seed=0), {}, False),
+    "n2048": ({"filter_threshold": 0.1}, dict(B=1, M=2048, seed=1), dict(seed=0), {}, False),
+    "n300x257_b2": ({"filter_threshold": 0.1}, dict(B=2, M=300, N=257, seed=5), dict(seed=1), {}, False),
+    "default_init_n256": ({"filter_threshold": 0.0}, dict(B=1, M=256, seed=7), dict(seed=2, sharpen=False), {}, False),
+    "scale_ori_n128": ({"filter_threshold": 0.1, "add_scale_ori": True}, dict(B=1, M=128, N=96, seed=8), dict(seed=4), {}, False),
+    "input_proj_n128": ({"filter_threshold": 0.1, "input_dim": 128}, dict(B=1, M=128, N=112, seed=9, dim=128), dict(seed=5), {}, False),
+    "prune_width_n512": (
+        {"filter_threshold": 0.1, "width_confidence": 0.95},
+        dict(B=1, M=512, N=480, seed=21),
+        dict(seed=6),
+        {"matchability_bias": PRUNE_BIAS},
+        False,
+    ),
+    "prune_depth_width_n512": (
+        {"filter_threshold": 0.1, "width_confidence": 0.95, "depth_confidence": 0.95},
+        dict(B=1, M=512, N=500, seed=22),
+        dict(seed=6),
+        {"matchability_bias": PRUNE_BIAS},
+        False,
+    ),
+    "early_stop_n256": (
+        {"filter_threshold": 0.1, "depth_confidence": 0.9},
+        dict(B=1, M=256, N=240, seed=23),
+        dict(seed=7),
+        {"token_bias_layer": (3, 6.0)},
+        False,
+    ),
+}
+
+
+def make_weights(conf, wkw, over):
+    sd = synthetic_state_dict(conf, **wkw)
+    L = conf.get("n_layers", 9)
+    if "matchability_bias" in over:
+        for i in range(L - 1):
+            sd[f"log_assignment.{i}.matchability.bias"][:] = over["matchability_bias"][i]
+    if "token_bias_layer" in over:
+        li, val = over["token_bias_layer"]
+        sd[f"token_confidence.{li}.token.0.bias"][:] = val
+    return sd
+
+
+def scale_ori(B, M, N, seed):
+    rng = np.random.Generator(np.random.PCG64(seed + 1000))
+    return {
+        "scales0": (rng.random((B, M)) * 2).astype(np.float32),
+        "oris0": (rng.random((B, M)) * 6.28 - 3.14).astype(np.float32),
+        "scales1": (rng.random((B, N)) * 2).astype(np.float32),
+        "oris1": (rng.random((B, N)) * 6.28 - 3.14).astype(np.float32),
+    }
+
+
+def run_case(lg_mod, name, spec):
+    conf, pkw, wkw, over, full = spec
+    sd = make_weights(conf, wkw, over)
+    pair = synthetic_pair(**pkw)
+    B, M = pkw["B"], pkw["M"]
+    N = pkw.get("N", M)
+    if conf.get("add_scale_ori"):
+        pair.update(scale_ori(B, M, N, pkw["seed"]))
+    model = lg_mod.LightGlue(dict(conf)).eval()
+    L = model.conf.n_layers
+    model.confidence_thresholds = [model.confidence_threshold(i) for i in range(L)]
+    missing = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    assert not missing.missing_keys and not missing.unexpected_keys
+    data = {k: torch.from_numpy(v) for k, v in pair.items() if not k.startswith("image_size")}
+    data["view0"] = {"image_size": torch.from_numpy(pair["image_size0"])}
+    data["view1"] = {"image_size": torch.from_numpy(pair["image_size1"])}
+    layers = []
+    hooks = [
+        t.register_forward_hook(lambda mod, inp, out: layers.append((out[0].clone(), out[1].clone())))
+        for t in model.transformers
+    ]
+    real_torch = lg_mod.torch
+    lg_mod.torch = _TorchProxy(real_torch)
+    try:
+        with torch.no_grad():
+            pred = model(data)
+    finally:
+        lg_mod.torch = real_torch
+        for h in hooks:
+            h.remove()
+    out = {
+        "matches0": pred["matches0"].numpy(),
+        "matches1": pred["matches1"].numpy(),
+        "matching_scores0": pred["matching_scores0"].numpy(),
+        "matching_scores1": pred["matching_scores1"].numpy(),
+        "prune0": pred["prune0"].numpy(),
+        "prune1": pred["prune1"].numpy(),
+        "n_layers_run": np.array(len(layers)),
+    }
+    la = pred["log_assignment"]
+    inner = la[:, :-1, :-1]
+    out["la_row_max"] = inner.max(2).values.numpy()
+    out["la_col_max"] = inner.max(1).values.numpy()
+    out["la_dustbin_col"] = la[:, :-1, -1].numpy()
+    out["la_dustbin_row"] = la[:, -1, :-1].numpy()
+    if pred["ref_descriptors0"].numel():
+        out["ref_descriptors0"] = pred["ref_descriptors0"].numpy() if full else pred["ref_descriptors0"][:, :, :8].numpy()
+        out["ref_descriptors1"] = pred["ref_descriptors1"].numpy() if full else pred["ref_descriptors1"][:, :, :8].numpy()
+    if full:
+        out["log_assignment"] = la.numpy()
+        for li, (a, b) in enumerate(layers):
+            out[f"layer{li}_desc0"] = a.numpy()
+            out[f"layer{li}_desc1"] = b.numpy()
+    meta = {
+        "conf": conf,
+        "pair": pkw,
+        "weights": wkw,
+        "overrides": {k: list(v) if isinstance(v, tuple) else v for k, v in over.items()},
+        "inputs_sha256": sha(pair),
+        "weights_sha256": sha(sd),
+        "store_full": full,
+    }
+    out["meta_json"] = np.array(json.dumps(meta))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    nm = int((out["matches0"] > -1).sum())
+    print(f"{name}: layers_run={len(layers)} matches={nm} prune0_min={out['prune0'].min()}", flush=True)
+
+
+def run_sinkhorn(sg_mod):
+    for name, (B, M, N, alpha, iters, seed) in {
+        "sinkhorn_b2_60x50": (2, 60, 50, 1.0, 50, 31),
+        "sinkhorn_b1_257x300": (1, 257, 300, 0.5, 50, 32),
+        "sinkhorn_b1_64x64_it3": (1, 64, 64, 2.0, 3, 33),
+    }.items():
+        rng = np.random.Generator(np.random.PCG64(seed))
+        scores = (rng.standard_normal((B, M, N)) * 2.0).astype(np.float32)
+        with torch.no_grad():
+            Z = sg_mod.log_optimal_transport(torch.from_numpy(scores), torch.tensor(alpha), iters)
+        Zi = Z[:, :-1, :-1]
+        max0, max1 = Zi.max(2), Zi.max(1)
+        meta = {"B": B, "M": M, "N": N, "alpha": alpha, "iters": iters, "seed": seed, "scale": 2.0}
+        np.savez_compressed(
+            os.path.join(HERE, f"{name}.npz"),
+            Z=Z.numpy(),
+            scores_sha256=np.array(sha({"scores": scores})),
+            row_argmax=max0.indices.numpy(),
+            col_argmax=max1.indices.numpy(),
+            meta_json=np.array(json.dumps(meta)),
+        )
+        print(f"{name}: Z range [{Z.min().item():.3f}, {Z.max().item():.3f}]", flush=True)
+
+
+def main():
+    torch.set_num_threads(8)
+    lg_mod, sg_mod = install_shim()
+    only = set(sys.argv[1:])
+    for name, spec in CASES.items():
+        if only and name not in only:
+            continue
+        run_case(lg_mod, name, spec)
+    if not only or "sinkhorn" in only:
+        run_sinkhorn(sg_mod)
+
+
+if __name__ == "__main__":
+    main()

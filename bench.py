@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X LightGlue matcher: image-pairs/s at N=2048 keypoints, d=256.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--npts N]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Workload (BASELINE.json configs[2]): SuperPoint-shaped synthetic pairs, N=2048 keypoints per
+image, 9 layers, no pruning, B=32 pairs per GPU per step (weak scaling: every rank matches its own
+32 pairs; a step also all-gathers the match results to every rank over RCCL when N > 1).
+Weights: deterministic random init of the full architecture (no network for checkpoints).
+One step = one full LightGlue.forward (positional encoding, 9 x self+cross layers, dual-softmax
+assignment with the [B,N+1,N+1] log_assignment written, mutual filter).
+
+Prints ONE JSON line on rank 0 with the metric, the attention kernel's roofline (in-library HIP
+events around every attention launch in the timed region; algorithmic flops per launch) and the
+CPU oracle's throughput on this host (rank 0, N=1 only, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import lgamd  # noqa: E402,F401
+from lightglue_amd import LightGlue  # noqa: E402
+from lightglue_amd.weights import synthetic_state_dict  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0
+
+
+def gpu_pairs(B, N, dim, seed, device, size=(640.0, 640.0)):
+    g = torch.Generator(device=device).manual_seed(seed)
+    wh = torch.tensor(size, device=device)
+    k0 = torch.rand((B, N, 2), generator=g, device=device) * wh
+    d0 = torch.randn((B, N, dim), generator=g, device=device)
+    d0 = d0 / d0.norm(dim=-1, keepdim=True)
+    perm = torch.argsort(torch.rand((B, N), generator=g, device=device), dim=1)
+    k1 = (torch.gather(k0, 1, perm[..., None].expand(-1, -1, 2)) + torch.randn((B, N, 2), generator=g, device=device)).clamp(0, 639.9)
+    d1 = torch.gather(d0, 1, perm[..., None].expand(-1, -1, dim)) + 0.05 * torch.randn((B, N, dim), generator=g, device=device)
+    d1 = d1 / d1.norm(dim=-1, keepdim=True)
+    isz = wh[None].expand(B, 2).contiguous()
+    return {
+        "keypoints0": k0, "keypoints1": k1, "descriptors0": d0, "descriptors1": d1,
+        "view0": {"image_size": isz}, "view1": {"image_size": isz},
+    }
+
+
+def attention_flops_per_pair(N, d=256, L=9):
+    return L * 14 * N * N * d  # SURVEY §8d attention term (self 8, cross 6 N^2 d per layer)
+
+
+def total_flops_per_pair(N, d=256, L=9):
+    return L * (76 * N * d * d + 14 * N * N * d) + 4 * N * d * d + 2 * N * N * d
+
+
+def cpu_baseline(npts, budget_s):
+    """The CPU oracle (torch-CPU restatement of the reference forward) on this host's cores."""
+    import oracle
+    from lightglue_amd.weights import synthetic_pair
+
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    conf = {"filter_threshold": 0.1}
+    sd = synthetic_state_dict(conf, seed=0)
+    data = synthetic_pair(B=1, M=npts, seed=1)
+    oracle.lightglue_forward(sd, data, conf)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        oracle.lightglue_forward(sd, data, conf)
+        n += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or n >= 50:
+            break
+    return {
+        "value": n / el,
+        "unit": "image-pairs/s",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": f"{n} pairs x N={npts} (B=1, 9 layers, fp32) in {el:.1f}s, torch-CPU oracle (oracle/lightglue_ref.py)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="pairs per GPU per step")
+    ap.add_argument("--npts", type=int, default=2048)
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work (0 = skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+
+    conf = {"filter_threshold": 0.1}
+    model = LightGlue(conf).eval().to(device)
+    sd = synthetic_state_dict(conf, seed=0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    B, N = args.batch, args.npts
+    data = gpu_pairs(B, N, 256, seed=1 + rank, device=device)
+
+    def step():
+        with torch.no_grad():
+            pred = model(data)
+        if distributed:  # RCCL all-gather of the match results
+            packed = torch.cat([pred["matches0"].float(), pred["matches1"].float(),
+                                pred["matching_scores0"], pred["matching_scores1"]], 1)
+            out = torch.empty((world,) + packed.shape, device=device, dtype=packed.dtype)
+            dist.all_gather_into_tensor(out, packed)
+        return pred
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    model.profile_enable(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pred = step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    att_ms, att_n, att_fl, att_by = model.profile_read("attention")
+    gem_ms, gem_n, gem_fl, _ = model.profile_read("gemm")
+    asg_ms, asg_n, _, asg_by = model.profile_read("assign")
+    model.profile_enable(False)
+    if distributed:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    pairs = B * args.steps * world
+    value = pairs / el
+    result = {
+        "metric": "image-pairs/sec at N=2048 kpts, d=256; HPatches AUC@3px parity",
+        "value": round(value, 3),
+        "unit": "image-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * el / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SuperPoint-shaped keypoints/descriptors, random-init weights)",
+        "config": {
+            "workload": "configs[2]: SuperPoint+LightGlue N=2048, 9 layers, no pruning, batch=32 per GPU",
+            "npts": N, "descriptor_dim": 256, "n_layers": 9, "pairs_per_gpu_per_step": B,
+            "global_batch": B * world, "parallelism": f"pair-sharded x{world} (+RCCL all-gather of matches)",
+        },
+        "achieved_tflops_total": round(total_flops_per_pair(N) * pairs / el / 1e12, 2),
+        "roofline": {
+            "kernel": "attention_f32_kernel (flash self/cross attention, f32 MFMA 32x32x2)",
+            "bound": "mfma",
+            "achieved": round(att_fl / (att_ms * 1e-3) / 1e12, 2) if att_ms > 0 else None,
+            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(att_fl / (att_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4) if att_ms > 0 else None,
+            "traffic": None,
+            "launches": att_n,
+            "avg_launch_ms": round(att_ms / max(att_n, 1), 4),
+            "algorithmic_flops_per_launch": att_fl / max(att_n, 1),
+        },
+        "kernels": {
+            "attention_ms_per_step": round(att_ms / args.steps, 3),
+            "gemm_ms_per_step": round(gem_ms / args.steps, 3),
+            "gemm_tflops": round(gem_fl / (gem_ms * 1e-3) / 1e12, 2) if gem_ms > 0 else None,
+            "assign_ms_per_step": round(asg_ms / args.steps, 3),
+            "assign_gbs": round(asg_by / (asg_ms * 1e-3) / 1e9, 1) if asg_ms > 0 else None,
+        },
+        "matches_per_pair": float((pred["matches0"] > -1).float().sum(1).mean()),
+    }
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        result["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+"""ctypes binding of liblightglue_mi355x.so (C-ABI in include/lightglue_mi355x.h).
+
+The library is built in-tree by ``make -C cs566-project-lightglue_amd/csrc`` (or
+``__graft_entry__.build()``).  There is no fallback: if the library is missing or fails to load,
+every entry point raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LIGHTGLUE_MI355X_LIB", os.path.join(_HERE, "liblightglue_mi355x.so"))
+ABI_VERSION = 1
+
+LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE = 0, -1, -2, -3, -4
+
+EXPORTED_SYMBOLS = [
+    "lg_abi_version",
+    "lg_last_error",
+    "lg_create",
+    "lg_destroy",
+    "lg_weight_count",
+    "lg_weight_name",
+    "lg_weight_numel",
+    "lg_load_weights",
+    "lg_workspace_bytes",
+    "lg_forward",
+    "lg_filter_workspace_bytes",
+    "lg_filter_matches",
+    "lg_sinkhorn_workspace_bytes",
+    "lg_log_optimal_transport",
+    "lg_profile_enable",
+    "lg_profile_read",
+]
+KERNEL_IDS = {"attention": 0, "gemm": 1, "assign": 2}
+
+
+class LGConfig(ctypes.Structure):
+    _fields_ = [
+        ("input_dim", ctypes.c_int32),
+        ("descriptor_dim", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("num_heads", ctypes.c_int32),
+        ("add_scale_ori", ctypes.c_int32),
+        ("depth_confidence", ctypes.c_double),
+        ("width_confidence", ctypes.c_double),
+        ("filter_threshold", ctypes.c_double),
+    ]
+
+
+_P = ctypes.c_void_p
+
+
+class LGInputs(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32),
+        ("M", ctypes.c_int32),
+        ("N", ctypes.c_int32),
+        ("keypoints0", _P),
+        ("keypoints1", _P),
+        ("descriptors0", _P),
+        ("descriptors1", _P),
+        ("image_size0", _P),
+        ("image_size1", _P),
+        ("scales0", _P),
+        ("oris0", _P),
+        ("scales1", _P),
+        ("oris1", _P),
+    ]
+
+
+class LGOutputs(ctypes.Structure):
+    _fields_ = [
+        ("matches0", _P),
+        ("matches1", _P),
+        ("matching_scores0", _P),
+        ("matching_scores1", _P),
+        ("log_assignment", _P),
+        ("ref_descriptors0", _P),
+        ("ref_descriptors1", _P),
+        ("prune0", _P),
+        ("prune1", _P),
+        ("stop_layer", ctypes.c_int32),
+        ("kept0", ctypes.c_int32),
+        ("kept1", ctypes.c_int32),
+    ]
+
+
+class LightGlueLibError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and type the C-ABI library.  Raises if it is missing: no fallback path."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LightGlueLibError(
+            f"HIP library not found at {LIB_PATH}; build it with `make -C cs566-project-lightglue_amd/csrc` "
+            "(or __graft_entry__.build())"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    sz = ctypes.c_size_t
+    i32 = ctypes.c_int32
+    sig = {
+        "lg_abi_version": (ctypes.c_int, []),
+        "lg_last_error": (ctypes.c_char_p, []),
+        "lg_create": (ctypes.c_int, [ctypes.POINTER(LGConfig), ctypes.c_int, ctypes.POINTER(_P)]),
+        "lg_destroy": (ctypes.c_int, [_P]),
+        "lg_weight_count": (ctypes.c_int, [_P]),
+        "lg_weight_name": (ctypes.c_char_p, [_P, ctypes.c_int]),
+        "lg_weight_numel": (ctypes.c_int64, [_P, ctypes.c_int]),
+        "lg_load_weights": (
+            ctypes.c_int,
+            [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64), _P],
+        ),
+        "lg_workspace_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_forward": (ctypes.c_int, [_P, ctypes.POINTER(LGInputs), ctypes.POINTER(LGOutputs), _P, sz, _P]),
+        "lg_filter_workspace_bytes": (ctypes.c_int, [i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_filter_matches": (ctypes.c_int, [_P, i32, i32, i32, ctypes.c_double, _P, _P, _P, _P, _P, sz, _P]),
+        "lg_sinkhorn_workspace_bytes": (ctypes.c_int, [i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_log_optimal_transport": (ctypes.c_int, [_P, ctypes.c_float, i32, i32, i32, i32, _P, _P, sz, _P]),
+        "lg_profile_enable": (ctypes.c_int, [_P, ctypes.c_int]),
+        "lg_profile_read": (
+            ctypes.c_int,
+            [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
+             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
+        ),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.lg_abi_version() != ABI_VERSION:
+        raise LightGlueLibError(f"ABI mismatch: library {lib.lg_abi_version()} != binding {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != LG_OK:
+        msg = load().lg_last_error().decode(errors="replace")
+        if rc == LG_E_INVALID and msg.startswith("max():"):
+            raise IndexError(msg)  # same exception type as the reference's torch.max on an empty dim
+        raise LightGlueLibError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,315 @@
+// Bandwidth-bound kernels of the LightGlue hot path (gfx950): positional encoding, fused
+// LayerNorm+GELU, 256-wide GEMVs (matchability / token confidence), weight repacking and the
+// point-pruning compaction.  One wave per row wherever a row reduction is needed.
+#include "common.h"
+#include "kernels.h"
+
+namespace lg {
+
+// ----------------------------------------------------------------------------------------
+// normalize_keypoints (lightglue.py:21-33) + ConditionalLearnableFourierPositionalEncoding
+// (lightglue.py:63-77).  The op order mirrors torch-CPU exactly (probed in the build
+// container): Wr(x) = fma chain starting from x0*w0 (MKL sgemm, K = 2), the condition
+// Linear(1,32) is a separate multiply and add, then `projected + condition` is a separate add.
+// With the reference's default init the condition term reaches |2000|, so a single rounding
+// difference moves the phase by ~1e-4 rad; mirroring the order keeps the phases bit-exact.
+// ----------------------------------------------------------------------------------------
+__global__ void kpt_extent_kernel(const float* kpts, int n, float* size_out) {
+  // size = 1 + max - min over the pair's keypoints (lightglue.py:25-26); one block per pair.
+  const int b = blockIdx.x;
+  float mx[2] = {-INFINITY, -INFINITY}, mn[2] = {INFINITY, INFINITY};
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float v = kpts[((size_t)b * n + i) * 2 + c];
+      mx[c] = fmaxf(mx[c], v);
+      mn[c] = fminf(mn[c], v);
+    }
+  }
+  __shared__ float red[4][256];
+  red[0][threadIdx.x] = mx[0]; red[1][threadIdx.x] = mx[1];
+  red[2][threadIdx.x] = mn[0]; red[3][threadIdx.x] = mn[1];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      red[0][threadIdx.x] = fmaxf(red[0][threadIdx.x], red[0][threadIdx.x + s]);
+      red[1][threadIdx.x] = fmaxf(red[1][threadIdx.x], red[1][threadIdx.x + s]);
+      red[2][threadIdx.x] = fminf(red[2][threadIdx.x], red[2][threadIdx.x + s]);
+      red[3][threadIdx.x] = fminf(red[3][threadIdx.x], red[3][threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 2) size_out[b * 2 + threadIdx.x] = add_rn(1.f, sub_rn(red[threadIdx.x][0], red[2 + threadIdx.x][0]));
+}
+
+__global__ void pe_kernel(PEArgs a) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;  // (point, freq)
+  const int f = gid & 31;
+  const int pt = gid >> 5;
+  if (pt >= a.B * a.n) return;
+  const int b = pt / a.n;
+  const float w = a.size[b * 2 + 0], h = a.size[b * 2 + 1];
+  const float scale = div_rn(fmaxf(w, h), 2.f);
+  float x[4];
+  x[0] = div_rn(sub_rn(a.kpts[(size_t)pt * 2 + 0], div_rn(w, 2.f)), scale);
+  x[1] = div_rn(sub_rn(a.kpts[(size_t)pt * 2 + 1], div_rn(h, 2.f)), scale);
+  if (a.m_in == 4) {
+    x[2] = a.scales[pt];
+    x[3] = a.oris[pt];
+  }
+  const float* wr = a.Wr + f * a.m_in;
+  float p = mul_rn(x[0], wr[0]);
+  for (int k = 1; k < a.m_in; ++k) p = __fmaf_rn(x[k], wr[k], p);
+  const float cond = add_rn(mul_rn((float)a.n, a.Wc[f]), a.bc[f]);  // relu(n) = n
+  p = add_rn(p, cond);
+  a.cosb[(size_t)pt * kFreq + f] = cosf(p);
+  a.sinb[(size_t)pt * kFreq + f] = sinf(p);
+}
+
+hipError_t positional_encoding(const PEArgs& a0, hipStream_t st) {
+  if (a0.B * a0.n == 0) return hipSuccess;
+  const int threads = a0.B * a0.n * 32;
+  hipLaunchKernelGGL(pe_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, a0);
+  return hipGetLastError();
+}
+
+hipError_t kpt_extent(const float* kpts, int B, int n, float* size_out, hipStream_t st) {
+  if (B == 0) return hipSuccess;
+  hipLaunchKernelGGL(kpt_extent_kernel, dim3(B), dim3(256), 0, st, kpts, n, size_out);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// ffn.1 LayerNorm(512, eps 1e-5) + ffn.2 GELU(erf) (lightglue.py:171-176), in place.
+// One wave per row: lane holds columns [4l, 4l+4) and [256+4l, 256+4l+4).
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ln_gelu_kernel(float* x, const float* g, const float* bta, int rows) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float* xr = x + (size_t)row * 512;
+  f32x4 v0 = *reinterpret_cast<f32x4*>(xr + lane * 4);
+  f32x4 v1 = *reinterpret_cast<f32x4*>(xr + 256 + lane * 4);
+  float s = (v0[0] + v0[1]) + (v0[2] + v0[3]) + (v1[0] + v1[1]) + (v1[2] + v1[3]);
+  const float mean = wave_sum(s) * (1.f / 512.f);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float d0 = v0[i] - mean, d1 = v1[i] - mean;
+    q += d0 * d0 + d1 * d1;
+  }
+  const float var = wave_sum(q) * (1.f / 512.f);
+  const float rstd = 1.f / sqrtf(var + 1e-5f);
+  const f32x4 g0 = *reinterpret_cast<const f32x4*>(g + lane * 4), g1 = *reinterpret_cast<const f32x4*>(g + 256 + lane * 4);
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(bta + lane * 4), b1 = *reinterpret_cast<const f32x4*>(bta + 256 + lane * 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float y0 = (v0[i] - mean) * rstd * g0[i] + b0[i];
+    float y1 = (v1[i] - mean) * rstd * g1[i] + b1[i];
+    v0[i] = 0.5f * y0 * (1.f + erff(y0 * 0.70710678118654752f));
+    v1[i] = 0.5f * y1 * (1.f + erff(y1 * 0.70710678118654752f));
+  }
+  *reinterpret_cast<f32x4*>(xr + lane * 4) = v0;
+  *reinterpret_cast<f32x4*>(xr + 256 + lane * 4) = v1;
+}
+
+hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(ln_gelu_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, g, b, rows);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// Linear(256 -> 1) (+ sigmoid): MatchAssignment.matchability (lightglue.py:303,312-313,318)
+// and TokenConfidence.token (:99,104-106).  One wave per row.
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gemv256_kernel(const float* x, const float* w, const float* b, float* y, int rows,
+                                                      int sigmoid) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const f32x4 xv = *reinterpret_cast<const f32x4*>(x + (size_t)row * kDim + lane * 4);
+  const f32x4 wv = *reinterpret_cast<const f32x4*>(w + lane * 4);
+  float s = xv[0] * wv[0] + xv[1] * wv[1] + xv[2] * wv[2] + xv[3] * wv[3];
+  s = wave_sum(s);
+  if (lane == 0) {
+    float v = s + b[0];
+    if (sigmoid) v = 1.f / (1.f + expf(-v));
+    y[row] = v;
+  }
+}
+
+hipError_t gemv_256(const float* x, const float* w, const float* b, float* y, int rows, int sigmoid, hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(gemv256_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, y, rows, sigmoid);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// weight repacking
+// ----------------------------------------------------------------------------------------
+__global__ void gather_rows_kernel(float* dst, const float* src, const int* idx, int rows, int cols) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)rows * cols) return;
+  const int r = (int)(i / cols), c = (int)(i % cols);
+  dst[i] = src[(size_t)idx[r] * cols + c];
+}
+
+hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st) {
+  const size_t n = (size_t)rows * cols;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dst, src, idx, rows, cols);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// Point pruning (lightglue.py:532-547, get_pruning_mask :586-593) and early stop
+// (check_if_stop :595-606), batch 1.
+// ----------------------------------------------------------------------------------------
+__global__ void prune_flags_kernel(const float* zmatch, const float* token, float width_thr, float conf_thr, int n,
+                                   int* flags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float prob = 1.f / (1.f + expf(-zmatch[i]));  // sigmoid(matchability)
+  bool keep = prob > width_thr;
+  if (token) keep = keep || (token[i] <= conf_thr);
+  flags[i] = keep ? 1 : 0;
+}
+
+hipError_t prune_flags(const float* zmatch, const float* token, float width_thr, float conf_thr, int n, int* flags,
+                       hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(prune_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, st, zmatch, token, width_thr, conf_thr, n,
+                     flags);
+  return hipGetLastError();
+}
+
+__global__ void count_below_kernel(const float* token, float thr, int n, int* counter) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool below = i < n && token[i] < thr;
+  const unsigned long long m = __ballot(below);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, (int)__popcll(m));
+}
+
+hipError_t count_below(const float* token, float thr, int n, int* counter, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(count_below_kernel, dim3((n + 255) / 256), dim3(256), 0, st, token, thr, n, counter);
+  return hipGetLastError();
+}
+
+// Exclusive scan of 0/1 flags in one workgroup (n is a keypoint count, <= a few 10^4).
+__global__ __launch_bounds__(1024) void compact_scan_kernel(const int* flags, int n, int* pos, int* count) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + threadIdx.x;
+    const int f = i < n ? flags[i] : 0;
+    const unsigned long long m = __ballot(f != 0);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = __popcll(m);
+    __syncthreads();
+    int off = carry;
+    for (int w = 0; w < wave; ++w) off += wsum[w];
+    if (i < n) pos[i] = off + before;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int w = 0; w < 16; ++w) t += wsum[w];
+      carry += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = carry;
+}
+
+hipError_t compact_scan(const int* flags, int n, int* pos, int* count, hipStream_t st) {
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, st, flags, n, pos, count);
+  return hipGetLastError();
+}
+
+__global__ void compact_rows_kernel(const float* src, float* dst, const int* flags, const int* pos, int n, int cols) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)n * cols) return;
+  const int r = (int)(i / cols), c = (int)(i % cols);
+  if (flags[r]) dst[(size_t)pos[r] * cols + c] = src[i];
+}
+
+hipError_t compact_rows(const float* src, float* dst, const int* flags, const int* pos, int n, int cols, hipStream_t st) {
+  const size_t t = (size_t)n * cols;
+  if (t == 0) return hipSuccess;
+  hipLaunchKernelGGL(compact_rows_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, src, dst, flags, pos, n,
+                     cols);
+  return hipGetLastError();
+}
+
+__global__ void compact_index_kernel(const int* ind, int* ind_out, int64_t* prune, const int* flags, const int* pos,
+                                     int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !flags[i]) return;
+  const int orig = ind[i];
+  ind_out[pos[i]] = orig;
+  prune[orig] += 1;  // prune0[:, ind0] += 1 after the selection (lightglue.py:540)
+}
+
+hipError_t compact_index(const int* ind, int* ind_out, int64_t* prune, const int* flags, const int* pos, int n,
+                         hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(compact_index_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ind, ind_out, prune, flags, pos, n);
+  return hipGetLastError();
+}
+
+__global__ void iota_kernel(int* p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = i;
+}
+hipError_t iota_fill(int* ind, int n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ind, n);
+  return hipGetLastError();
+}
+
+__global__ void fill_i64_kernel(int64_t* p, int64_t v, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+hipError_t fill_i64(int64_t* p, int64_t v, size_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_i64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, v, n);
+  return hipGetLastError();
+}
+
+// Scatter compact matches back to full size (lightglue.py:553-562).
+__global__ void remap_kernel(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind0,
+                             const int* ind1, int kept0, int kept1, int64_t* m0, int64_t* m1, float* s0, float* s1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < kept0) {
+    const int64_t j = m0c[i];
+    m0[ind0[i]] = j == -1 ? -1 : (int64_t)ind1[j];
+    s0[ind0[i]] = s0c[i];
+  } else if (i < kept0 + kept1) {
+    const int k = i - kept0;
+    const int64_t j = m1c[k];
+    m1[ind1[k]] = j == -1 ? -1 : (int64_t)ind0[j];
+    s1[ind1[k]] = s1c[k];
+  }
+}
+
+hipError_t remap_matches(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind0,
+                         const int* ind1, int kept0, int kept1, int64_t* m0, int64_t* m1, float* s0, float* s1, int M,
+                         int N, hipStream_t st) {
+  hipError_t e;
+  if ((e = fill_i64(m0, -1, M, st)) != hipSuccess) return e;
+  if ((e = fill_i64(m1, -1, N, st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(s0, 0, sizeof(float) * M, st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(s1, 0, sizeof(float) * N, st)) != hipSuccess) return e;
+  const int n = kept0 + kept1;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(remap_kernel, dim3((n + 255) / 256), dim3(256), 0, st, m0c, m1c, s0c, s1c, ind0, ind1, kept0, kept1,
+                     m0, m1, s0, s1);
+  return hipGetLastError();
+}
+
+}  // namespace lg

@@ -1,0 +1,230 @@
+// fp32 "linear" GEMM on gfx950 f32-input MFMA (v_mfma_f32_32x32x2_f32), with fused epilogues.
+//
+//   Y[r, c] = epilogue( sum_k A[r, k] * W[c, k] + bias[c] )
+//
+// Replaces every nn.Linear on the LightGlue hot path (reference lightglue.py):
+//   SelfBlock.Wqkv        :168,184   -> EPI_QKV_ROT  (+ rotary :36-43,187-188, head-major scatter :185-186)
+//   SelfBlock.out_proj    :170,190   -> EPI_STORE
+//   CrossBlock.to_qk/to_v :203-204,223-228,235 -> EPI_CROSS_QKV (one GEMM, 512 outputs, qk * scale^0.5)
+//   CrossBlock.to_out     :205,246   -> EPI_STORE
+//   ffn.0 on cat([x,msg]) :172,191,247-248 -> EPI_STORE with a two-source A (the cat is never built)
+//   ffn.3 + residual      :175,191   -> EPI_STORE with res (x + ffn(...))
+//   MatchAssignment.final_proj / d^.25 :304,308-310 -> EPI_STORE with out_scale 0.25
+//   MatchAssignment einsum bmd,bnd->bmn :311 -> EPI_STORE, batched over pairs (blockIdx.z)
+//
+// Tiling: BM x BN block tile, BK = 32, one wave per WM x WN sub-tile of 32x32 MFMA tiles.
+// K is permuted inside each 32-wide k-tile (MFMA step s, lane half h uses k = 16h + s) so a
+// lane's operands for 4 consecutive steps are one 16-byte LDS read.  LDS rows are padded to
+// 36 floats: the 16 lanes of each ds_read_b128 group then hit 16 distinct 4-bank slots.
+// Global->LDS is register-staged and double-buffered (one barrier per k-tile).
+// blockIdx -> tile goes through a bijective XCD remap so tiles sharing A rows share an L2.
+#include "common.h"
+#include "kernels.h"
+
+namespace lg {
+
+constexpr int BK = 32;
+constexpr int LDS_STRIDE = BK + 4;  // floats
+
+__device__ __forceinline__ int xcd_remap(int id, int n) {
+  const int xcd = id & 7, local = id >> 3;
+  const int base = n >> 3, extra = n & 7;
+  return xcd * base + (xcd < extra ? xcd : extra) + local;
+}
+
+// row -> (set, b, n) for the two-image row space: rows [0, B*M) are image 0, then image 1.
+__device__ __forceinline__ size_t head_row_offset(const HeadLayout& hl, int row, int head) {
+  int b, n, cnt;
+  size_t base;
+  if (row < hl.B * hl.M) {
+    b = row / hl.M; n = row - b * hl.M; cnt = hl.M; base = 0;
+  } else {
+    const int r2 = row - hl.B * hl.M;
+    b = r2 / hl.N; n = r2 - b * hl.N; cnt = hl.N; base = (size_t)hl.B * hl.H * hl.M * kHeadDim;
+  }
+  return base + ((size_t)(b * hl.H + head) * cnt + n) * kHeadDim;
+}
+
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(GemmArgs args) {
+  constexpr int NWN = BN / WN;
+  constexpr int NT = 64 * (BM / WM) * NWN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int A_LD = BM * BK / 4 / NT;  // float4 loads per thread per k-tile
+  constexpr int B_LD = BN * BK / 4 / NT;
+  static_assert(BM * BK / 4 % NT == 0 && BN * BK / 4 % NT == 0, "tile/threads mismatch");
+
+  __shared__ float As[2][BM * LDS_STRIDE];
+  __shared__ float Bs[2][BN * LDS_STRIDE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, half = lane >> 5;
+  const int wm0 = (wave / NWN) * WM, wn0 = (wave % NWN) * WN;
+
+  const int num_m = (args.R + BM - 1) / BM;
+  const int num_n = (args.Nout + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, num_m * num_n);
+  const int tm_blk = tile / num_n, tn_blk = tile - tm_blk * num_n;
+  const int m0 = tm_blk * BM, n0 = tn_blk * BN;
+  const size_t z = blockIdx.z;
+
+  const float* A0 = args.A0 + z * args.sA;
+  const float* A1 = args.A1 ? args.A1 + z * args.sA1 : nullptr;
+  const float* W = args.W + z * args.sW;
+
+  f32x4 ra[A_LD], rb[B_LD];
+  auto gload = [&](int kt) {
+    const int k0 = kt * BK;
+    const float* src;
+    int ld, kk;
+    if (k0 < args.K0) { src = A0; ld = args.lda0; kk = k0; }
+    else { src = A1; ld = args.lda1; kk = k0 - args.K0; }
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int q = tid + i * NT;
+      const int r = q >> 3, c4 = q & 7;
+      int row = m0 + r;
+      row = row < args.R ? row : args.R - 1;
+      ra[i] = *reinterpret_cast<const f32x4*>(src + (size_t)row * ld + kk + c4 * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int q = tid + i * NT;
+      const int r = q >> 3, c4 = q & 7;
+      int col = n0 + r;
+      col = col < args.Nout ? col : args.Nout - 1;
+      rb[i] = *reinterpret_cast<const f32x4*>(W + (size_t)col * args.ldw + k0 + c4 * 4);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int q = tid + i * NT;
+      *reinterpret_cast<f32x4*>(&As[buf][(q >> 3) * LDS_STRIDE + (q & 7) * 4]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int q = tid + i * NT;
+      *reinterpret_cast<f32x4*>(&Bs[buf][(q >> 3) * LDS_STRIDE + (q & 7) * 4]) = rb[i];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{0.f};
+
+  const int nk = args.K / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(kt + 1);
+    const float* as = &As[cur][0];
+    const float* bs = &Bs[cur][0];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      f32x4 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        a[i] = *reinterpret_cast<const f32x4*>(as + (wm0 + i * 32 + l32) * LDS_STRIDE + half * 16 + s4 * 4);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b[j] = *reinterpret_cast<const f32x4*>(bs + (wn0 + j * 32 + l32) * LDS_STRIDE + half * 16 + s4 * 4);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][kk], b[j][kk], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ------------------------------------------------------------------ epilogues
+  float* Y = args.Y ? args.Y + z * args.sY : nullptr;
+  if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn0 + j * 32 + l32;
+      if (col >= args.Nout) continue;
+      const float bj = args.bias ? args.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + i * 32 + row32(r, half);
+          if (row >= args.R) continue;
+          float v = (acc[i][j][r] + bj) * args.out_scale;
+          if (args.res) v = args.res[(size_t)row * args.ldr + col] + v;
+          Y[(size_t)row * args.ldy + col] = v;
+        }
+    }
+  } else {
+    // Head-major scatter.  WN == 64 and n0 + wn0 is a multiple of 64, so the wave owns one
+    // (type, head) block: type t = col / 256, head = (col % 256) / 64, stored dim = j*32 + l32.
+    static_assert(EPI != EPI_QKV_ROT || (WN == 64 && TN == 2), "rotary epilogue needs 64-wide wave tiles");
+    const HeadLayout& hl = args.hl;
+    const int cbase = n0 + wn0;
+    const int t = cbase / kDim, head = (cbase % kDim) / kHeadDim;
+    float* dst = t == 0 ? hl.q : (t == 1 ? hl.k : hl.v);
+    float b2[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b2[j] = args.bias[cbase + j * 32 + l32];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + row32(r, half);
+        if (row >= args.R) continue;
+        const size_t off = head_row_offset(hl, row, head);
+        if constexpr (EPI == EPI_QKV_ROT) {
+          const float xe = acc[i][0][r] + b2[0];  // dim 2*l32   (even)
+          const float xo = acc[i][1][r] + b2[1];  // dim 2*l32+1 (odd)
+          if (t < 2) {
+            // t*cos + rotate_half(t)*sin, rotate_half(x)[2i] = -x[2i+1], [2i+1] = x[2i]
+            const float c = hl.cosb[(size_t)row * kFreq + l32];
+            const float s = hl.sinb[(size_t)row * kFreq + l32];
+            dst[off + l32] = add_rn(mul_rn(xe, c), mul_rn(-xo, s));
+            dst[off + 32 + l32] = add_rn(mul_rn(xo, c), mul_rn(xe, s));
+          } else {
+            dst[off + l32] = xe;
+            dst[off + 32 + l32] = xo;
+          }
+        } else {  // EPI_CROSS_QKV
+          const float sc = t == 0 ? hl.qk_scale : 1.f;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) dst[off + j * 32 + l32] = (acc[i][j][r] + b2[j]) * sc;
+        }
+      }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI>
+static hipError_t launch(const GemmArgs& a, int batch, hipStream_t st) {
+  const int nt = 64 * (BM / WM) * (BN / WN);
+  const int blocks = ((a.R + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
+  if (blocks == 0 || batch == 0) return hipSuccess;
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI>), dim3(blocks, 1, batch), dim3(nt), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, hipStream_t st) {
+  if (a.K % BK != 0 || (a.A1 && a.K0 % BK != 0)) return hipErrorInvalidValue;
+  switch (epi) {
+    case EPI_STORE:
+      return launch<64, 256, 64, 64, EPI_STORE>(a, batch, st);
+    case EPI_QKV_ROT:
+      return launch<64, 256, 64, 64, EPI_QKV_ROT>(a, batch, st);
+    case EPI_CROSS_QKV:
+      return launch<64, 256, 64, 64, EPI_CROSS_QKV>(a, batch, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace lg

@@ -1,0 +1,114 @@
+// Host-visible launch wrappers for the gfx950 kernels (internal to liblightglue_mi355x.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lg {
+
+enum EpiKind { EPI_STORE = 0, EPI_QKV_ROT = 1, EPI_CROSS_QKV = 2 };
+
+// Head-major destination [set][b][h][n][64] for the QKV epilogues; set 0 = image 0 (B*M rows),
+// set 1 = image 1 (B*N rows), rows in GEMM order (image 0 rows first).
+struct HeadLayout {
+  float* q;
+  float* k;
+  float* v;
+  int B, H, M, N;
+  const float* cosb;  // [rows][32] rotary cos table, by GEMM row
+  const float* sinb;
+  float qk_scale;
+};
+
+struct GemmArgs {
+  const float* A0;  // [R][lda0], columns [0, K0)
+  int lda0, K0;
+  const float* A1;  // [R][lda1], columns [K0, K) (nullable: K0 == K)
+  int lda1;
+  const float* W;   // [Nout][ldw] (PyTorch Linear layout), k contiguous
+  int ldw, K;
+  const float* bias;  // [Nout] or null
+  const float* res;   // residual [R][ldr] or null (EPI_STORE): Y = res + (acc + bias) * out_scale
+  int ldr;
+  float* Y;
+  int ldy;
+  float out_scale;
+  int R, Nout;
+  long long sA, sA1, sW, sY;  // per-blockIdx.z strides (floats)
+  HeadLayout hl;
+};
+
+hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, hipStream_t st);
+
+// Attention over head-major Q/K/V ([set][b][h][n][64]); O written row-major into ctx
+// [rows][256] at column h*64 (rows in GEMM order).  Two "sets" per launch (blockIdx.z).
+struct AttnSet {
+  const float* q;  // [B][H][Nq][64]
+  const float* k;  // [B][H][Nk][64]
+  const float* v;  // [B][H][Nk][64]
+  float* o;        // ctx + row_base*256
+  int Nq, Nk;
+};
+hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st);
+
+// Positional encoding: normalised keypoints -> cos/sin tables [rows][32].
+struct PEArgs {
+  const float* kpts;   // [B][n][2]
+  const float* size;   // [B][2] or null
+  const float* scales; // [B][n] or null
+  const float* oris;   // [B][n] or null
+  const float* Wr;     // [32][m_in]
+  const float* Wc;     // [32]
+  const float* bc;     // [32]
+  float* cosb;         // [B*n][32]
+  float* sinb;
+  int B, n, m_in;
+};
+hipError_t positional_encoding(const PEArgs& a, hipStream_t st);
+// size = 1 + max - min of each pair's keypoints (normalize_keypoints fallback, lightglue.py:25-26)
+hipError_t kpt_extent(const float* kpts, int B, int n, float* size_out, hipStream_t st);
+
+hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, hipStream_t st);
+// y[r] = dot(x[r,:256], w) + b ; optional sigmoid
+hipError_t gemv_256(const float* x, const float* w, const float* b, float* y, int rows, int sigmoid, hipStream_t st);
+
+// Dual-softmax assignment + mutual filter (lightglue.py:284-296, 321-337).
+struct AssignArgs {
+  const float* sim;  // [B][M][N]
+  const float* z0;   // [B*M] matchability logits
+  const float* z1;   // [B*N]
+  float* la;         // [B][M+1][N+1] or null
+  float* ws;         // scratch
+  int B, M, N;
+  float th;
+  int64_t* m0; int64_t* m1; float* s0; float* s1;
+};
+size_t assign_workspace_floats(int B, int M, int N);
+hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st);
+// filter_matches on an existing [B][M+1][N+1] log-assignment.
+hipError_t filter_from_scores(const float* scores, int B, int M, int N, float th, float* ws, int64_t* m0, int64_t* m1,
+                              float* s0, float* s1, hipStream_t st);
+size_t filter_workspace_floats(int B, int M, int N);
+
+// Weight repacking: dst[r,:] = src[idx[r],:] (row length `cols`).
+hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st);
+
+// Pruning support (B == 1).
+hipError_t prune_flags(const float* zmatch, const float* token, float width_thr, float conf_thr, int n, int* flags,
+                       hipStream_t st);
+hipError_t count_below(const float* token, float thr, int n, int* counter, hipStream_t st);
+hipError_t compact_scan(const int* flags, int n, int* pos, int* count, hipStream_t st);
+hipError_t compact_rows(const float* src, float* dst, const int* flags, const int* pos, int n, int cols, hipStream_t st);
+hipError_t compact_index(const int* ind, int* ind_out, int64_t* prune, const int* flags, const int* pos, int n,
+                         hipStream_t st);
+hipError_t iota_fill(int* ind, int n, hipStream_t st);
+hipError_t fill_i64(int64_t* p, int64_t v, size_t n, hipStream_t st);
+hipError_t remap_matches(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind0,
+                         const int* ind1, int kept0, int kept1, int64_t* m0, int64_t* m1, float* s0, float* s1, int M,
+                         int N, hipStream_t st);
+
+// Sinkhorn (superglue.py:173-201).
+size_t sinkhorn_workspace_floats(int B, int M, int N);
+hipError_t log_optimal_transport(const float* scores, float alpha, int B, int M, int N, int iters, float* Z, float* ws,
+                                 hipStream_t st);
+
+}  // namespace lg

@@ -1,0 +1,716 @@
+// C-ABI of liblightglue_mi355x.so: handle, weight repacking and the LightGlue eval forward
+// orchestration (reference gluefactory/models/matchers/lightglue.py:444-579).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/lightglue_mi355x.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define LG_HIP(expr)                                                                                \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    if (_e != hipSuccess)                                                                           \
+      return fail(LG_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));                     \
+  } while (0)
+
+struct Tensor {
+  std::string name;
+  std::vector<int64_t> shape;
+  int64_t numel() const {
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    return n;
+  }
+};
+
+// Same order as lightglue_amd.weights.state_dict_schema (lightglue.py:367-398).
+std::vector<Tensor> make_schema(const lg_config_t& c) {
+  const int64_t d = c.descriptor_dim, din = c.input_dim, L = c.n_layers;
+  const int64_t hd = d / c.num_heads, m_in = 2 + 2 * (c.add_scale_ori ? 1 : 0);
+  std::vector<Tensor> s;
+  auto add = [&](const std::string& n, std::vector<int64_t> sh) { s.push_back({n, sh}); };
+  auto ffn = [&](const std::string& p) {
+    add(p + ".ffn.0.weight", {2 * d, 2 * d});
+    add(p + ".ffn.0.bias", {2 * d});
+    add(p + ".ffn.1.weight", {2 * d});
+    add(p + ".ffn.1.bias", {2 * d});
+    add(p + ".ffn.3.weight", {d, 2 * d});
+    add(p + ".ffn.3.bias", {d});
+  };
+  if (din != d) {
+    add("input_proj.weight", {d, din});
+    add("input_proj.bias", {d});
+  }
+  add("posenc.Wr.weight", {hd / 2, m_in});
+  add("posenc.condition_modulation.weight", {hd / 2, 1});
+  add("posenc.condition_modulation.bias", {hd / 2});
+  for (int64_t i = 0; i < L; ++i) {
+    const std::string sp = "transformers." + std::to_string(i) + ".self_attn";
+    add(sp + ".Wqkv.weight", {3 * d, d});
+    add(sp + ".Wqkv.bias", {3 * d});
+    add(sp + ".out_proj.weight", {d, d});
+    add(sp + ".out_proj.bias", {d});
+    ffn(sp);
+    const std::string cp = "transformers." + std::to_string(i) + ".cross_attn";
+    add(cp + ".to_qk.weight", {d, d});
+    add(cp + ".to_qk.bias", {d});
+    add(cp + ".to_v.weight", {d, d});
+    add(cp + ".to_v.bias", {d});
+    add(cp + ".to_out.weight", {d, d});
+    add(cp + ".to_out.bias", {d});
+    ffn(cp);
+  }
+  for (int64_t i = 0; i < L; ++i) {
+    const std::string a = "log_assignment." + std::to_string(i);
+    add(a + ".matchability.weight", {1, d});
+    add(a + ".matchability.bias", {1});
+    add(a + ".final_proj.weight", {d, d});
+    add(a + ".final_proj.bias", {d});
+  }
+  for (int64_t i = 0; i + 1 < L; ++i) {
+    const std::string t = "token_confidence." + std::to_string(i) + ".token.0";
+    add(t + ".weight", {1, d});
+    add(t + ".bias", {1});
+  }
+  return s;
+}
+
+constexpr int D = 256;
+
+// Packed per-layer weights (offsets in floats into one device buffer).
+struct BlockW {
+  size_t Wqkv, bqkv, Wo, bo, W1, b1, g, be, W2, b2;
+};
+struct LayerW {
+  BlockW self, cross;
+  size_t Wf, bf, wm, bm, wt, bt;
+};
+
+size_t align64(size_t n) { return (n + 63) & ~size_t(63); }
+
+}  // namespace
+
+struct lg_handle {
+  lg_config_t cfg;
+  int device;
+  std::vector<Tensor> schema;
+  std::map<std::string, int> index;
+  // where each schema tensor goes: destination offset (floats), or gather for Wqkv
+  std::vector<size_t> dst;
+  std::vector<LayerW> layers;
+  size_t Wr, Wc, bc, Wi, bi, total;
+  float* wbuf = nullptr;
+  int* perm = nullptr;  // Wqkv row permutation [768]
+  bool loaded = false;
+  // profiling (lg_profile_enable / lg_profile_read)
+  struct Rec {
+    hipEvent_t a, b;
+    int kind;
+    double flops, bytes;
+  };
+  bool prof_on = false;
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t ev() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  int prof_begin(int kind, hipStream_t st) {
+    if (!prof_on) return -1;
+    Rec r{ev(), ev(), kind, 0.0, 0.0};
+    (void)hipEventRecord(r.a, st);
+    recs.push_back(r);
+    return (int)recs.size() - 1;
+  }
+  void prof_end(int idx, double flops, double bytes, hipStream_t st) {
+    if (idx < 0) return;
+    recs[idx].flops = flops;
+    recs[idx].bytes = bytes;
+    (void)hipEventRecord(recs[idx].b, st);
+  }
+};
+
+namespace {
+
+// Packed Wqkv row order: c' = t*256 + h*64 + j ; for q,k (t<2) j<32 -> dim 2j, j>=32 -> dim
+// 2(j-32)+1 (rotary partners in the same lane of the GEMM tile); v keeps natural dims.
+// Reference layout (lightglue.py:185): row = h*192 + dim*3 + t.
+std::vector<int> wqkv_perm(int H) {
+  std::vector<int> p(3 * D);
+  for (int t = 0; t < 3; ++t)
+    for (int h = 0; h < H; ++h)
+      for (int j = 0; j < 64; ++j) {
+        const int dim = t < 2 ? (j < 32 ? 2 * j : 2 * (j - 32) + 1) : j;
+        p[t * D + h * 64 + j] = h * 192 + dim * 3 + t;
+      }
+  return p;
+}
+
+void plan_layout(lg_handle* h) {
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    size_t o = off;
+    off += align64(n);
+    return o;
+  };
+  const int L = h->cfg.n_layers;
+  const int m_in = 2 + 2 * (h->cfg.add_scale_ori ? 1 : 0);
+  h->layers.resize(L);
+  h->Wr = take(32 * m_in);
+  h->Wc = take(32);
+  h->bc = take(32);
+  h->Wi = take((size_t)D * h->cfg.input_dim);
+  h->bi = take(D);
+  for (int i = 0; i < L; ++i) {
+    for (int b = 0; b < 2; ++b) {
+      BlockW& w = b == 0 ? h->layers[i].self : h->layers[i].cross;
+      const int nq = b == 0 ? 3 * D : 2 * D;
+      w.Wqkv = take((size_t)nq * D);
+      w.bqkv = take(nq);
+      w.Wo = take((size_t)D * D);
+      w.bo = take(D);
+      w.W1 = take((size_t)2 * D * 2 * D);
+      w.b1 = take(2 * D);
+      w.g = take(2 * D);
+      w.be = take(2 * D);
+      w.W2 = take((size_t)D * 2 * D);
+      w.b2 = take(D);
+    }
+    h->layers[i].Wf = take((size_t)D * D);
+    h->layers[i].bf = take(D);
+    h->layers[i].wm = take(D);
+    h->layers[i].bm = take(1);
+    h->layers[i].wt = take(D);
+    h->layers[i].bt = take(1);
+  }
+  h->total = off;
+
+  // destination of each schema tensor (Wqkv weight/bias are gathered, marked by SIZE_MAX-1/-2)
+  h->dst.assign(h->schema.size(), SIZE_MAX);
+  for (size_t k = 0; k < h->schema.size(); ++k) {
+    const std::string& n = h->schema[k].name;
+    size_t o = SIZE_MAX;
+    if (n == "posenc.Wr.weight") o = h->Wr;
+    else if (n == "posenc.condition_modulation.weight") o = h->Wc;
+    else if (n == "posenc.condition_modulation.bias") o = h->bc;
+    else if (n == "input_proj.weight") o = h->Wi;
+    else if (n == "input_proj.bias") o = h->bi;
+    else {
+      int li = -1;
+      char rest[160] = {0};
+      if (sscanf(n.c_str(), "transformers.%d.%159s", &li, rest) == 2) {
+        const std::string r = rest;
+        LayerW& lw = h->layers[li];
+        const bool self = r.rfind("self_attn.", 0) == 0;
+        BlockW& w = self ? lw.self : lw.cross;
+        const std::string f = r.substr(r.find('.') + 1);
+        if (f == "Wqkv.weight" || f == "Wqkv.bias") o = SIZE_MAX - 1;  // gathered
+        else if (f == "to_qk.weight") o = w.Wqkv;
+        else if (f == "to_qk.bias") o = w.bqkv;
+        else if (f == "to_v.weight") o = w.Wqkv + (size_t)D * D;
+        else if (f == "to_v.bias") o = w.bqkv + D;
+        else if (f == "out_proj.weight" || f == "to_out.weight") o = w.Wo;
+        else if (f == "out_proj.bias" || f == "to_out.bias") o = w.bo;
+        else if (f == "ffn.0.weight") o = w.W1;
+        else if (f == "ffn.0.bias") o = w.b1;
+        else if (f == "ffn.1.weight") o = w.g;
+        else if (f == "ffn.1.bias") o = w.be;
+        else if (f == "ffn.3.weight") o = w.W2;
+        else if (f == "ffn.3.bias") o = w.b2;
+      } else if (sscanf(n.c_str(), "log_assignment.%d.%159s", &li, rest) == 2) {
+        const std::string r = rest;
+        LayerW& lw = h->layers[li];
+        if (r == "final_proj.weight") o = lw.Wf;
+        else if (r == "final_proj.bias") o = lw.bf;
+        else if (r == "matchability.weight") o = lw.wm;
+        else if (r == "matchability.bias") o = lw.bm;
+      } else if (sscanf(n.c_str(), "token_confidence.%d.%159s", &li, rest) == 2) {
+        const std::string r = rest;
+        if (r == "token.0.weight") o = h->layers[li].wt;
+        else if (r == "token.0.bias") o = h->layers[li].bt;
+      }
+    }
+    h->dst[k] = o;
+  }
+}
+
+// ------------------------------------------------------------------ forward workspace
+struct Work {
+  float *X, *X2, *cosb, *sinb, *cos2, *sin2, *size, *Q, *K, *V, *ctx, *msg, *H1, *md, *z, *tok, *sim, *aws;
+  int *flags, *pos, *ind0, *ind1, *ind0b, *ind1b, *counts;
+  int64_t *m0c, *m1c;
+  float *s0c, *s1c;
+  size_t bytes;
+};
+
+Work carve(char* base, int B, int M, int N, bool prune) {
+  const size_t R = (size_t)B * (M + N);
+  Work w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += (bytes + 255) & ~size_t(255);
+    return p;
+  };
+  auto tf = [&](size_t n) { return reinterpret_cast<float*>(take(n * sizeof(float))); };
+  auto ti = [&](size_t n) { return reinterpret_cast<int*>(take(n * sizeof(int))); };
+  w.X = tf(R * D);
+  w.cosb = tf(R * 32);
+  w.sinb = tf(R * 32);
+  w.size = tf(4 * (size_t)B);
+  w.Q = tf(R * D);
+  w.K = tf(R * D);
+  w.V = tf(R * D);
+  w.ctx = tf(R * D);
+  w.msg = tf(R * D);
+  w.H1 = tf(R * 2 * D);
+  w.md = tf(R * D);
+  w.z = tf(R);
+  w.tok = tf(R);
+  w.sim = tf((size_t)B * M * N);
+  w.aws = tf(lg::assign_workspace_floats(B, M, N));
+  if (prune) {
+    w.X2 = tf(R * D);
+    w.cos2 = tf(R * 32);
+    w.sin2 = tf(R * 32);
+    w.flags = ti(R);
+    w.pos = ti(R);
+    w.ind0 = ti(M);
+    w.ind1 = ti(N);
+    w.ind0b = ti(M);
+    w.ind1b = ti(N);
+    w.counts = ti(64);
+    w.m0c = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * M));
+    w.m1c = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * N));
+    w.s0c = tf(M);
+    w.s1c = tf(N);
+  }
+  w.bytes = off;
+  return w;
+}
+
+bool prune_enabled(const lg_config_t& c) { return c.width_confidence > 0.f || c.depth_confidence > 0.f; }
+
+lg::GemmArgs gemm_base() {
+  lg::GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.out_scale = 1.f;
+  return a;
+}
+
+float confidence_threshold(int i, int L) {  // lightglue.py:581-584
+  double t = 0.8 + 0.1 * std::exp(-4.0 * i / L);
+  return (float)std::min(1.0, std::max(0.0, t));  // compared in fp32 like torch
+}
+
+}  // namespace
+
+extern "C" {
+
+int lg_abi_version(void) { return LG_ABI_VERSION; }
+const char* lg_last_error(void) { return g_err.c_str(); }
+
+int lg_create(const lg_config_t* cfg, int device, lg_handle_t** out) {
+  if (!cfg || !out) return fail(LG_E_INVALID, "null argument");
+  if (cfg->descriptor_dim != D) return fail(LG_E_INVALID, "descriptor_dim must be 256 (kernels are specialised)");
+  if (cfg->num_heads <= 0 || cfg->descriptor_dim / cfg->num_heads != 64 || cfg->descriptor_dim % cfg->num_heads)
+    return fail(LG_E_INVALID, "head_dim must be 64 (descriptor_dim / num_heads)");
+  if (cfg->n_layers < 1) return fail(LG_E_INVALID, "n_layers must be >= 1");
+  if (cfg->input_dim <= 0 || cfg->input_dim % 32) return fail(LG_E_INVALID, "input_dim must be a positive multiple of 32");
+  LG_HIP(hipSetDevice(device));
+  lg_handle* h = new lg_handle();
+  h->cfg = *cfg;
+  h->device = device;
+  h->schema = make_schema(*cfg);
+  for (size_t k = 0; k < h->schema.size(); ++k) h->index[h->schema[k].name] = (int)k;
+  plan_layout(h);
+  for (size_t k = 0; k < h->schema.size(); ++k)
+    if (h->dst[k] == SIZE_MAX) {
+      std::string n = h->schema[k].name;
+      delete h;
+      return fail(LG_E_WEIGHTS, "internal: unplaced schema tensor " + n);
+    }
+  hipError_t e = hipMalloc(&h->wbuf, h->total * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&h->perm, 3 * D * sizeof(int));
+  if (e == hipSuccess) {
+    auto p = wqkv_perm(cfg->num_heads);
+    e = hipMemcpy(h->perm, p.data(), p.size() * sizeof(int), hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess) e = hipMemset(h->wbuf, 0, h->total * sizeof(float));
+  if (e != hipSuccess) {
+    if (h->wbuf) (void)hipFree(h->wbuf);
+    if (h->perm) (void)hipFree(h->perm);
+    delete h;
+    return fail(LG_E_HIP, std::string("allocation: ") + hipGetErrorString(e));
+  }
+  *out = h;
+  return LG_OK;
+}
+
+int lg_destroy(lg_handle_t* h) {
+  if (!h) return LG_OK;
+  (void)hipSetDevice(h->device);
+  if (h->wbuf) (void)hipFree(h->wbuf);
+  if (h->perm) (void)hipFree(h->perm);
+  for (auto& r : h->recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto e : h->pool) (void)hipEventDestroy(e);
+  delete h;
+  return LG_OK;
+}
+
+int lg_weight_count(const lg_handle_t* h) { return h ? (int)h->schema.size() : 0; }
+const char* lg_weight_name(const lg_handle_t* h, int i) {
+  return (h && i >= 0 && i < (int)h->schema.size()) ? h->schema[i].name.c_str() : nullptr;
+}
+int64_t lg_weight_numel(const lg_handle_t* h, int i) {
+  return (h && i >= 0 && i < (int)h->schema.size()) ? h->schema[i].numel() : -1;
+}
+
+int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float* const* tensors, const int64_t* numels,
+                    void* stream) {
+  if (!h || n < 0 || (n && (!names || !tensors || !numels))) return fail(LG_E_INVALID, "null argument");
+  LG_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<int> seen(h->schema.size(), 0);
+  for (int i = 0; i < n; ++i) {
+    auto it = h->index.find(names[i]);
+    if (it == h->index.end()) return fail(LG_E_WEIGHTS, std::string("unexpected key in state_dict: ") + names[i]);
+    const int k = it->second;
+    if (seen[k]++) return fail(LG_E_WEIGHTS, std::string("duplicate key: ") + names[i]);
+    if (numels[i] != h->schema[k].numel())
+      return fail(LG_E_WEIGHTS, std::string("size mismatch for ") + names[i] + ": expected " +
+                                    std::to_string(h->schema[k].numel()) + " got " + std::to_string(numels[i]));
+  }
+  for (size_t k = 0; k < h->schema.size(); ++k)
+    if (!seen[k]) return fail(LG_E_WEIGHTS, "missing key in state_dict: " + h->schema[k].name);
+  for (int i = 0; i < n; ++i) {
+    const int k = h->index[names[i]];
+    const std::string& name = h->schema[k].name;
+    if (h->dst[k] == SIZE_MAX - 1) {
+      int li = -1;
+      sscanf(name.c_str(), "transformers.%d.", &li);
+      const bool is_w = name.size() > 6 && name.compare(name.size() - 6, 6, "weight") == 0;
+      float* dst = h->wbuf + (is_w ? h->layers[li].self.Wqkv : h->layers[li].self.bqkv);
+      hipError_t e = lg::gather_rows(dst, tensors[i], h->perm, 3 * D, is_w ? D : 1, st);
+      if (e != hipSuccess) return fail(LG_E_HIP, std::string("gather Wqkv: ") + hipGetErrorString(e));
+    } else {
+      LG_HIP(hipMemcpyAsync(h->wbuf + h->dst[k], tensors[i], numels[i] * sizeof(float), hipMemcpyDeviceToDevice, st));
+    }
+  }
+  h->loaded = true;
+  return LG_OK;
+}
+
+int lg_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (!h || !bytes || B < 0 || M < 0 || N < 0) return fail(LG_E_INVALID, "bad argument");
+  *bytes = carve(nullptr, B, M, N, prune_enabled(h->cfg)).bytes;
+  return LG_OK;
+}
+
+int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* workspace, size_t workspace_bytes,
+               void* stream) {
+  using namespace lg;
+  if (!h || !in || !out) return fail(LG_E_INVALID, "null argument");
+  if (!h->loaded) return fail(LG_E_WEIGHTS, "weights not loaded");
+  const lg_config_t& c = h->cfg;
+  const int B = in->B, M0 = in->M, N0 = in->N, H = c.num_heads, L = c.n_layers;
+  if (B <= 0) return fail(LG_E_INVALID, "batch must be >= 1");
+  if (M0 <= 0 || N0 <= 0)
+    return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size (empty keypoint set)");
+  if (!in->keypoints0 || !in->keypoints1 || !in->descriptors0 || !in->descriptors1)
+    return fail(LG_E_INVALID, "missing input tensor");
+  if (c.add_scale_ori && (!in->scales0 || !in->oris0 || !in->scales1 || !in->oris1))
+    return fail(LG_E_INVALID, "add_scale_ori requires scales0/1 and oris0/1");
+  if (!out->matches0 || !out->matches1 || !out->matching_scores0 || !out->matching_scores1)
+    return fail(LG_E_INVALID, "missing output tensor");
+  const bool do_stop = c.depth_confidence > 0.f, do_prune = c.width_confidence > 0.f;
+  if ((do_stop || do_prune) && B != 1) return fail(LG_E_INVALID, "pruning / early stop require batch size 1");
+  if (do_prune && (!out->prune0 || !out->prune1)) return fail(LG_E_INVALID, "prune0/prune1 outputs required with pruning");
+  const Work need = carve(nullptr, B, M0, N0, prune_enabled(c));
+  if (!workspace || workspace_bytes < need.bytes)
+    return fail(LG_E_WORKSPACE, "workspace too small: need " + std::to_string(need.bytes));
+  LG_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  Work w = carve((char*)workspace, B, M0, N0, prune_enabled(c));
+  const float* Wb = h->wbuf;
+  int M = M0, N = N0;
+  // launch wrappers that feed lg_profile_* (algorithmic flops / bytes per launch)
+  auto gemm = [&](const GemmArgs& g, int epi, int batch) -> hipError_t {
+    const int p = h->prof_begin(LG_KERNEL_GEMM, st);
+    const hipError_t e = gemm_f32(g, epi, batch, st);
+    const double R = g.R, K = g.K, O = g.Nout;
+    h->prof_end(p, 2.0 * R * K * O * batch, 4.0 * (R * K + O * K + R * O) * batch, st);
+    return e;
+  };
+  auto attn = [&](const AttnSet& a0, const AttnSet& a1, float scale, bool cross) -> hipError_t {
+    const int p = h->prof_begin(LG_KERNEL_ATTENTION, st);
+    const hipError_t e = attention_f32(a0, a1, B, H, scale, st);
+    // self: 2 matmuls per image (QK^T, PV); cross: one shared sim + two PV (lightglue.py:236-242)
+    const double hd = 64.0 * H * B;
+    const double fl = cross ? 6.0 * a0.Nq * a0.Nk * hd : 4.0 * hd * ((double)a0.Nq * a0.Nk + (double)a1.Nq * a1.Nk);
+    const double by = 4.0 * 256.0 * B * 4.0 * (a0.Nq + a1.Nq);  // q, k, v read + o written, per row
+    h->prof_end(p, fl, by, st);
+    return e;
+  };
+  auto assign = [&](const AssignArgs& a) -> hipError_t {
+    const int p = h->prof_begin(LG_KERNEL_ASSIGN, st);
+    const hipError_t e = assign_and_filter(a, st);
+    const double mn = (double)a.B * a.M * a.N;
+    h->prof_end(p, 0.0, 4.0 * (mn + (a.la ? (double)a.B * (a.M + 1) * (a.N + 1) : 0.0)), st);
+    return e;
+  };
+
+  // ---- input projection (lightglue.py:370-373,486-487)
+  if (c.input_dim != D) {
+    GemmArgs g = gemm_base();
+    g.W = Wb + h->Wi; g.ldw = c.input_dim; g.K = c.input_dim; g.K0 = c.input_dim;
+    g.bias = Wb + h->bi; g.ldy = D; g.Nout = D;
+    g.A0 = in->descriptors0; g.lda0 = c.input_dim; g.R = B * M; g.Y = w.X;
+    LG_HIP(gemm(g, EPI_STORE, 1));
+    g.A0 = in->descriptors1; g.R = B * N; g.Y = w.X + (size_t)B * M * D;
+    LG_HIP(gemm(g, EPI_STORE, 1));
+  } else {
+    LG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
+    LG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
+  }
+
+  // ---- keypoint normalisation + positional encoding (lightglue.py:455-456,490-494)
+  {
+    const float* s0 = in->image_size0;
+    const float* s1 = in->image_size1;
+    if (!s0) { LG_HIP(kpt_extent(in->keypoints0, B, M, w.size, st)); s0 = w.size; }
+    if (!s1) { LG_HIP(kpt_extent(in->keypoints1, B, N, w.size + 2 * B, st)); s1 = w.size + 2 * B; }
+    PEArgs p;
+    p.Wr = Wb + h->Wr; p.Wc = Wb + h->Wc; p.bc = Wb + h->bc; p.m_in = c.add_scale_ori ? 4 : 2; p.B = B;
+    p.kpts = in->keypoints0; p.size = s0; p.scales = in->scales0; p.oris = in->oris0; p.n = M;
+    p.cosb = w.cosb; p.sinb = w.sinb;
+    LG_HIP(positional_encoding(p, st));
+    p.kpts = in->keypoints1; p.size = s1; p.scales = in->scales1; p.oris = in->oris1; p.n = N;
+    p.cosb = w.cosb + (size_t)B * M * 32; p.sinb = w.sinb + (size_t)B * M * 32;
+    LG_HIP(positional_encoding(p, st));
+  }
+
+  if (do_prune) {
+    LG_HIP(iota_fill(w.ind0, M, st));
+    LG_HIP(iota_fill(w.ind1, N, st));
+  }
+  if (out->prune0) LG_HIP(fill_i64(out->prune0, do_prune ? 1 : L, (size_t)B * M0, st));
+  if (out->prune1) LG_HIP(fill_i64(out->prune1, do_prune ? 1 : L, (size_t)B * N0, st));
+
+  const float thr_w = (float)(1.0 - c.width_confidence);  // python-float arithmetic, then fp32 compare
+  int stop = L - 1;
+  for (int i = 0; i < L; ++i) {
+    const LayerW& lw = h->layers[i];
+    const int R = B * (M + N);
+    for (int blk = 0; blk < 2; ++blk) {
+      const BlockW& bw = blk == 0 ? lw.self : lw.cross;
+      // QKV projection with fused rotary (self) / scale (cross) and head-major scatter
+      GemmArgs g = gemm_base();
+      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wqkv; g.ldw = D; g.bias = Wb + bw.bqkv;
+      g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D;
+      g.hl.B = B; g.hl.H = H; g.hl.M = M; g.hl.N = N; g.hl.cosb = w.cosb; g.hl.sinb = w.sinb;
+      g.hl.q = w.Q; g.hl.k = w.K; g.hl.v = w.V;
+      g.hl.qk_scale = std::sqrt(1.f / std::sqrt(64.f));  // scale**0.5 (lightglue.py:235)
+      LG_HIP(gemm(g, blk == 0 ? EPI_QKV_ROT : EPI_CROSS_QKV, 1));
+      const size_t img1 = (size_t)B * H * M * 64;
+      AttnSet a0, a1;
+      if (blk == 0) {  // self: q/k/v of the same image, scale 1/sqrt(64) (SDPA default)
+        a0 = {w.Q, w.K, w.V, w.ctx, M, M};
+        a1 = {w.Q + img1, w.K + img1, w.V + img1, w.ctx + (size_t)B * M * D, N, N};
+        LG_HIP(attn(a0, a1, 0.125f, false));
+      } else {  // cross: QK in w.Q, V in w.K (t=1 of the 512-wide GEMM)
+        a0 = {w.Q, w.Q + img1, w.K + img1, w.ctx, M, N};
+        a1 = {w.Q + img1, w.Q, w.K, w.ctx + (size_t)B * M * D, N, M};
+        LG_HIP(attn(a0, a1, 1.0f, true));
+      }
+      // out projection
+      g = gemm_base();
+      g.A0 = w.ctx; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wo; g.ldw = D; g.bias = Wb + bw.bo;
+      g.R = R; g.Nout = D; g.Y = w.msg; g.ldy = D;
+      LG_HIP(gemm(g, EPI_STORE, 1));
+      // FFN: Linear(cat[x, msg]) -> LN -> GELU -> Linear + residual
+      g = gemm_base();
+      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.A1 = w.msg; g.lda1 = D; g.K = 2 * D;
+      g.W = Wb + bw.W1; g.ldw = 2 * D; g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
+      LG_HIP(gemm(g, EPI_STORE, 1));
+      LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, st));
+      g = gemm_base();
+      g.A0 = w.H1; g.lda0 = 2 * D; g.K0 = 2 * D; g.K = 2 * D; g.W = Wb + bw.W2; g.ldw = 2 * D; g.bias = Wb + bw.b2;
+      g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
+      LG_HIP(gemm(g, EPI_STORE, 1));
+    }
+    if (i == L - 1) break;
+
+    // ---- early stop (lightglue.py:527-531, check_if_stop :595-606; thresholds per :581-584)
+    const float thr_c = confidence_threshold(i, L);
+    if (do_stop) {
+      LG_HIP(gemv_256(w.X, Wb + lw.wt, Wb + lw.bt, w.tok, R, 1, st));
+      LG_HIP(hipMemsetAsync(w.counts, 0, sizeof(int), st));
+      LG_HIP(count_below(w.tok, thr_c, R, w.counts, st));
+      int below = 0;
+      LG_HIP(hipMemcpyAsync(&below, w.counts, sizeof(int), hipMemcpyDeviceToHost, st));
+      LG_HIP(hipStreamSynchronize(st));
+      const float ratio = 1.0f - (float)below / (float)(M0 + N0);
+      if (ratio > (float)c.depth_confidence) {
+        stop = i;
+        break;
+      }
+    }
+    // ---- width pruning (lightglue.py:532-547, get_pruning_mask :586-593)
+    if (do_prune) {
+      LG_HIP(gemv_256(w.X, Wb + lw.wm, Wb + lw.bm, w.z, R, 0, st));
+      LG_HIP(prune_flags(w.z, do_stop ? w.tok : nullptr, thr_w, thr_c, R, w.flags, st));
+      LG_HIP(compact_scan(w.flags, M, w.pos, w.counts + 1, st));
+      LG_HIP(compact_scan(w.flags + M, N, w.pos + M, w.counts + 2, st));
+      LG_HIP(compact_rows(w.X, w.X2, w.flags, w.pos, M, D, st));
+      LG_HIP(compact_rows(w.cosb, w.cos2, w.flags, w.pos, M, 32, st));
+      LG_HIP(compact_rows(w.sinb, w.sin2, w.flags, w.pos, M, 32, st));
+      LG_HIP(compact_index(w.ind0, w.ind0b, out->prune0 ? out->prune0 : nullptr, w.flags, w.pos, M, st));
+      int cnt[2] = {0, 0};
+      LG_HIP(hipMemcpyAsync(cnt, w.counts + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      LG_HIP(hipStreamSynchronize(st));
+      const int M2 = cnt[0], N2 = cnt[1];
+      // image-1 rows land right after the M2 kept image-0 rows
+      LG_HIP(compact_rows(w.X + (size_t)M * D, w.X2 + (size_t)M2 * D, w.flags + M, w.pos + M, N, D, st));
+      LG_HIP(compact_rows(w.cosb + (size_t)M * 32, w.cos2 + (size_t)M2 * 32, w.flags + M, w.pos + M, N, 32, st));
+      LG_HIP(compact_rows(w.sinb + (size_t)M * 32, w.sin2 + (size_t)M2 * 32, w.flags + M, w.pos + M, N, 32, st));
+      LG_HIP(compact_index(w.ind1, w.ind1b, out->prune1 ? out->prune1 : nullptr, w.flags + M, w.pos + M, N, st));
+      std::swap(w.X, w.X2);
+      std::swap(w.cosb, w.cos2);
+      std::swap(w.sinb, w.sin2);
+      std::swap(w.ind0, w.ind0b);
+      std::swap(w.ind1, w.ind1b);
+      M = M2;
+      N = N2;
+      if (M == 0 || N == 0)
+        return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size (all keypoints pruned)");
+    }
+  }
+  out->stop_layer = stop;
+  out->kept0 = M;
+  out->kept1 = N;
+
+  // ---- assignment head of the last executed layer (lightglue.py:549-551, MatchAssignment :306-315)
+  const LayerW& la = h->layers[stop];
+  const int R = B * (M + N);
+  {
+    GemmArgs g = gemm_base();
+    g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + la.Wf; g.ldw = D; g.bias = Wb + la.bf;
+    g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
+    LG_HIP(gemm(g, EPI_STORE, 1));
+    LG_HIP(gemv_256(w.X, Wb + la.wm, Wb + la.bm, w.z, R, 0, st));
+    g = gemm_base();
+    g.A0 = w.md; g.lda0 = D; g.K0 = D; g.K = D; g.sA = (long long)M * D;
+    g.W = w.md + (size_t)B * M * D; g.ldw = D; g.sW = (long long)N * D;
+    g.R = M; g.Nout = N; g.Y = w.sim; g.ldy = N; g.sY = (long long)M * N;
+    LG_HIP(gemm(g, EPI_STORE, B));
+  }
+  AssignArgs aa;
+  aa.sim = w.sim; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = out->log_assignment; aa.ws = w.aws;
+  aa.B = B; aa.M = M; aa.N = N; aa.th = (float)c.filter_threshold;
+  if (do_prune) {
+    aa.m0 = w.m0c; aa.m1 = w.m1c; aa.s0 = w.s0c; aa.s1 = w.s1c;
+    LG_HIP(assign(aa));
+    LG_HIP(remap_matches(w.m0c, w.m1c, w.s0c, w.s1c, w.ind0, w.ind1, M, N, out->matches0, out->matches1,
+                         out->matching_scores0, out->matching_scores1, M0, N0, st));
+  } else {
+    aa.m0 = out->matches0; aa.m1 = out->matches1; aa.s0 = out->matching_scores0; aa.s1 = out->matching_scores1;
+    LG_HIP(assign(aa));
+  }
+  if (out->ref_descriptors0)
+    LG_HIP(hipMemcpyAsync(out->ref_descriptors0, w.X, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
+  if (out->ref_descriptors1)
+    LG_HIP(hipMemcpyAsync(out->ref_descriptors1, w.X + (size_t)B * M * D, sizeof(float) * B * N * D,
+                          hipMemcpyDeviceToDevice, st));
+  return LG_OK;
+}
+
+int lg_profile_enable(lg_handle_t* h, int enable) {
+  if (!h) return fail(LG_E_INVALID, "null handle");
+  for (auto& r : h->recs) {
+    h->pool.push_back(r.a);
+    h->pool.push_back(r.b);
+  }
+  h->recs.clear();
+  h->prof_on = enable != 0;
+  return LG_OK;
+}
+
+int lg_profile_read(lg_handle_t* h, int kernel, double* total_ms, int64_t* launches, double* flops, double* bytes) {
+  if (!h || kernel < 0 || kernel >= LG_KERNEL_COUNT) return fail(LG_E_INVALID, "bad argument");
+  double ms = 0.0, fl = 0.0, by = 0.0;
+  int64_t n = 0;
+  for (auto& r : h->recs) {
+    if (r.kind != kernel) continue;
+    LG_HIP(hipEventSynchronize(r.b));
+    float t = 0.f;
+    LG_HIP(hipEventElapsedTime(&t, r.a, r.b));
+    ms += t;
+    fl += r.flops;
+    by += r.bytes;
+    ++n;
+  }
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = n;
+  if (flops) *flops = fl;
+  if (bytes) *bytes = by;
+  return LG_OK;
+}
+
+int lg_filter_workspace_bytes(int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (!bytes) return fail(LG_E_INVALID, "null argument");
+  *bytes = lg::filter_workspace_floats(B, M, N) * sizeof(float);
+  return LG_OK;
+}
+
+int lg_filter_matches(const float* scores, int32_t B, int32_t M, int32_t N, double threshold, int64_t* m0, int64_t* m1,
+                      float* s0, float* s1, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!scores || !m0 || !m1 || !s0 || !s1) return fail(LG_E_INVALID, "null argument");
+  if (B <= 0 || M <= 0 || N <= 0) return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size");
+  if (!workspace || workspace_bytes < lg::filter_workspace_floats(B, M, N) * sizeof(float))
+    return fail(LG_E_WORKSPACE, "workspace too small");
+  LG_HIP(lg::filter_from_scores(scores, B, M, N, (float)threshold, (float*)workspace, m0, m1, s0, s1, (hipStream_t)stream));
+  return LG_OK;
+}
+
+int lg_sinkhorn_workspace_bytes(int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (!bytes) return fail(LG_E_INVALID, "null argument");
+  *bytes = lg::sinkhorn_workspace_floats(B, M, N) * sizeof(float);
+  return LG_OK;
+}
+
+int lg_log_optimal_transport(const float* scores, float alpha, int32_t B, int32_t M, int32_t N, int32_t iters, float* Z,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  if (!scores || !Z) return fail(LG_E_INVALID, "null argument");
+  if (B < 0 || M < 0 || N < 0 || iters < 0) return fail(LG_E_INVALID, "bad shape");
+  if (!workspace || workspace_bytes < lg::sinkhorn_workspace_floats(B, M, N) * sizeof(float))
+    return fail(LG_E_WORKSPACE, "workspace too small");
+  LG_HIP(lg::log_optimal_transport(scores, alpha, B, M, N, iters, Z, (float*)workspace, (hipStream_t)stream));
+  return LG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,321 @@
+"""Drop-in for ``gluefactory.models.matchers.lightglue.LightGlue`` (reference lightglue.py:340-666).
+
+Same constructor config keys (``default_conf``, :341-361), same parameter names / state-dict
+schema (so reference checkpoints load unchanged, including the old ``self_attn.{i}`` key renames,
+:423-430), same ``forward(data) -> dict`` contract (:444-579).  The modules below are parameter
+containers only: the whole eval forward runs in ``liblightglue_mi355x.so`` (hand-written gfx950
+HIP kernels) through the C-ABI in ``include/lightglue_mi355x.h``.  There is no PyTorch compute
+fallback; a CPU input or a missing library raises.
+
+Deliberate behaviour differences from the reference:
+* early stop uses ``[confidence_threshold(i) for i in range(L)]`` (the reference reads an
+  undefined attribute, :592,604) and returns the stopping layer's descriptors (the reference
+  crashes in ``torch.stack([])``, :572);
+* without ``view*['image_size']`` the keypoints are normalised by their extent (:25-26) instead of
+  raising ``UnboundLocalError`` (:452-455);
+* ``ref_descriptors*`` is ``[B, 1, M', 256]`` (final layer only, as the reference's eval path).
+"""
+import ctypes
+import warnings
+from pathlib import Path
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from .weights import DEFAULT_CONF
+
+DATA_PATH = Path(__file__).resolve().parent.parent / "data"
+
+
+class AttrDict(dict):
+    """Minimal stand-in for the OmegaConf DictConfig the reference uses for ``self.conf``."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def merge_conf(*cfgs):
+    out = AttrDict()
+    for c in cfgs:
+        for k, v in dict(c or {}).items():
+            if isinstance(v, dict):
+                prev = out.get(k)
+                out[k] = merge_conf(prev if isinstance(prev, dict) else {}, v)
+            else:
+                out[k] = v
+    return out
+
+
+# ---------------------------------------------------------------- parameter containers
+class _PosEnc(nn.Module):  # lightglue.py:50-61
+    def __init__(self, m_in, f_dim, gamma=1.0):
+        super().__init__()
+        self.Wr = nn.Linear(m_in, f_dim // 2, bias=False)
+        nn.init.normal_(self.Wr.weight.data, mean=0, std=gamma**-2)
+        self.condition_modulation = nn.Linear(1, f_dim // 2)
+
+
+def _ffn(d):
+    return nn.Sequential(nn.Linear(2 * d, 2 * d), nn.LayerNorm(2 * d, elementwise_affine=True), nn.GELU(), nn.Linear(2 * d, d))
+
+
+class _SelfBlock(nn.Module):  # lightglue.py:159-176
+    def __init__(self, d):
+        super().__init__()
+        self.Wqkv = nn.Linear(d, 3 * d)
+        self.out_proj = nn.Linear(d, d)
+        self.ffn = _ffn(d)
+
+
+class _CrossBlock(nn.Module):  # lightglue.py:194-211
+    def __init__(self, d):
+        super().__init__()
+        self.to_qk = nn.Linear(d, d)
+        self.to_v = nn.Linear(d, d)
+        self.to_out = nn.Linear(d, d)
+        self.ffn = _ffn(d)
+
+
+class _Layer(nn.Module):  # lightglue.py:252-256
+    def __init__(self, d):
+        super().__init__()
+        self.self_attn = _SelfBlock(d)
+        self.cross_attn = _CrossBlock(d)
+
+
+class _MatchAssignment(nn.Module):  # lightglue.py:299-304
+    def __init__(self, d):
+        super().__init__()
+        self.matchability = nn.Linear(d, 1, bias=True)
+        self.final_proj = nn.Linear(d, d, bias=True)
+
+
+class _TokenConfidence(nn.Module):  # lightglue.py:96-99
+    def __init__(self, d):
+        super().__init__()
+        self.token = nn.Sequential(nn.Linear(d, 1), nn.Sigmoid())
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class LightGlue(nn.Module):
+    default_conf = DEFAULT_CONF
+    required_data_keys = ["keypoints0", "keypoints1", "descriptors0", "descriptors1"]
+    url = "https://github.com/cvg/LightGlue/releases/download/{}/{}_lightglue.pth"
+
+    def __init__(self, conf) -> None:
+        super().__init__()
+        self.conf = conf = merge_conf(self.default_conf, conf)
+        d, h, n = int(conf.descriptor_dim), int(conf.num_heads), int(conf.n_layers)
+        if conf.input_dim != conf.descriptor_dim:
+            self.input_proj = nn.Linear(conf.input_dim, d, bias=True)
+        else:
+            self.input_proj = nn.Identity()
+        self.posenc = _PosEnc(2 + 2 * int(bool(conf.add_scale_ori)), d // h)
+        self.transformers = nn.ModuleList([_Layer(d) for _ in range(n)])
+        self.log_assignment = nn.ModuleList([_MatchAssignment(d) for _ in range(n)])
+        self.token_confidence = nn.ModuleList([_TokenConfidence(d) for _ in range(n - 1)])
+        self._handle = None
+        self._handle_device = None
+        self._weights_key = None
+        self._ws = None
+
+        state_dict = None
+        if conf.weights is not None:  # lightglue.py:402-421
+            if Path(conf.weights).exists():
+                state_dict = torch.load(conf.weights, map_location="cpu", weights_only=True)
+            elif (DATA_PATH / conf.weights).exists():
+                state_dict = torch.load(str(DATA_PATH / conf.weights), map_location="cpu", weights_only=True)
+            else:
+                fname = f"{conf.weights}_{conf.weights_from_version}".replace(".", "-") + ".pth"
+                state_dict = torch.hub.load_state_dict_from_url(
+                    self.url.format(conf.weights_from_version, conf.weights), file_name=fname
+                )
+        if state_dict:
+            for i in range(n):  # lightglue.py:424-429
+                pattern = f"self_attn.{i}", f"transformers.{i}.self_attn"
+                state_dict = {k.replace(*pattern): v for k, v in state_dict.items()}
+                pattern = f"cross_attn.{i}", f"transformers.{i}.cross_attn"
+                state_dict = {k.replace(*pattern): v for k, v in state_dict.items()}
+            self.load_state_dict(state_dict, strict=False)
+
+    # ------------------------------------------------------------ reference helpers
+    def confidence_threshold(self, layer_index: int) -> float:
+        """lightglue.py:581-584."""
+        threshold = 0.8 + 0.1 * np.exp(-4.0 * layer_index / self.conf.n_layers)
+        return np.clip(threshold, 0, 1)
+
+    @property
+    def confidence_thresholds(self):
+        return [self.confidence_threshold(i) for i in range(self.conf.n_layers)]
+
+    def compile(self, mode="reduce-overhead"):
+        """The reference torch.compile()s the layers (:432-442); the HIP path needs no tracing."""
+        warnings.warn("lightglue_amd: compile() is a no-op (the forward is native HIP)", stacklevel=2)
+
+    # ------------------------------------------------------------ native handle
+    def _lib_config(self):
+        c = self.conf
+        return _lib.LGConfig(
+            int(c.input_dim),
+            int(c.descriptor_dim),
+            int(c.n_layers),
+            int(c.num_heads),
+            int(bool(c.add_scale_ori)),
+            float(c.depth_confidence),
+            float(c.width_confidence),
+            float(c.filter_threshold),
+        )
+
+    def _ensure_handle(self, device):
+        lib = _lib.load()
+        cfg = self._lib_config()
+        cfg_key = tuple(getattr(cfg, f) for f, _ in _lib.LGConfig._fields_)
+        if self._handle is not None and (self._handle_device != device or self._cfg_key != cfg_key):
+            lib.lg_destroy(self._handle)
+            self._handle = None
+        if self._handle is None:
+            h = ctypes.c_void_p()
+            _lib.check(lib.lg_create(ctypes.byref(cfg), device.index or 0, ctypes.byref(h)), "lg_create")
+            self._handle, self._handle_device, self._cfg_key = h, device, cfg_key
+            self._weights_key = None
+        sd = self.state_dict(keep_vars=True)
+        names = [n for n in sd]
+        key = tuple((n, sd[n].data_ptr(), sd[n]._version) for n in names)
+        if key != self._weights_key:
+            ts = []
+            for n in names:
+                t = sd[n].detach()
+                if t.device != device or t.dtype != torch.float32:
+                    raise RuntimeError(
+                        f"lightglue_amd: parameter {n} is {t.dtype} on {t.device}; move the module to {device} in fp32"
+                    )
+                ts.append(t.contiguous())
+            arr_n = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+            arr_p = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+            arr_k = (ctypes.c_int64 * len(ts))(*[t.numel() for t in ts])
+            stream = torch.cuda.current_stream(device).cuda_stream
+            _lib.check(lib.lg_load_weights(self._handle, len(ts), arr_n, arr_p, arr_k, ctypes.c_void_p(stream)), "lg_load_weights")
+            torch.cuda.current_stream(device).synchronize()  # sources may be temporaries
+            self._weights_key = key
+        return lib
+
+    def __del__(self):
+        try:
+            if self._handle is not None and _lib._lib is not None:
+                _lib._lib.lg_destroy(self._handle)
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ forward
+    def forward(self, data: dict) -> dict:
+        for key in self.required_data_keys:  # lightglue.py:445-446
+            assert key in data, f"Missing key {key} in data"
+        kpts0, kpts1 = data["keypoints0"], data["keypoints1"]
+        device = kpts0.device
+        if device.type != "cuda":
+            raise RuntimeError("lightglue_amd: inputs must be on a HIP (cuda) device; there is no CPU path")
+        b, m, _ = kpts0.shape
+        _, n, _ = kpts1.shape
+        c = self.conf
+        desc0, desc1 = data["descriptors0"], data["descriptors1"]
+        assert desc0.shape[-1] == c.input_dim  # :481-482
+        assert desc1.shape[-1] == c.input_dim
+        size0 = size1 = None
+        if "view0" in data and "view1" in data:  # :452-454
+            size0 = data["view0"].get("image_size")
+            size1 = data["view1"].get("image_size")
+
+        def f32(t):
+            return None if t is None else torch.as_tensor(t, device=device).to(torch.float32).contiguous()
+
+        def per_point(t):  # scales/oris may be [B,N] or [B,N,1] (:464-465)
+            t = f32(t)
+            return t.reshape(t.shape[0], t.shape[1]) if t is not None else None
+
+        k0, k1, d0, d1 = f32(kpts0), f32(kpts1), f32(desc0), f32(desc1)
+        s0 = f32(size0).reshape(b, 2) if size0 is not None else None
+        s1 = f32(size1).reshape(b, 2) if size1 is not None else None
+        sc0 = o0 = sc1 = o1 = None
+        if c.add_scale_ori:
+            sc0, o0 = per_point(data["scales0"]), per_point(data["oris0"])
+            sc1, o1 = per_point(data["scales1"]), per_point(data["oris1"])
+
+        lib = self._ensure_handle(device)
+        pruning = c.width_confidence > 0 or c.depth_confidence > 0
+        if pruning and b != 1:
+            raise AssertionError("pruning / early stop require batch size 1")  # :528,533
+        L = int(c.n_layers)
+        m0 = torch.empty((b, m), dtype=torch.int64, device=device)
+        m1 = torch.empty((b, n), dtype=torch.int64, device=device)
+        ms0 = torch.empty((b, m), dtype=torch.float32, device=device)
+        ms1 = torch.empty((b, n), dtype=torch.float32, device=device)
+        la = torch.empty((b, m + 1, n + 1), dtype=torch.float32, device=device)
+        rd0 = torch.empty((b, m, 256), dtype=torch.float32, device=device)
+        rd1 = torch.empty((b, n, 256), dtype=torch.float32, device=device)
+        p0 = torch.empty((b, m), dtype=torch.int64, device=device)
+        p1 = torch.empty((b, n), dtype=torch.int64, device=device)
+
+        ws_bytes = ctypes.c_size_t()
+        _lib.check(lib.lg_workspace_bytes(self._handle, b, m, n, ctypes.byref(ws_bytes)), "lg_workspace_bytes")
+        if self._ws is None or self._ws.numel() < ws_bytes.value or self._ws.device != device:
+            self._ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=device)
+        inp = _lib.LGInputs(b, m, n, *[_ptr(t) for t in (k0, k1, d0, d1, s0, s1, sc0, o0, sc1, o1)])
+        out = _lib.LGOutputs(*[_ptr(t) for t in (m0, m1, ms0, ms1, la, rd0, rd1, p0, p1)], 0, 0, 0)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        _lib.check(
+            lib.lg_forward(self._handle, ctypes.byref(inp), ctypes.byref(out), _ptr(self._ws), ws_bytes.value, ctypes.c_void_p(stream)),
+            "lg_forward",
+        )
+        kept0, kept1 = out.kept0, out.kept1
+        if kept0 != m or kept1 != n:  # log_assignment was written for the kept points
+            la = la.view(-1)[: b * (kept0 + 1) * (kept1 + 1)].view(b, kept0 + 1, kept1 + 1)
+        if c.width_confidence > 0:
+            prune0, prune1 = p0, p1
+        else:
+            prune0 = torch.full((b, m), float(L), device=device)
+            prune1 = torch.full((b, n), float(L), device=device)
+        return {
+            "matches0": m0,
+            "matches1": m1,
+            "matching_scores0": ms0,
+            "matching_scores1": ms1,
+            "ref_descriptors0": rd0[:, None, :kept0],
+            "ref_descriptors1": rd1[:, None, :kept1],
+            "log_assignment": la,
+            "prune0": prune0,
+            "prune1": prune1,
+            "stop_layer": out.stop_layer,
+        }
+
+    # ------------------------------------------------------------ profiling (bench.py)
+    def profile_enable(self, enable=True):
+        if self._handle is None:
+            raise RuntimeError("run one forward first (the native handle is created lazily)")
+        _lib.check(_lib.load().lg_profile_enable(self._handle, int(enable)), "lg_profile_enable")
+
+    def profile_read(self, kernel):
+        """(total_ms, launches, algorithmic_flops, algorithmic_bytes) since profile_enable()."""
+        ms, n, fl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        _lib.check(
+            _lib.load().lg_profile_read(self._handle, _lib.KERNEL_IDS[kernel], ctypes.byref(ms), ctypes.byref(n),
+                                        ctypes.byref(fl), ctypes.byref(by)),
+            "lg_profile_read",
+        )
+        return ms.value, n.value, fl.value, by.value
+
+    def loss(self, pred, data):
+        raise NotImplementedError("training is out of scope for the MI355X matcher (SURVEY.md §2)")
+
+
+__main_model__ = LightGlue

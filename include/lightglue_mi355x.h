@@ -1,0 +1,143 @@
+/*
+ * lightglue_mi355x.h — C-ABI of the MI355X-native LightGlue matcher (gfx950 HIP kernels).
+ *
+ * The reference exposes this path as a Python plugin, not an FFI:
+ *   gluefactory/models/matchers/lightglue.py:340-666  class LightGlue(nn.Module)
+ *     __init__(conf)            :367-430  -> lg_create + lg_load_weights
+ *     forward(data) -> dict     :444-579  -> lg_workspace_bytes + lg_forward
+ *     filter_matches(scores,th) :321-337  -> lg_filter_matches
+ *   gluefactory_nonfree/superglue.py:181-201 log_optimal_transport(scores, alpha, iters)
+ *                                         -> lg_log_optimal_transport
+ * The binding a maintainer adds on the reference side is in INTEGRATION.md (ctypes).
+ *
+ * Conventions
+ *   - Every pointer argument marked "device" is caller-allocated HIP device memory on the
+ *     handle's device (torch CUDA tensors on ROCm); the library never frees caller memory.
+ *   - All device work is stream-ordered on `stream` (a hipStream_t; NULL = default stream).
+ *     lg_forward synchronises the stream only when pruning / early stop is enabled (the kept
+ *     point counts decide launch sizes, as the reference's torch.where does).
+ *   - Functions return 0 on success and a negative LG_E* code on failure; lg_last_error()
+ *     returns a thread-local message for the last failure on the calling thread.
+ *   - A handle belongs to one device; it is not re-entrant (one forward at a time), separate
+ *     handles are independent.
+ *   - fp32 everywhere; indices int64 (torch.long), -1 = unmatched (lightglue.py:335-336).
+ */
+#ifndef LIGHTGLUE_MI355X_H
+#define LIGHTGLUE_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LG_ABI_VERSION 1
+
+enum {
+  LG_OK = 0,
+  LG_E_INVALID = -1,  /* bad argument / shape (reference: assert, lightglue.py:446,481-482,528) */
+  LG_E_HIP = -2,      /* HIP runtime error */
+  LG_E_WEIGHTS = -3,  /* missing / mis-shaped weight tensor */
+  LG_E_WORKSPACE = -4 /* workspace too small */
+};
+
+typedef struct lg_handle lg_handle_t;
+
+/* Mirrors LightGlue.default_conf (lightglue.py:341-361); training-only keys are host-side. */
+typedef struct {
+  int32_t input_dim;        /* 256 */
+  int32_t descriptor_dim;   /* 256 (the kernels are specialised for 256) */
+  int32_t n_layers;         /* 9 */
+  int32_t num_heads;        /* 4 (head_dim must be 64) */
+  int32_t add_scale_ori;    /* 0/1: positional input is (x,y) or (x,y,scale,ori) */
+  double depth_confidence;  /* early stop; <= 0 disables (lightglue.py:502) */
+  double width_confidence;  /* point pruning; <= 0 disables (lightglue.py:503) */
+  double filter_threshold;  /* match threshold, strict '>' (lightglue.py:333) */
+  /* doubles: the reference keeps these as Python floats and derives thresholds in double
+   * (e.g. 1 - width_confidence, :590) before the fp32 comparison. */
+} lg_config_t;
+
+typedef struct {
+  int32_t B, M, N;              /* pairs, keypoints in image 0 / image 1 */
+  const float* keypoints0;      /* device [B,M,2] pixels (x,y) */
+  const float* keypoints1;      /* device [B,N,2] */
+  const float* descriptors0;    /* device [B,M,input_dim] */
+  const float* descriptors1;    /* device [B,N,input_dim] */
+  const float* image_size0;     /* device [B,2] (w,h) or NULL -> min/max fallback (lightglue.py:25-26) */
+  const float* image_size1;     /* device [B,2] or NULL */
+  const float* scales0;         /* device [B,M] when add_scale_ori, else NULL */
+  const float* oris0;           /* device [B,M] */
+  const float* scales1;         /* device [B,N] */
+  const float* oris1;           /* device [B,N] */
+} lg_inputs_t;
+
+typedef struct {
+  int64_t* matches0;            /* device [B,M]  (required) */
+  int64_t* matches1;            /* device [B,N]  (required) */
+  float* matching_scores0;      /* device [B,M]  (required) */
+  float* matching_scores1;      /* device [B,N]  (required) */
+  float* log_assignment;        /* device [B,M'+1,N'+1] or NULL (M',N' = kept counts) */
+  float* ref_descriptors0;      /* device [B,M,256] or NULL: final descriptors (first M' rows valid) */
+  float* ref_descriptors1;      /* device [B,N,256] or NULL */
+  int64_t* prune0;              /* device [B,M] or NULL: layer count per point (lightglue.py:511,540,564) */
+  int64_t* prune1;              /* device [B,N] or NULL */
+  int32_t stop_layer;           /* host out: index of the last executed layer */
+  int32_t kept0, kept1;         /* host out: M', N' after width pruning (= M, N without) */
+} lg_outputs_t;
+
+int lg_abi_version(void);
+const char* lg_last_error(void);
+
+int lg_create(const lg_config_t* cfg, int device, lg_handle_t** out);
+int lg_destroy(lg_handle_t* h);
+
+/* Number of tensors / name / numel of the expected state dict (reference key schema,
+ * lightglue.py:367-398; old 'self_attn.{i}' names are renamed host-side, :425-429). */
+int lg_weight_count(const lg_handle_t* h);
+const char* lg_weight_name(const lg_handle_t* h, int index);
+int64_t lg_weight_numel(const lg_handle_t* h, int index);
+
+/* Copies + repacks weights from caller device buffers (fp32, contiguous, PyTorch layouts) into
+ * the handle's kernel layouts.  `names[i]` must be a schema name; every schema tensor must be
+ * present exactly once (strict load).  Stream-ordered; the sources may be freed after the
+ * stream reaches this point. */
+int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float* const* tensors,
+                    const int64_t* numels, void* stream);
+
+/* Device scratch needed by lg_forward for this shape (bytes, 256-B aligned pieces). */
+int lg_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+
+/* LightGlue.forward (lightglue.py:444-579), eval mode.  Pruning / early stop need B == 1
+ * (lightglue.py:528,533). */
+int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* workspace,
+               size_t workspace_bytes, void* stream);
+
+/* In-library kernel timing (no reference counterpart; the reference times whole forwards with
+ * CUDA events, gluefactory/utils/benchmark.py:7-33).  While enabled, lg_forward brackets every
+ * launch of the profiled kernel families with hipEvents on the forward's stream and accumulates
+ * the ALGORITHMIC flops / bytes of each launch.  lg_profile_read synchronises on the recorded
+ * events and returns totals since the last lg_profile_enable(h, 1). */
+enum { LG_KERNEL_ATTENTION = 0, LG_KERNEL_GEMM = 1, LG_KERNEL_ASSIGN = 2, LG_KERNEL_COUNT = 3 };
+int lg_profile_enable(lg_handle_t* h, int enable);
+int lg_profile_read(lg_handle_t* h, int kernel, double* total_ms, int64_t* launches, double* flops,
+                    double* bytes);
+
+/* filter_matches (lightglue.py:321-337 == superglue.py:288-298) on a [B,M+1,N+1] log
+ * assignment.  Workspace: lg_filter_workspace_bytes. */
+int lg_filter_workspace_bytes(int32_t B, int32_t M, int32_t N, size_t* bytes);
+int lg_filter_matches(const float* scores, int32_t B, int32_t M, int32_t N, double threshold,
+                      int64_t* matches0, int64_t* matches1, float* scores0, float* scores1,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* log_optimal_transport (superglue.py:181-201): Z [B,M+1,N+1] = log-domain Sinkhorn of
+ * `scores` [B,M,N] with a dustbin of score `alpha`, `iters` iterations, multiplied by M+N. */
+int lg_sinkhorn_workspace_bytes(int32_t B, int32_t M, int32_t N, size_t* bytes);
+int lg_log_optimal_transport(const float* scores, float alpha, int32_t B, int32_t M, int32_t N,
+                             int32_t iters, float* Z, void* workspace, size_t workspace_bytes,
+                             void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIGHTGLUE_MI355X_H */

@@ -26,6 +26,7 @@ in ``torch.stack([])`` (``:572``) after the matches were computed; the harness s
 module's ``torch`` for a proxy whose ``stack`` returns an empty tensor for an empty list, and the
 fixture omits ``ref_descriptors*``.
 """
+import copy
 import hashlib
 import importlib
 import json
@@ -225,6 +226,21 @@ def run_case(lg_mod, name, spec):
     out["la_col_max"] = inner.max(1).values.numpy()
     out["la_dustbin_col"] = la[:, :-1, -1].numpy()
     out["la_dustbin_row"] = la[:, -1, :-1].numpy()
+    if conf.get("width_confidence", -1) <= 0 and conf.get("depth_confidence", -1) <= 0:
+        # The same reference run in float64: top-1 / top-2 margins of every row and column of
+        # the inner log assignment.  Rows/columns with a margin below the fp32 noise floor are
+        # near-ties whose argmax no fp32 implementation decides reliably.
+        m64 = copy.deepcopy(model).double()
+        d64 = {k: (v.double() if isinstance(v, torch.Tensor) else {kk: vv.double() for kk, vv in v.items()}) for k, v in data.items()}
+        torch.set_default_dtype(torch.float64)  # the reference builds its condition tensor with torch.ones
+        try:
+            with torch.no_grad():
+                la64 = m64(d64)["log_assignment"][:, :-1, :-1]
+        finally:
+            torch.set_default_dtype(torch.float32)
+        t0, t1 = la64.topk(min(2, la64.shape[2]), dim=2).values, la64.topk(min(2, la64.shape[1]), dim=1).values
+        out["margin0"] = (t0[..., 0] - t0[..., -1]).float().numpy()
+        out["margin1"] = (t1[:, 0] - t1[:, -1]).float().numpy()
     if pred["ref_descriptors0"].numel():
         out["ref_descriptors0"] = pred["ref_descriptors0"].numpy() if full else pred["ref_descriptors0"][:, :, :8].numpy()
         out["ref_descriptors1"] = pred["ref_descriptors1"].numpy() if full else pred["ref_descriptors1"][:, :, :8].numpy()

@@ -1,0 +1,118 @@
+"""CPU-only checks: the C-ABI library loads and exports what include/*.h declares, the drop-in
+module keeps the reference's config keys and state-dict schema, and the host helpers behave."""
+import ctypes
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import lgamd  # noqa: F401
+from lightglue_amd import _lib
+from lightglue_amd.weights import DEFAULT_CONF, state_dict_schema, synthetic_pair, synthetic_state_dict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        syms |= set(re.findall(r"\b(lg_[a-z_0-9]+)\s*\(", src))
+    return syms
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = _lib.load()
+    declared = declared_symbols()
+    assert declared, "no declarations found"
+    for s in sorted(declared):
+        assert hasattr(lib, s), f"{s} declared in include/ but not exported"
+    assert declared == set(_lib.EXPORTED_SYMBOLS)
+    assert lib.lg_abi_version() == _lib.ABI_VERSION
+
+
+def test_ctypes_structs_match_header_layout():
+    # lg_config_t: 5 x int32 then 3 doubles (8-byte aligned) -> 48 bytes
+    assert ctypes.sizeof(_lib.LGConfig) == 48
+    assert ctypes.sizeof(_lib.LGInputs) == 16 + 10 * 8
+    assert ctypes.sizeof(_lib.LGOutputs) == 9 * 8 + 12 + 4
+
+
+def test_error_path_without_gpu_reports_message():
+    lib = _lib.load()
+    b = ctypes.c_size_t()
+    assert lib.lg_filter_workspace_bytes(2, 10, 12, ctypes.byref(b)) == 0 and b.value > 0
+    rc = lib.lg_filter_matches(None, 1, 1, 1, 0.0, None, None, None, None, None, 0, None)
+    assert rc == _lib.LG_E_INVALID
+    assert b"null" in lib.lg_last_error()
+
+
+def test_module_schema_matches_reference_schema():
+    from lightglue_amd import LightGlue
+
+    for conf in ({}, {"add_scale_ori": True}, {"input_dim": 128}, {"n_layers": 3}):
+        m = LightGlue(conf)
+        sd = m.state_dict()
+        schema = state_dict_schema(conf)
+        assert list(sd.keys()) == [n for n, _ in schema]
+        for n, shape in schema:
+            assert tuple(sd[n].shape) == tuple(shape), n
+
+
+def test_default_conf_keys_match_reference():
+    # lightglue.py:341-361
+    assert set(DEFAULT_CONF) == {
+        "name", "input_dim", "add_scale_ori", "descriptor_dim", "n_layers", "num_heads", "flash", "mp",
+        "depth_confidence", "width_confidence", "filter_threshold", "checkpointed", "weights",
+        "weights_from_version", "loss",
+    }
+
+
+def test_checkpoint_key_renames(tmp_path):
+    """Old 'self_attn.{i}' / 'cross_attn.{i}' keys are renamed like lightglue.py:424-429."""
+    from lightglue_amd import LightGlue
+
+    sd = synthetic_state_dict({}, seed=3)
+    old = {}
+    for k, v in sd.items():
+        k2 = re.sub(r"^transformers\.(\d+)\.self_attn", r"self_attn.\1", k)
+        k2 = re.sub(r"^transformers\.(\d+)\.cross_attn", r"cross_attn.\1", k2)
+        old[k2] = torch.from_numpy(v)
+    p = tmp_path / "w.pth"
+    torch.save(old, p)
+    m = LightGlue({"weights": str(p)})
+    got = m.state_dict()
+    for k, v in sd.items():
+        assert torch.equal(got[k], torch.from_numpy(v)), k
+
+
+def test_forward_refuses_cpu_inputs():
+    from lightglue_amd import LightGlue
+
+    m = LightGlue({})
+    data = {k: torch.from_numpy(v) for k, v in synthetic_pair(B=1, M=8, seed=0).items()}
+    with pytest.raises((RuntimeError, AssertionError)):
+        m(data)
+
+
+def test_assignment_helpers_refuse_cpu():
+    from lightglue_amd import filter_matches, log_optimal_transport
+
+    with pytest.raises(RuntimeError):
+        filter_matches(torch.zeros(1, 3, 3), 0.1)
+    with pytest.raises(RuntimeError):
+        log_optimal_transport(torch.zeros(1, 3, 3), 1.0, 3)
+
+
+def test_synthetic_recipes_are_deterministic():
+    a = synthetic_state_dict({}, seed=0)
+    b = synthetic_state_dict({}, seed=0)
+    assert all(np.array_equal(a[k], b[k]) for k in a)
+    p, q = synthetic_pair(B=2, M=20, N=30, seed=1), synthetic_pair(B=2, M=20, N=30, seed=1)
+    assert all(np.array_equal(p[k], q[k]) for k in p)
+    assert p["keypoints1"].shape == (2, 30, 2)
+    np.testing.assert_allclose(np.linalg.norm(p["descriptors1"], axis=-1), 1.0, atol=1e-5)

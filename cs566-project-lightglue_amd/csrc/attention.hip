@@ -10,28 +10,43 @@
 //     equals attention(q = qk1, k = qk0, v = v0), the same identity the reference's flash path
 //     uses (:229-233).
 //
-// Structure: a workgroup of 4 waves owns 128 queries of one (set, pair, head); each wave 32
-// queries.  K/V stream through LDS in 64-key tiles (register-staged, double-buffered).
+// Structure: a workgroup of WAVES waves owns 32*WAVES queries of one (set, pair, head); each
+// wave 32 queries.  K/V stream through LDS in KT-key tiles (register-staged, double-buffered).
 // S^T = K Q^T is computed with the KEY on the MFMA row and the QUERY on the lane, so each lane
-// holds 32 scores of one query: the softmax row reduction is in-register plus one exchange
+// holds the scores of one query: the softmax row reduction is in-register plus one exchange
 // with lane^32, and the probability accumulator is directly the B operand of O^T = V^T P^T
 // (no LDS round trip for P).  Q lives in registers (32 floats per lane).
+// Work items (set, pair*head, query block) are walked through an XCD-aware remap so that the
+// query blocks sharing one K/V run on the same XCD (L2).
 #include "common.h"
 #include "kernels.h"
 
 namespace lg {
 
-constexpr int QB = 128;         // queries per workgroup (4 waves x 32)
-constexpr int KT = 64;          // keys per tile
 constexpr int KS = kHeadDim + 4;  // LDS row stride (floats): conflict-free ds_read_b128 rows
 
-__global__ __launch_bounds__(256) void attention_f32_kernel(AttnSet s0, AttnSet s1, int B, int H, float scale_log2e) {
+__device__ __forceinline__ int xcd_chunk(int id, int n) {
+  const int xcd = id & 7, local = id >> 3;
+  const int base = n >> 3, extra = n & 7;
+  return xcd * base + (xcd < extra ? xcd : extra) + local;
+}
+
+template <int WAVES, int KT>
+__global__ __launch_bounds__(64 * WAVES) void attention_f32_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+                                                                    float scale_log2e) {
+  constexpr int NT = 64 * WAVES;
+  constexpr int QB = 32 * WAVES;
+  constexpr int NSUB = KT / 32;                 // 32-key sub-tiles per tile
+  constexpr int LD = KT * 16 / NT;              // float4 loads per thread per tile (each of K, V)
   __shared__ float Ks[2][KT * KS];
   __shared__ float Vs[2][KT * KS];
 
-  const AttnSet& S = blockIdx.z == 0 ? s0 : s1;
-  const int bh = blockIdx.y;
-  const int q_blk = blockIdx.x * QB;
+  const int item = xcd_chunk(blockIdx.x, gridDim.x);
+  const int qb = item % nqb;
+  const int sbh = item / nqb;                   // set * (B*H) + bh
+  const int set = sbh / (B * H), bh = sbh - set * (B * H);
+  const AttnSet& S = set == 0 ? s0 : s1;
+  const int q_blk = qb * QB;
   if (q_blk >= S.Nq) return;
   const int Nq = S.Nq, Nk = S.Nk;
   const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
@@ -55,12 +70,11 @@ __global__ __launch_bounds__(256) void attention_f32_kernel(AttnSet s0, AttnSet 
     }
   }
 
-  // K/V tile staging: 64 rows x 64 floats x 2 = 2048 float4, 8 per thread.
-  f32x4 rk[4], rv[4];
+  f32x4 rk[LD], rv[LD];
   auto gload = [&](int t0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = tid + i * 256;
+    for (int i = 0; i < LD; ++i) {
+      const int q = tid + i * NT;
       const int r = q >> 4, c4 = q & 15;
       const int key = min(t0 + r, Nk - 1);
       rk[i] = *reinterpret_cast<const f32x4*>(K + (size_t)key * kHeadDim + c4 * 4);
@@ -69,8 +83,8 @@ __global__ __launch_bounds__(256) void attention_f32_kernel(AttnSet s0, AttnSet 
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = tid + i * 256;
+    for (int i = 0; i < LD; ++i) {
+      const int q = tid + i * NT;
       const int r = q >> 4, c4 = q & 15;
       *reinterpret_cast<f32x4*>(&Ks[buf][r * KS + c4 * 4]) = rk[i];
       *reinterpret_cast<f32x4*>(&Vs[buf][r * KS + c4 * 4]) = rv[i];
@@ -92,10 +106,10 @@ __global__ __launch_bounds__(256) void attention_f32_kernel(AttnSet s0, AttnSet 
     const float* ks = &Ks[cur][0];
     const float* vs = &Vs[cur][0];
 
-    // ---- S^T = K Q^T for two 32-key sub-tiles
-    f32x16 sc[2];
+    // ---- S^T = K Q^T for NSUB 32-key sub-tiles
+    f32x16 sc[NSUB];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NSUB; ++u) {
       sc[u] = f32x16{0.f};
       const float* kr = ks + (u * 32 + l32) * KS + half * 32;
 #pragma unroll
@@ -105,27 +119,30 @@ __global__ __launch_bounds__(256) void attention_f32_kernel(AttnSet s0, AttnSet 
         for (int j = 0; j < 4; ++j) sc[u] = mfma32(kv[j], qreg[s4 * 4 + j], sc[u]);
       }
     }
-    // ---- mask keys beyond Nk, online softmax
+    // ---- mask keys beyond Nk (last tile only), online softmax
+    if (t0 + KT > Nk) {
+#pragma unroll
+      for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (t0 + u * 32 + row32(r, half) >= Nk) sc[u][r] = -INFINITY;
+    }
     float tmax = -INFINITY;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NSUB; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = t0 + u * 32 + row32(r, half);
-        if (key >= Nk) sc[u][r] = -INFINITY;
-        tmax = fmaxf(tmax, sc[u][r]);
-      }
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[u][r]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m_run, tmax);
-    const float alpha = exp2f((m_run - m_new) * scale_log2e);
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2e);
     m_run = m_new;
     const float mb = m_new * scale_log2e;
     float psum = 0.f;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NSUB; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(fmaf(sc[u][r], scale_log2e, -mb));
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], scale_log2e, -mb));
         sc[u][r] = p;
         psum += p;
       }
@@ -135,7 +152,7 @@ __global__ __launch_bounds__(256) void attention_f32_kernel(AttnSet s0, AttnSet 
 
     // ---- O^T += V^T P^T : step (u, r) consumes key u*32 + row32(r, half) for this lane half
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NSUB; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float* vr = vs + (u * 32 + row32(r, half)) * KS + l32;
@@ -165,13 +182,26 @@ __global__ __launch_bounds__(256) void attention_f32_kernel(AttnSet s0, AttnSet 
   }
 }
 
-hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+template <int WAVES, int KT>
+static hipError_t attention_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+  constexpr int QB = 32 * WAVES;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
   if (nq == 0 || B == 0) return hipSuccess;
   if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
-  dim3 grid((nq + QB - 1) / QB, B * H, 2);
-  hipLaunchKernelGGL(attention_f32_kernel, grid, dim3(256), 0, st, s0, s1, B, H, scale * 1.4426950408889634f);
+  const int nqb = (nq + QB - 1) / QB;
+  const int items = nqb * B * H * 2;
+  hipLaunchKernelGGL((attention_f32_kernel<WAVES, KT>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
+                     scale * 1.4426950408889634f);
   return hipGetLastError();
+}
+
+#ifndef LG_ATTN_CONFIG
+// WAVES, KT: 8 waves (256 queries) per workgroup, 64-key tiles (tools/kbench_attn.hip).
+#define LG_ATTN_CONFIG 8, 64
+#endif
+
+hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+  return attention_launch<LG_ATTN_CONFIG>(s0, s1, B, H, scale, st);
 }
 
 }  // namespace lg

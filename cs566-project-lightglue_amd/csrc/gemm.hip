@@ -12,19 +12,17 @@
 //   MatchAssignment.final_proj / d^.25 :304,308-310 -> EPI_STORE with out_scale 0.25
 //   MatchAssignment einsum bmd,bnd->bmn :311 -> EPI_STORE, batched over pairs (blockIdx.z)
 //
-// Tiling: BM x BN block tile, BK = 32, one wave per WM x WN sub-tile of 32x32 MFMA tiles.
-// K is permuted inside each 32-wide k-tile (MFMA step s, lane half h uses k = 16h + s) so a
-// lane's operands for 4 consecutive steps are one 16-byte LDS read.  LDS rows are padded to
-// 36 floats: the 16 lanes of each ds_read_b128 group then hit 16 distinct 4-bank slots.
-// Global->LDS is register-staged and double-buffered (one barrier per k-tile).
-// blockIdx -> tile goes through a bijective XCD remap so tiles sharing A rows share an L2.
+// Tiling: BM x BN block tile, BK-deep k-tiles, one wave per WM x WN sub-tile of 32x32 MFMA
+// tiles.  K is permuted inside each k-tile (MFMA step s, lane half h uses k = h*BK/2 + s) so a
+// lane's operands for 4 consecutive steps are one 16-byte LDS read.  LDS rows are padded by 4
+// floats (stride 20 or 36 dwords): the 16 lanes of each ds_read_b128 group then hit 16
+// distinct 4-bank slots.  Global->LDS is register-staged and double-buffered (one barrier per
+// k-tile).  blockIdx -> tile goes through a bijective XCD remap so that the column tiles of one
+// row panel run on one XCD and share its L2.
 #include "common.h"
 #include "kernels.h"
 
 namespace lg {
-
-constexpr int BK = 32;
-constexpr int LDS_STRIDE = BK + 4;  // floats
 
 __device__ __forceinline__ int xcd_remap(int id, int n) {
   const int xcd = id & 7, local = id >> 3;
@@ -32,30 +30,36 @@ __device__ __forceinline__ int xcd_remap(int id, int n) {
   return xcd * base + (xcd < extra ? xcd : extra) + local;
 }
 
-// row -> (set, b, n) for the two-image row space: rows [0, B*M) are image 0, then image 1.
-__device__ __forceinline__ size_t head_row_offset(const HeadLayout& hl, int row, int head) {
-  int b, n, cnt;
-  size_t base;
+// Row -> head-major base offset for the two-image row space: rows [0, B*M) are image 0, then
+// image 1; destination [set][b][h][n][64].  Returns the offset of head 0; heads are `stride` apart.
+__device__ __forceinline__ void head_row_base(const HeadLayout& hl, int row, int& base, int& stride) {
   if (row < hl.B * hl.M) {
-    b = row / hl.M; n = row - b * hl.M; cnt = hl.M; base = 0;
+    const int b = row / hl.M, n = row - b * hl.M;
+    base = (b * hl.H * hl.M + n) * kHeadDim;
+    stride = hl.M * kHeadDim;
   } else {
     const int r2 = row - hl.B * hl.M;
-    b = r2 / hl.N; n = r2 - b * hl.N; cnt = hl.N; base = (size_t)hl.B * hl.H * hl.M * kHeadDim;
+    const int b = r2 / hl.N, n = r2 - b * hl.N;
+    base = hl.B * hl.H * hl.M * kHeadDim + (b * hl.H * hl.N + n) * kHeadDim;
+    stride = hl.N * kHeadDim;
   }
-  return base + ((size_t)(b * hl.H + head) * cnt + n) * kHeadDim;
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int BK, int WM, int WN, int EPI>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(GemmArgs args) {
   constexpr int NWN = BN / WN;
   constexpr int NT = 64 * (BM / WM) * NWN;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int A_LD = BM * BK / 4 / NT;  // float4 loads per thread per k-tile
-  constexpr int B_LD = BN * BK / 4 / NT;
-  static_assert(BM * BK / 4 % NT == 0 && BN * BK / 4 % NT == 0, "tile/threads mismatch");
+  constexpr int C4 = BK / 4;              // float4 chunks per row of a k-tile
+  constexpr int LDS = BK + 4;             // padded row stride (floats)
+  constexpr int HK = BK / 2;              // k per lane half
+  constexpr int A_LD = BM * C4 / NT;      // float4 loads per thread per k-tile
+  constexpr int B_LD = BN * C4 / NT;
+  static_assert(BM * C4 % NT == 0 && BN * C4 % NT == 0, "tile/threads mismatch");
 
-  __shared__ float As[2][BM * LDS_STRIDE];
-  __shared__ float Bs[2][BN * LDS_STRIDE];
+  __shared__ float As[2][BM * LDS];
+  __shared__ float Bs[2][BN * LDS];
+  __shared__ int rowinfo[EPI == EPI_STORE ? 1 : 2 * BM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -73,8 +77,17 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
   const float* A1 = args.A1 ? args.A1 + z * args.sA1 : nullptr;
   const float* W = args.W + z * args.sW;
 
-  f32x4 ra[A_LD], rb[B_LD];
-  auto gload = [&](int kt) {
+  if constexpr (EPI != EPI_STORE) {
+    for (int r = tid; r < BM; r += NT) {
+      int base = 0, stride = 0;
+      if (m0 + r < args.R) head_row_base(args.hl, m0 + r, base, stride);
+      rowinfo[2 * r] = base;
+      rowinfo[2 * r + 1] = stride;
+    }
+  }
+
+  f32x4 ra[1][A_LD], rb[1][B_LD];
+  auto gload = [&](int kt, f32x4 (&ra)[A_LD], f32x4 (&rb)[B_LD]) {
     const int k0 = kt * BK;
     const float* src;
     int ld, kk;
@@ -83,7 +96,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const int q = tid + i * NT;
-      const int r = q >> 3, c4 = q & 7;
+      const int r = q / C4, c4 = q % C4;
       int row = m0 + r;
       row = row < args.R ? row : args.R - 1;
       ra[i] = *reinterpret_cast<const f32x4*>(src + (size_t)row * ld + kk + c4 * 4);
@@ -91,22 +104,22 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
       const int q = tid + i * NT;
-      const int r = q >> 3, c4 = q & 7;
+      const int r = q / C4, c4 = q % C4;
       int col = n0 + r;
       col = col < args.Nout ? col : args.Nout - 1;
       rb[i] = *reinterpret_cast<const f32x4*>(W + (size_t)col * args.ldw + k0 + c4 * 4);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const f32x4 (&ra)[A_LD], const f32x4 (&rb)[B_LD]) {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const int q = tid + i * NT;
-      *reinterpret_cast<f32x4*>(&As[buf][(q >> 3) * LDS_STRIDE + (q & 7) * 4]) = ra[i];
+      *reinterpret_cast<f32x4*>(&As[buf][(q / C4) * LDS + (q % C4) * 4]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
       const int q = tid + i * NT;
-      *reinterpret_cast<f32x4*>(&Bs[buf][(q >> 3) * LDS_STRIDE + (q & 7) * 4]) = rb[i];
+      *reinterpret_cast<f32x4*>(&Bs[buf][(q / C4) * LDS + (q % C4) * 4]) = rb[i];
     }
   };
 
@@ -116,24 +129,18 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{0.f};
 
-  const int nk = args.K / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload(kt + 1);
-    const float* as = &As[cur][0];
-    const float* bs = &Bs[cur][0];
+  auto compute = [&](int buf) {
+    const float* as = &As[buf][0];
+    const float* bs = &Bs[buf][0];
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
+    for (int s4 = 0; s4 < HK / 4; ++s4) {
       f32x4 a[TM], b[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        a[i] = *reinterpret_cast<const f32x4*>(as + (wm0 + i * 32 + l32) * LDS_STRIDE + half * 16 + s4 * 4);
+        a[i] = *reinterpret_cast<const f32x4*>(as + (wm0 + i * 32 + l32) * LDS + half * HK + s4 * 4);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        b[j] = *reinterpret_cast<const f32x4*>(bs + (wn0 + j * 32 + l32) * LDS_STRIDE + half * 16 + s4 * 4);
+        b[j] = *reinterpret_cast<const f32x4*>(bs + (wn0 + j * 32 + l32) * LDS + half * HK + s4 * 4);
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
@@ -141,7 +148,19 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][kk], b[j][kk], acc[i][j]);
     }
-    if (kt + 1 < nk) sstore(cur ^ 1);
+  };
+
+  // Tile kt+1 is loaded into registers while tile kt is consumed from LDS.  (A two-deep
+  // register ring measured no faster on these K = 256/512 shapes and costs ~60 VGPRs.)
+  const int nk = args.K / BK;
+  gload(0, ra[0], rb[0]);
+  sstore(0, ra[0], rb[0]);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(kt + 1, ra[0], rb[0]);
+    compute(cur);
+    if (kt + 1 < nk) sstore(cur ^ 1, ra[0], rb[0]);
     __syncthreads();
     cur ^= 1;
   }
@@ -168,7 +187,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
   } else {
     // Head-major scatter.  WN == 64 and n0 + wn0 is a multiple of 64, so the wave owns one
     // (type, head) block: type t = col / 256, head = (col % 256) / 64, stored dim = j*32 + l32.
-    static_assert(EPI != EPI_QKV_ROT || (WN == 64 && TN == 2), "rotary epilogue needs 64-wide wave tiles");
+    static_assert(WN == 64 && TN == 2, "head epilogues need 64-wide wave tiles");
     const HeadLayout& hl = args.hl;
     const int cbase = n0 + wn0;
     const int t = cbase / kDim, head = (cbase % kDim) / kHeadDim;
@@ -180,9 +199,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + i * 32 + row32(r, half);
+        const int lr = wm0 + i * 32 + row32(r, half);
+        const int row = m0 + lr;
         if (row >= args.R) continue;
-        const size_t off = head_row_offset(hl, row, head);
+        const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1];
         if constexpr (EPI == EPI_QKV_ROT) {
           const float xe = acc[i][0][r] + b2[0];  // dim 2*l32   (even)
           const float xo = acc[i][1][r] + b2[1];  // dim 2*l32+1 (odd)
@@ -205,24 +225,30 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int BK, int WM, int WN, int EPI>
 static hipError_t launch(const GemmArgs& a, int batch, hipStream_t st) {
   const int nt = 64 * (BM / WM) * (BN / WN);
   const int blocks = ((a.R + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
   if (blocks == 0 || batch == 0) return hipSuccess;
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI>), dim3(blocks, 1, batch), dim3(nt), 0, st, a);
+  if (a.K % BK != 0 || (a.A1 && a.K0 % BK != 0)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, WM, WN, EPI>), dim3(blocks, 1, batch), dim3(nt), 0, st, a);
   return hipGetLastError();
 }
 
+#ifndef LG_GEMM_CONFIG
+// BM, BN, BK, WM, WN: 8 waves of 64x64, chosen by tools/kbench_gemm.hip on MI355X
+// (K = 256/512 shapes of this model, R = 131072 rows).
+#define LG_GEMM_CONFIG 256, 128, 16, 64, 64
+#endif
+
 hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, hipStream_t st) {
-  if (a.K % BK != 0 || (a.A1 && a.K0 % BK != 0)) return hipErrorInvalidValue;
   switch (epi) {
     case EPI_STORE:
-      return launch<64, 256, 64, 64, EPI_STORE>(a, batch, st);
+      return launch<LG_GEMM_CONFIG, EPI_STORE>(a, batch, st);
     case EPI_QKV_ROT:
-      return launch<64, 256, 64, 64, EPI_QKV_ROT>(a, batch, st);
+      return launch<LG_GEMM_CONFIG, EPI_QKV_ROT>(a, batch, st);
     case EPI_CROSS_QKV:
-      return launch<64, 256, 64, 64, EPI_CROSS_QKV>(a, batch, st);
+      return launch<LG_GEMM_CONFIG, EPI_CROSS_QKV>(a, batch, st);
   }
   return hipErrorInvalidValue;
 }

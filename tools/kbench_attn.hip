@@ -1,0 +1,91 @@
+// Micro-benchmark of attention variants (tools only; not shipped).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/kbench_attn.hip -o /tmp/ka && /tmp/ka
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../cs566-project-lightglue_amd/csrc/attention.hip"
+
+using namespace lg;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
+
+__global__ void fill(float* p, size_t n, unsigned seed, float scale) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < n) {
+    unsigned x = (unsigned)(i * 2654435761u) ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995; x ^= x >> 15;
+    p[i] = (((x & 0xffffff) / 16777216.0f) * 2.f - 1.f) * scale;
+  }
+}
+
+// naive reference: one thread per (bh, query), double accumulation
+__global__ void ref_attn(const float* Q, const float* K, const float* V, float* O, int BH, int H, int N, float scale) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= BH * N) return;
+  const int bh = t / N, q = t % N;
+  const float* qp = Q + ((size_t)bh * N + q) * 64;
+  double m = -1e300;
+  for (int k = 0; k < N; ++k) {
+    double s = 0;
+    for (int d = 0; d < 64; ++d) s += (double)qp[d] * K[((size_t)bh * N + k) * 64 + d];
+    m = fmax(m, s * scale);
+  }
+  double l = 0, o[64] = {0};
+  for (int k = 0; k < N; ++k) {
+    double s = 0;
+    for (int d = 0; d < 64; ++d) s += (double)qp[d] * K[((size_t)bh * N + k) * 64 + d];
+    const double p = exp(s * scale - m);
+    l += p;
+    for (int d = 0; d < 64; ++d) o[d] += p * V[((size_t)bh * N + k) * 64 + d];
+  }
+  const int b = bh / H, h = bh % H;
+  for (int d = 0; d < 64; ++d) O[((size_t)b * N + q) * 256 + h * 64 + d] = (float)(o[d] / l);
+}
+
+template <int W, int KT>
+void run(const char* name, const AttnSet& a0, const AttnSet& a1, int B, int H, float scale, float* Oref, float* O, size_t on) {
+  CK(hipMemset(O, 0, on * 4));
+  CK((attention_launch<W, KT>(a0, a1, B, H, scale, 0)));
+  CK(hipDeviceSynchronize());
+  std::vector<float> x(on), y(on);
+  CK(hipMemcpy(x.data(), O, on * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(y.data(), Oref, on * 4, hipMemcpyDeviceToHost));
+  double md = 0;
+  for (size_t i = 0; i < on; ++i) md = fmax(md, fabs((double)x[i] - y[i]));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const int it = 10;
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < it; ++i) CK((attention_launch<W, KT>(a0, a1, B, H, scale, 0)));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= it;
+  const double fl = 2.0 * 4.0 * 64.0 * H * B * ((double)a0.Nq * a0.Nk + (double)a1.Nq * a1.Nk);
+  printf("%-22s %8.1f us  %6.1f TF/s  maxdiff(set0 vs fp64) %.2e\n", name, ms * 1e3, fl / ms / 1e9, md);
+}
+
+int main(int argc, char** argv) {
+  const int B = 32, H = 4, N = argc > 1 ? atoi(argv[1]) : 2048;
+  const size_t n = (size_t)B * H * N * 64;
+  float *Q, *K, *V, *O, *Oref;
+  CK(hipMalloc(&Q, 2 * n * 4)); CK(hipMalloc(&K, 2 * n * 4)); CK(hipMalloc(&V, 2 * n * 4));
+  CK(hipMalloc(&O, 2 * n * 4)); CK(hipMalloc(&Oref, 2 * n * 4));
+  fill<<<(2 * n + 255) / 256, 256>>>(Q, 2 * n, 1, 2.f);
+  fill<<<(2 * n + 255) / 256, 256>>>(K, 2 * n, 2, 2.f);
+  fill<<<(2 * n + 255) / 256, 256>>>(V, 2 * n, 3, 1.f);
+  const float scale = 0.125f;
+  // reference for set 0 only (rows [0, B*N) of O)
+  ref_attn<<<(B * H * N + 127) / 128, 128>>>(Q, K, V, Oref, B * H, H, N, scale);
+  CK(hipDeviceSynchronize());
+  AttnSet a0{Q, K, V, O, N, N}, a1{Q + n, K + n, V + n, O + (size_t)B * N * 256, N, N};
+  const size_t on = (size_t)B * N * 256;  // compare set 0
+  run<4, 64>("w4 kt64", a0, a1, B, H, scale, Oref, O, on);
+  run<4, 128>("w4 kt128", a0, a1, B, H, scale, Oref, O, on);
+  run<8, 64>("w8 kt64", a0, a1, B, H, scale, Oref, O, on);
+  run<8, 128>("w8 kt128", a0, a1, B, H, scale, Oref, O, on);
+  run<2, 64>("w2 kt64", a0, a1, B, H, scale, Oref, O, on);
+  return 0;
+}

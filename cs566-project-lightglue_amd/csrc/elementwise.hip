@@ -146,6 +146,37 @@ hipError_t gemv_256(const float* x, const float* w, const float* b, float* y, in
 }
 
 // ----------------------------------------------------------------------------------------
+// Load-time fold of out_proj into ffn.0 (lightglue.py:172,190-191):
+//   ffn0([x, Wo c + bo]) = W1[:, :256] x + (W1[:, 256:] Wo) c + (b1 + W1[:, 256:] bo)
+// The folded block and bias are accumulated in fp64 and rounded once to fp32.
+// ----------------------------------------------------------------------------------------
+__global__ void fold_out_proj_kernel(const float* W1, const float* b1, const float* Wo, const float* bo, float* Wf,
+                                     float* bf) {
+  const int r = blockIdx.x;  // 0..511 (ffn.0 output row)
+  const int c = threadIdx.x; // 0..255 (context column)
+  const float* w1r = W1 + (size_t)r * 512 + 256;
+  double s = 0.0;
+  for (int k = 0; k < 256; ++k) s += (double)w1r[k] * (double)Wo[(size_t)k * 256 + c];
+  Wf[(size_t)r * 256 + c] = (float)s;
+  if (c == 0) {
+    double t = (double)b1[r];
+    for (int k = 0; k < 256; ++k) t += (double)w1r[k] * (double)bo[k];
+    bf[r] = (float)t;
+  }
+}
+
+hipError_t fold_out_proj(float* W1, float* b1, const float* Wo, const float* bo, float* tmp, hipStream_t st) {
+  // tmp: 512*256 + 512 floats
+  hipLaunchKernelGGL(fold_out_proj_kernel, dim3(512), dim3(256), 0, st, W1, b1, Wo, bo, tmp, tmp + 512 * 256);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipMemcpy2DAsync(W1 + 256, 512 * sizeof(float), tmp, 256 * sizeof(float), 256 * sizeof(float), 512,
+                       hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return e;
+  return hipMemcpyAsync(b1, tmp + 512 * 256, 512 * sizeof(float), hipMemcpyDeviceToDevice, st);
+}
+
+// ----------------------------------------------------------------------------------------
 // weight repacking
 // ----------------------------------------------------------------------------------------
 __global__ void gather_rows_kernel(float* dst, const float* src, const int* idx, int rows, int cols) {

@@ -5,7 +5,7 @@
 
 namespace lg {
 
-enum EpiKind { EPI_STORE = 0, EPI_QKV_ROT = 1, EPI_CROSS_QKV = 2 };
+enum EpiKind { EPI_STORE = 0, EPI_QKV_ROT = 1, EPI_CROSS_QKV = 2, EPI_PROBE = 3 /* benchmarking only */ };
 
 // Head-major destination [set][b][h][n][64] for the QKV epilogues; set 0 = image 0 (B*M rows),
 // set 1 = image 1 (B*N rows), rows in GEMM order (image 0 rows first).
@@ -88,6 +88,10 @@ hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st);
 hipError_t filter_from_scores(const float* scores, int B, int M, int N, float th, float* ws, int64_t* m0, int64_t* m1,
                               float* s0, float* s1, hipStream_t st);
 size_t filter_workspace_floats(int B, int M, int N);
+
+// Load-time fold of out_proj/to_out into ffn.0 (W1 [512][512], b1 [512], Wo [256][256], bo [256]);
+// tmp holds 512*256 + 512 floats.
+hipError_t fold_out_proj(float* W1, float* b1, const float* Wo, const float* bo, float* tmp, hipStream_t st);
 
 // Weight repacking: dst[r,:] = src[idx[r],:] (row length `cols`).
 hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st);

@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -117,6 +118,8 @@ struct lg_handle {
   float* wbuf = nullptr;
   int* perm = nullptr;  // Wqkv row permutation [768]
   bool loaded = false;
+  // fold out_proj / to_out into ffn.0 at load time (env LG_FOLD_OUT_PROJ=0 disables)
+  bool fold = true;
   // profiling (lg_profile_enable / lg_profile_read)
   struct Rec {
     hipEvent_t a, b;
@@ -342,6 +345,7 @@ int lg_create(const lg_config_t* cfg, int device, lg_handle_t** out) {
   lg_handle* h = new lg_handle();
   h->cfg = *cfg;
   h->device = device;
+  if (const char* f = getenv("LG_FOLD_OUT_PROJ")) h->fold = atoi(f) != 0;
   h->schema = make_schema(*cfg);
   for (size_t k = 0; k < h->schema.size(); ++k) h->index[h->schema[k].name] = (int)k;
   plan_layout(h);
@@ -420,6 +424,17 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
     } else {
       LG_HIP(hipMemcpyAsync(h->wbuf + h->dst[k], tensors[i], numels[i] * sizeof(float), hipMemcpyDeviceToDevice, st));
     }
+  }
+  if (h->fold) {
+    float* tmp = nullptr;
+    LG_HIP(hipMallocAsync((void**)&tmp, (512 * 256 + 512) * sizeof(float), st));
+    for (auto& lw : h->layers)
+      for (int b = 0; b < 2; ++b) {
+        const BlockW& w = b == 0 ? lw.self : lw.cross;
+        hipError_t e = lg::fold_out_proj(h->wbuf + w.W1, h->wbuf + w.b1, h->wbuf + w.Wo, h->wbuf + w.bo, tmp, st);
+        if (e != hipSuccess) return fail(LG_E_HIP, std::string("fold_out_proj: ") + hipGetErrorString(e));
+      }
+    LG_HIP(hipFreeAsync(tmp, st));
   }
   h->loaded = true;
   return LG_OK;
@@ -547,14 +562,16 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
         a1 = {w.Q + img1, w.Q, w.K, w.ctx + (size_t)B * M * D, N, M};
         LG_HIP(attn(a0, a1, 1.0f, true));
       }
-      // out projection
-      g = gemm_base();
-      g.A0 = w.ctx; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wo; g.ldw = D; g.bias = Wb + bw.bo;
-      g.R = R; g.Nout = D; g.Y = w.msg; g.ldy = D;
-      LG_HIP(gemm(g, EPI_STORE, 1));
+      // out projection (skipped when folded into ffn.0 at load time: ffn.0 then reads ctx)
+      if (!h->fold) {
+        g = gemm_base();
+        g.A0 = w.ctx; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wo; g.ldw = D; g.bias = Wb + bw.bo;
+        g.R = R; g.Nout = D; g.Y = w.msg; g.ldy = D;
+        LG_HIP(gemm(g, EPI_STORE, 1));
+      }
       // FFN: Linear(cat[x, msg]) -> LN -> GELU -> Linear + residual
       g = gemm_base();
-      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.A1 = w.msg; g.lda1 = D; g.K = 2 * D;
+      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.A1 = h->fold ? w.ctx : w.msg; g.lda1 = D; g.K = 2 * D;
       g.W = Wb + bw.W1; g.ldw = 2 * D; g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
       LG_HIP(gemm(g, EPI_STORE, 1));
       LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, st));

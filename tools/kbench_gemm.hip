@@ -13,7 +13,7 @@ using namespace lg;
 
 struct Shape { int R, K, N; const char* name; };
 
-template <int BM, int BN, int BK, int WM, int WN>
+template <int BM, int BN, int BK, int WM, int WN, int EPI = EPI_STORE>
 double run(const Shape& s, float* A, float* W, float* bias, float* Y, int iters) {
   GemmArgs a;
   memset(&a, 0, sizeof(a));
@@ -21,10 +21,10 @@ double run(const Shape& s, float* A, float* W, float* bias, float* Y, int iters)
   a.R = s.R; a.Nout = s.N; a.Y = Y; a.ldy = s.N;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  CK((launch<BM, BN, BK, WM, WN, EPI_STORE>(a, 1, 0)));
+  CK((launch<BM, BN, BK, WM, WN, EPI>(a, 1, 0)));
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK((launch<BM, BN, BK, WM, WN, EPI_STORE>(a, 1, 0)));
+  for (int i = 0; i < iters; ++i) CK((launch<BM, BN, BK, WM, WN, EPI>(a, 1, 0)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -64,16 +64,16 @@ int main() {
       printf("%-5s %-28s %8.1f us %7.1f TF/s  maxdiff %.2e\n", s.name, name, ms * 1e3, fl / ms / 1e9, maxdiff(Y0, Y, (size_t)s.R * s.N));
     };
     const int it = 20;
-    double ms = run<64, 256, 32, 64, 64>(s, A, W, bias, Y0, it); rep("64x256x32 w64x64 (4w)", ms);
+    double ms = run<256, 128, 16, 64, 64>(s, A, W, bias, Y0, it); rep("256x128x16 w64x64 (8w)", ms);
+    ms = run<256, 128, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
     ms = run<128, 256, 32, 64, 64>(s, A, W, bias, Y, it); rep("128x256x32 w64x64 (8w)", ms);
-    ms = run<128, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("128x256x16 w64x64 (8w)", ms);
+    ms = run<128, 256, 32, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
     ms = run<128, 128, 32, 64, 64>(s, A, W, bias, Y, it); rep("128x128x32 w64x64 (4w)", ms);
+    ms = run<128, 128, 32, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
     ms = run<128, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("128x128x16 w64x64 (4w)", ms);
-    ms = run<64, 128, 32, 32, 64>(s, A, W, bias, Y, it); rep("64x128x32 w32x64 (4w)", ms);
-    ms = run<128, 256, 32, 64, 128>(s, A, W, bias, Y, it); rep("128x256x32 w64x128 (4w)", ms);
-    ms = run<256, 256, 16, 64, 128>(s, A, W, bias, Y, it); rep("256x256x16 w64x128 (8w)", ms);
-    ms = run<256, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("256x128x16 w64x64 (8w)", ms);
-    ms = run<64, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("64x256x16 w64x64 (4w)", ms);
+    ms = run<128, 128, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
+    ms = run<256, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("256x256x16 w64x64 (16w)", ms);
+    ms = run<256, 256, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(bias)); CK(hipFree(Y0)); CK(hipFree(Y));
   }
   return 0;

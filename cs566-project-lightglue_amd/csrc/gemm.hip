@@ -1,28 +1,41 @@
-// fp32 "linear" GEMM on gfx950 f32-input MFMA (v_mfma_f32_32x32x2_f32), with fused epilogues.
+// fp32-accurate "linear" GEMM on gfx950 matrix cores, with fused epilogues.
 //
 //   Y[r, c] = epilogue( sum_k A[r, k] * W[c, k] + bias[c] )
 //
 // Replaces every nn.Linear on the LightGlue hot path (reference lightglue.py):
 //   SelfBlock.Wqkv        :168,184   -> EPI_QKV_ROT  (+ rotary :36-43,187-188, head-major scatter :185-186)
-//   SelfBlock.out_proj    :170,190   -> EPI_STORE
+//   SelfBlock.out_proj    :170,190   -> folded into ffn.0 at load time (or EPI_STORE)
 //   CrossBlock.to_qk/to_v :203-204,223-228,235 -> EPI_CROSS_QKV (one GEMM, 512 outputs, qk * scale^0.5)
-//   CrossBlock.to_out     :205,246   -> EPI_STORE
+//   CrossBlock.to_out     :205,246   -> folded into ffn.0 at load time (or EPI_STORE)
 //   ffn.0 on cat([x,msg]) :172,191,247-248 -> EPI_STORE with a two-source A (the cat is never built)
 //   ffn.3 + residual      :175,191   -> EPI_STORE with res (x + ffn(...))
 //   MatchAssignment.final_proj / d^.25 :304,308-310 -> EPI_STORE with out_scale 0.25
 //   MatchAssignment einsum bmd,bnd->bmn :311 -> EPI_STORE, batched over pairs (blockIdx.z)
 //
+// Two arithmetic modes, both fp32-accurate:
+//  * MODE_F32: v_mfma_f32_32x32x2_f32 (exact fp32 FMA chain).  K is permuted inside each k-tile
+//    (MFMA step s, lane half h uses k = h*BK/2 + s) so a lane's operands for 4 consecutive steps
+//    are one 16-byte LDS read.
+//  * MODE_X6: "bf16x6" on v_mfma_f32_32x32x16_bf16.  Each fp32 operand is split exactly into
+//    three bf16 pieces x = x0 + x1 + x2 (round-to-nearest each; residual <= 2^-27 |x|) when the
+//    k-tile is staged into LDS, and the product is accumulated as the six terms whose weight is
+//    >= 2^-18 (a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0, small terms first).  Every term is an
+//    exact bf16*bf16 product summed in fp32, so the result is as accurate as the fp32 chain
+//    (simulated: mean relative error 5e-9 vs 2e-8 for fp32 FMA, K = 256) at 6 x 32 cycles per
+//    32x32x16 block instead of 8 x 64.
 // Tiling: BM x BN block tile, BK-deep k-tiles, one wave per WM x WN sub-tile of 32x32 MFMA
-// tiles.  K is permuted inside each k-tile (MFMA step s, lane half h uses k = h*BK/2 + s) so a
-// lane's operands for 4 consecutive steps are one 16-byte LDS read.  LDS rows are padded by 4
-// floats (stride 20 or 36 dwords): the 16 lanes of each ds_read_b128 group then hit 16
-// distinct 4-bank slots.  Global->LDS is register-staged and double-buffered (one barrier per
-// k-tile).  blockIdx -> tile goes through a bijective XCD remap so that the column tiles of one
-// row panel run on one XCD and share its L2.
+// tiles; LDS rows padded so every 16-lane ds_read_b128 group hits 16 distinct 4-bank slots;
+// register-staged double buffer (one barrier per k-tile); blockIdx -> tile through a bijective
+// XCD remap so the column tiles of one row panel run on one XCD and share its L2.
 #include "common.h"
 #include "kernels.h"
 
 namespace lg {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+enum GemmMode { MODE_F32 = 0, MODE_X6 = 1 };
 
 __device__ __forceinline__ int xcd_remap(int id, int n) {
   const int xcd = id & 7, local = id >> 3;
@@ -45,21 +58,36 @@ __device__ __forceinline__ void head_row_base(const HeadLayout& hl, int row, int
   }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int EPI>
-__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(GemmArgs args) {
+// Exact split x = h + m + l into bf16 pieces (round-to-nearest-even each).
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r = x - (float)h;  // exact
+  m = (__bf16)r;
+  l = (__bf16)(r - (float)m);   // exact subtraction, rounded once
+}
+
+template <int MODE, int BM, int BN, int BK>
+struct GemmSmem {
+  static constexpr int LDF = BK + 4;  // fp32 row stride (floats)
+  static constexpr int LDH = BK + 8;  // bf16 row stride (elements): 20 or 12 dwords for BK 32/16
+  static constexpr size_t bytes =
+      MODE == MODE_F32 ? 2 * (size_t)(BM + BN) * LDF * 4 : 2 * 3 * (size_t)(BM + BN) * LDH * 2;
+};
+
+template <int MODE, int BM, int BN, int BK, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmArgs args) {
   constexpr int NWN = BN / WN;
   constexpr int NT = 64 * (BM / WM) * NWN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int C4 = BK / 4;              // float4 chunks per row of a k-tile
-  constexpr int LDS = BK + 4;             // padded row stride (floats)
-  constexpr int HK = BK / 2;              // k per lane half
   constexpr int A_LD = BM * C4 / NT;      // float4 loads per thread per k-tile
   constexpr int B_LD = BN * C4 / NT;
+  using SM = GemmSmem<MODE, BM, BN, BK>;
   static_assert(BM * C4 % NT == 0 && BN * C4 % NT == 0, "tile/threads mismatch");
+  static_assert(MODE == MODE_F32 || BK % 16 == 0, "bf16x6 needs BK % 16 == 0");
 
-  __shared__ float As[2][BM * LDS];
-  __shared__ float Bs[2][BN * LDS];
-  __shared__ int rowinfo[EPI == EPI_STORE ? 1 : 2 * BM];
+  __shared__ __attribute__((aligned(16))) char smem[SM::bytes];
+  __shared__ int rowinfo[EPI == EPI_STORE || EPI == EPI_PROBE ? 1 : 2 * BM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -77,7 +105,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
   const float* A1 = args.A1 ? args.A1 + z * args.sA1 : nullptr;
   const float* W = args.W + z * args.sW;
 
-  if constexpr (EPI != EPI_STORE) {
+  if constexpr (EPI == EPI_QKV_ROT || EPI == EPI_CROSS_QKV) {
     for (int r = tid; r < BM; r += NT) {
       int base = 0, stride = 0;
       if (m0 + r < args.R) head_row_base(args.hl, m0 + r, base, stride);
@@ -86,8 +114,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
     }
   }
 
-  f32x4 ra[1][A_LD], rb[1][B_LD];
-  auto gload = [&](int kt, f32x4 (&ra)[A_LD], f32x4 (&rb)[B_LD]) {
+  f32x4 ra[A_LD], rb[B_LD];
+  auto gload = [&](int kt) {
     const int k0 = kt * BK;
     const float* src;
     int ld, kk;
@@ -110,18 +138,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
       rb[i] = *reinterpret_cast<const f32x4*>(W + (size_t)col * args.ldw + k0 + c4 * 4);
     }
   };
-  auto sstore = [&](int buf, const f32x4 (&ra)[A_LD], const f32x4 (&rb)[B_LD]) {
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      const int q = tid + i * NT;
-      *reinterpret_cast<f32x4*>(&As[buf][(q / C4) * LDS + (q % C4) * 4]) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-      const int q = tid + i * NT;
-      *reinterpret_cast<f32x4*>(&Bs[buf][(q / C4) * LDS + (q % C4) * 4]) = rb[i];
-    }
-  };
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -129,38 +145,106 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{0.f};
 
+  // ---------------------------------------------------------------- stage / compute per mode
+  auto sstore = [&](int buf) {
+    if constexpr (MODE == MODE_F32) {
+      float* As = reinterpret_cast<float*>(smem) + (size_t)buf * (BM + BN) * SM::LDF;
+      float* Bs = As + BM * SM::LDF;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        const int q = tid + i * NT;
+        *reinterpret_cast<f32x4*>(&As[(q / C4) * SM::LDF + (q % C4) * 4]) = ra[i];
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) {
+        const int q = tid + i * NT;
+        *reinterpret_cast<f32x4*>(&Bs[(q / C4) * SM::LDF + (q % C4) * 4]) = rb[i];
+      }
+    } else {
+      // three bf16 planes per operand: plane p of A at [p][BM][LDH], of B at [p][BN][LDH]
+      __bf16* As = reinterpret_cast<__bf16*>(smem) + (size_t)buf * 3 * (BM + BN) * SM::LDH;
+      __bf16* Bs = As + 3 * BM * SM::LDH;
+      auto put = [&](__bf16* base, int rows, int q, const f32x4& v) {
+        bf16x4 h, m, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          __bf16 a, b, c;
+          split3(v[e], a, b, c);
+          h[e] = a; m[e] = b; l[e] = c;
+        }
+        const int off = (q / C4) * SM::LDH + (q % C4) * 4;
+        *reinterpret_cast<bf16x4*>(base + off) = h;
+        *reinterpret_cast<bf16x4*>(base + rows * SM::LDH + off) = m;
+        *reinterpret_cast<bf16x4*>(base + 2 * rows * SM::LDH + off) = l;
+      };
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) put(As, BM, tid + i * NT, ra[i]);
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) put(Bs, BN, tid + i * NT, rb[i]);
+    }
+  };
   auto compute = [&](int buf) {
-    const float* as = &As[buf][0];
-    const float* bs = &Bs[buf][0];
+    if constexpr (MODE == MODE_F32) {
+      constexpr int HK = BK / 2;
+      const float* as = reinterpret_cast<const float*>(smem) + (size_t)buf * (BM + BN) * SM::LDF;
+      const float* bs = as + BM * SM::LDF;
 #pragma unroll
-    for (int s4 = 0; s4 < HK / 4; ++s4) {
-      f32x4 a[TM], b[TN];
+      for (int s4 = 0; s4 < HK / 4; ++s4) {
+        f32x4 a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        a[i] = *reinterpret_cast<const f32x4*>(as + (wm0 + i * 32 + l32) * LDS + half * HK + s4 * 4);
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const f32x4*>(as + (wm0 + i * 32 + l32) * SM::LDF + half * HK + s4 * 4);
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        b[j] = *reinterpret_cast<const f32x4*>(bs + (wn0 + j * 32 + l32) * LDS + half * HK + s4 * 4);
+        for (int j = 0; j < TN; ++j)
+          b[j] = *reinterpret_cast<const f32x4*>(bs + (wn0 + j * 32 + l32) * SM::LDF + half * HK + s4 * 4);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][kk], b[j][kk], acc[i][j]);
+      }
+    } else {
+      const __bf16* as = reinterpret_cast<const __bf16*>(smem) + (size_t)buf * 3 * (BM + BN) * SM::LDH;
+      const __bf16* bs = as + 3 * BM * SM::LDH;
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8 a[TM][3], b[TN][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            a[i][p] = *reinterpret_cast<const bf16x8*>(as + (p * BM + wm0 + i * 32 + l32) * SM::LDH + s * 16 + half * 8);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            b[j][p] = *reinterpret_cast<const bf16x8*>(bs + (p * BN + wn0 + j * 32 + l32) * SM::LDH + s * 16 + half * 8);
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][kk], b[j][kk], acc[i][j]);
+          for (int j = 0; j < TN; ++j) {
+            f32x16 c = acc[i][j];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+            acc[i][j] = c;
+          }
+      }
     }
   };
 
-  // Tile kt+1 is loaded into registers while tile kt is consumed from LDS.  (A two-deep
-  // register ring measured no faster on these K = 256/512 shapes and costs ~60 VGPRs.)
   const int nk = args.K / BK;
-  gload(0, ra[0], rb[0]);
-  sstore(0, ra[0], rb[0]);
+  gload(0);
+  sstore(0);
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload(kt + 1, ra[0], rb[0]);
+    if (kt + 1 < nk) gload(kt + 1);
     compute(cur);
-    if (kt + 1 < nk) sstore(cur ^ 1, ra[0], rb[0]);
+    if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
     cur ^= 1;
   }
@@ -235,20 +319,22 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_f32_kernel(Ge
   }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int EPI>
+template <int MODE, int BM, int BN, int BK, int WM, int WN, int EPI>
 static hipError_t launch(const GemmArgs& a, int batch, hipStream_t st) {
   const int nt = 64 * (BM / WM) * (BN / WN);
   const int blocks = ((a.R + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
   if (blocks == 0 || batch == 0) return hipSuccess;
   if (a.K % BK != 0 || (a.A1 && a.K0 % BK != 0)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, WM, WN, EPI>), dim3(blocks, 1, batch), dim3(nt), 0, st, a);
+  hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, BK, WM, WN, EPI>), dim3(blocks, 1, batch), dim3(nt), 0, st, a);
   return hipGetLastError();
 }
 
 #ifndef LG_GEMM_CONFIG
-// BM, BN, BK, WM, WN: 8 waves of 64x64, chosen by tools/kbench_gemm.hip on MI355X
-// (K = 256/512 shapes of this model, R = 131072 rows).
-#define LG_GEMM_CONFIG 256, 128, 16, 64, 64
+// MODE, BM, BN, BK, WM, WN: chosen by tools/kbench_gemm.hip on MI355X (K = 256/512 shapes of
+// this model, R = 131072 rows).
+// bf16x6 at 256x256x16 with 16 waves of 64x64 ran 173-198 TF/s on the four Linear shapes
+// (fp32 MFMA 256x128x16: 95-120 TF/s) with a lower error vs fp64 (mean 1.4e-8 vs 1.7e-8).
+#define LG_GEMM_CONFIG MODE_X6, 256, 256, 16, 64, 64
 #endif
 
 hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, hipStream_t st) {

@@ -1,5 +1,6 @@
-// Micro-benchmark of GEMM tilings (tools only; not shipped).  Build + run on the GPU box:
+// Micro-benchmark of GEMM tilings / arithmetic modes (tools only; not shipped).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I cs566-project-lightglue_amd/csrc tools/kbench_gemm.hip -o /tmp/kb && /tmp/kb
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -13,7 +14,7 @@ using namespace lg;
 
 struct Shape { int R, K, N; const char* name; };
 
-template <int BM, int BN, int BK, int WM, int WN, int EPI = EPI_STORE>
+template <int MODE, int BM, int BN, int BK, int WM, int WN, int EPI = EPI_STORE>
 double run(const Shape& s, float* A, float* W, float* bias, float* Y, int iters) {
   GemmArgs a;
   memset(&a, 0, sizeof(a));
@@ -21,10 +22,10 @@ double run(const Shape& s, float* A, float* W, float* bias, float* Y, int iters)
   a.R = s.R; a.Nout = s.N; a.Y = Y; a.ldy = s.N;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  CK((launch<BM, BN, BK, WM, WN, EPI>(a, 1, 0)));
+  CK((launch<MODE, BM, BN, BK, WM, WN, EPI>(a, 1, 0)));
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK((launch<BM, BN, BK, WM, WN, EPI>(a, 1, 0)));
+  for (int i = 0; i < iters; ++i) CK((launch<MODE, BM, BN, BK, WM, WN, EPI>(a, 1, 0)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -41,40 +42,55 @@ __global__ void fill(float* p, size_t n, unsigned seed) {
   }
 }
 
-float maxdiff(const float* a, const float* b, size_t n) {
-  std::vector<float> x(n), y(n);
-  hipMemcpy(x.data(), a, n * 4, hipMemcpyDeviceToHost);
-  hipMemcpy(y.data(), b, n * 4, hipMemcpyDeviceToHost);
-  float m = 0;
-  for (size_t i = 0; i < n; ++i) m = fmaxf(m, fabsf(x[i] - y[i]));
-  return m;
+// fp64 reference for the first `rows` rows; also sum |a*b| for relative errors
+__global__ void ref64(const float* A, const float* W, const float* bias, double* Y, double* S, int rows, int K, int N) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * N) return;
+  const int r = t / N, c = t % N;
+  double s = bias[c], a = 0;
+  for (int k = 0; k < K; ++k) { const double p = (double)A[(size_t)r * K + k] * W[(size_t)c * K + k]; s += p; a += fabs(p); }
+  Y[t] = s; S[t] = a;
 }
 
 int main() {
   const Shape shapes[] = {{131072, 256, 768, "qkv"}, {131072, 512, 512, "ffn1"}, {131072, 512, 256, "ffn2"}, {131072, 256, 256, "outp"}};
+  const int RR = 512;  // rows checked against fp64
   for (const Shape& s : shapes) {
-    float *A, *W, *bias, *Y0, *Y;
+    float *A, *W, *bias, *Y;
+    double *Yr, *Sr;
     CK(hipMalloc(&A, (size_t)s.R * s.K * 4)); CK(hipMalloc(&W, (size_t)s.N * s.K * 4));
-    CK(hipMalloc(&bias, s.N * 4)); CK(hipMalloc(&Y0, (size_t)s.R * s.N * 4)); CK(hipMalloc(&Y, (size_t)s.R * s.N * 4));
+    CK(hipMalloc(&bias, s.N * 4)); CK(hipMalloc(&Y, (size_t)s.R * s.N * 4));
+    CK(hipMalloc(&Yr, (size_t)RR * s.N * 8)); CK(hipMalloc(&Sr, (size_t)RR * s.N * 8));
     fill<<<(s.R * (size_t)s.K + 255) / 256, 256>>>(A, (size_t)s.R * s.K, 1);
     fill<<<(s.N * (size_t)s.K + 255) / 256, 256>>>(W, (size_t)s.N * s.K, 2);
     fill<<<(s.N + 255) / 256, 256>>>(bias, s.N, 3);
+    ref64<<<(RR * s.N + 255) / 256, 256>>>(A, W, bias, Yr, Sr, RR, s.K, s.N);
+    CK(hipDeviceSynchronize());
+    std::vector<double> yr((size_t)RR * s.N), sr((size_t)RR * s.N);
+    CK(hipMemcpy(yr.data(), Yr, yr.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(sr.data(), Sr, sr.size() * 8, hipMemcpyDeviceToHost));
     const double fl = 2.0 * s.R * s.K * s.N;
-    auto rep = [&](const char* name, double ms) {
-      printf("%-5s %-28s %8.1f us %7.1f TF/s  maxdiff %.2e\n", s.name, name, ms * 1e3, fl / ms / 1e9, maxdiff(Y0, Y, (size_t)s.R * s.N));
+    auto rep = [&](const char* name, double ms, bool check) {
+      double mx = 0, mean = 0;
+      if (check) {
+        std::vector<float> y((size_t)RR * s.N);
+        CK(hipMemcpy(y.data(), Y, y.size() * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < y.size(); ++i) { const double e = fabs(y[i] - yr[i]) / sr[i]; mx = fmax(mx, e); mean += e; }
+        mean /= y.size();
+      }
+      printf("%-5s %-30s %8.1f us %7.1f TF/s  rel.err mean %.2e max %.2e\n", s.name, name, ms * 1e3, fl / ms / 1e9, mean, mx);
     };
     const int it = 20;
-    double ms = run<256, 128, 16, 64, 64>(s, A, W, bias, Y0, it); rep("256x128x16 w64x64 (8w)", ms);
-    ms = run<256, 128, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
-    ms = run<128, 256, 32, 64, 64>(s, A, W, bias, Y, it); rep("128x256x32 w64x64 (8w)", ms);
-    ms = run<128, 256, 32, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
-    ms = run<128, 128, 32, 64, 64>(s, A, W, bias, Y, it); rep("128x128x32 w64x64 (4w)", ms);
-    ms = run<128, 128, 32, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
-    ms = run<128, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("128x128x16 w64x64 (4w)", ms);
-    ms = run<128, 128, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
-    ms = run<256, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("256x256x16 w64x64 (16w)", ms);
-    ms = run<256, 256, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("  same, no store", ms);
-    CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(bias)); CK(hipFree(Y0)); CK(hipFree(Y));
+    double ms;
+    ms = run<MODE_F32, 256, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("f32 256x128x16 (8w)", ms, true);
+    ms = run<MODE_X6, 256, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x128x16 (8w)", ms, true);
+    ms = run<MODE_X6, 256, 128, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("x6  256x128x16 no store", ms, false);
+    ms = run<MODE_X6, 128, 128, 32, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x128x32 (4w)", ms, true);
+    ms = run<MODE_X6, 128, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x256x16 (8w)", ms, true);
+    ms = run<MODE_X6, 128, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x128x16 (4w)", ms, true);
+    ms = run<MODE_X6, 256, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x256x16 (16w)", ms, true);
+    ms = run<MODE_X6, 128, 128, 32, 64, 32>(s, A, W, bias, Y, it); rep("x6  128x128x32 w64x32 (8w)", ms, true);
+    CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(bias)); CK(hipFree(Y)); CK(hipFree(Yr)); CK(hipFree(Sr));
   }
   return 0;
 }

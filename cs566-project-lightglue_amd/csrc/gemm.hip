@@ -32,9 +32,6 @@
 
 namespace lg {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-
 enum GemmMode { MODE_F32 = 0, MODE_X6 = 1 };
 
 __device__ __forceinline__ int xcd_remap(int id, int n) {
@@ -56,14 +53,6 @@ __device__ __forceinline__ void head_row_base(const HeadLayout& hl, int row, int
     base = hl.B * hl.H * hl.M * kHeadDim + (b * hl.H * hl.N + n) * kHeadDim;
     stride = hl.N * kHeadDim;
   }
-}
-
-// Exact split x = h + m + l into bf16 pieces (round-to-nearest-even each).
-__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
-  h = (__bf16)x;
-  const float r = x - (float)h;  // exact
-  m = (__bf16)r;
-  l = (__bf16)(r - (float)m);   // exact subtraction, rounded once
 }
 
 template <int MODE, int BM, int BN, int BK>
@@ -222,16 +211,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            f32x16 c = acc[i][j];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);
-            acc[i][j] = c;
-          }
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = mfma_x6(a[i][0], a[i][1], a[i][2], b[j][0], b[j][1], b[j][2], acc[i][j]);
       }
     }
   };

@@ -43,10 +43,16 @@ __global__ void ref_attn(const float* Q, const float* K, const float* V, float* 
   for (int d = 0; d < 64; ++d) O[((size_t)b * N + q) * 256 + h * 64 + d] = (float)(o[d] / l);
 }
 
-template <int W, int KT>
+template <int X6, int W, int KT>
+hipError_t launch_any(const AttnSet& a0, const AttnSet& a1, int B, int H, float scale) {
+  if (X6) return attention_x6_launch<W, KT>(a0, a1, B, H, scale, 0);
+  return attention_launch<W, KT>(a0, a1, B, H, scale, 0);
+}
+
+template <int X6, int W, int KT>
 void run(const char* name, const AttnSet& a0, const AttnSet& a1, int B, int H, float scale, float* Oref, float* O, size_t on) {
   CK(hipMemset(O, 0, on * 4));
-  CK((attention_launch<W, KT>(a0, a1, B, H, scale, 0)));
+  CK((launch_any<X6, W, KT>(a0, a1, B, H, scale)));
   CK(hipDeviceSynchronize());
   std::vector<float> x(on), y(on);
   CK(hipMemcpy(x.data(), O, on * 4, hipMemcpyDeviceToHost));
@@ -57,13 +63,13 @@ void run(const char* name, const AttnSet& a0, const AttnSet& a1, int B, int H, f
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int it = 10;
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < it; ++i) CK((attention_launch<W, KT>(a0, a1, B, H, scale, 0)));
+  for (int i = 0; i < it; ++i) CK((launch_any<X6, W, KT>(a0, a1, B, H, scale)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= it;
-  const double fl = 2.0 * 4.0 * 64.0 * H * B * ((double)a0.Nq * a0.Nk + (double)a1.Nq * a1.Nk);
+  const double fl = 4.0 * 64.0 * H * B * ((double)a0.Nq * a0.Nk + (double)a1.Nq * a1.Nk);
   printf("%-22s %8.1f us  %6.1f TF/s  maxdiff(set0 vs fp64) %.2e\n", name, ms * 1e3, fl / ms / 1e9, md);
 }
 
@@ -82,10 +88,10 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   AttnSet a0{Q, K, V, O, N, N}, a1{Q + n, K + n, V + n, O + (size_t)B * N * 256, N, N};
   const size_t on = (size_t)B * N * 256;  // compare set 0
-  run<4, 64>("w4 kt64", a0, a1, B, H, scale, Oref, O, on);
-  run<4, 128>("w4 kt128", a0, a1, B, H, scale, Oref, O, on);
-  run<8, 64>("w8 kt64", a0, a1, B, H, scale, Oref, O, on);
-  run<8, 128>("w8 kt128", a0, a1, B, H, scale, Oref, O, on);
-  run<2, 64>("w2 kt64", a0, a1, B, H, scale, Oref, O, on);
+  run<0, 8, 64>("f32 w8 kt64", a0, a1, B, H, scale, Oref, O, on);
+  run<1, 8, 64>("x6  w8 kt64", a0, a1, B, H, scale, Oref, O, on);
+  run<1, 4, 64>("x6  w4 kt64", a0, a1, B, H, scale, Oref, O, on);
+  run<1, 8, 32>("x6  w8 kt32", a0, a1, B, H, scale, Oref, O, on);
+  run<1, 4, 32>("x6  w4 kt32", a0, a1, B, H, scale, Oref, O, on);
   return 0;
 }

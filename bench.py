@@ -31,7 +31,27 @@ from lightglue_amd import LightGlue  # noqa: E402
 from lightglue_amd.weights import synthetic_state_dict  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
+# The hot kernels compute fp32-accurate products as six bf16 MFMA products (bf16x6, DESIGN.md
+# §3), so their fp32-equivalent matrix peak is the bf16 dense peak / 6.
+X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBS = 8000.0
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def measured_traffic(kernel_prefix):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes (tools/profile.sh:
+    separate FETCH_SIZE and WRITE_SIZE runs of this bench; FETCH_SIZE doubled per the gfx950
+    correction in MI355X_MICROARCH.md §HBM).  None if no profile is committed."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    for name, v in t.get("kernels", {}).items():
+        if name.startswith(kernel_prefix):
+            return v.get("hbm_bytes_per_launch"), t.get("source")
+    return None, None
 
 
 def gpu_pairs(B, N, dim, seed, device, size=(640.0, 640.0)):
@@ -147,6 +167,7 @@ def main():
 
     pairs = B * args.steps * world
     value = pairs / el
+    traffic, traffic_src = measured_traffic("lg::attention_x6_kernel")
     result = {
         "metric": "image-pairs/sec at N=2048 kpts, d=256; HPatches AUC@3px parity",
         "value": round(value, 3),
@@ -167,13 +188,15 @@ def main():
         },
         "achieved_tflops_total": round(total_flops_per_pair(N) * pairs / el / 1e12, 2),
         "roofline": {
-            "kernel": "attention_f32_kernel (flash self/cross attention, f32 MFMA 32x32x2)",
+            "kernel": "lg::attention_x6_kernel (flash self/cross attention, bf16x6 on v_mfma_f32_32x32x16_bf16)",
             "bound": "mfma",
             "achieved": round(att_fl / (att_ms * 1e-3) / 1e12, 2) if att_ms > 0 else None,
-            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "peak": round(X6_PEAK_TFLOPS, 1),
+            "peak_note": "fp32-equivalent: bf16 dense 2500 TF/s / 6 products per fp32 product (fp32 MFMA peak is 157.3)",
             "unit": "TFLOP/s",
-            "frac": round(att_fl / (att_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4) if att_ms > 0 else None,
-            "traffic": None,
+            "frac": round(att_fl / (att_ms * 1e-3) / 1e12 / X6_PEAK_TFLOPS, 4) if att_ms > 0 else None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "launches": att_n,
             "avg_launch_ms": round(att_ms / max(att_n, 1), 4),
             "algorithmic_flops_per_launch": att_fl / max(att_n, 1),

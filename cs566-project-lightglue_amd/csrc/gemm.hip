@@ -58,10 +58,18 @@ __device__ __forceinline__ void head_row_base(const HeadLayout& hl, int row, int
 template <int MODE, int BM, int BN, int BK>
 struct GemmSmem {
   static constexpr int LDF = BK + 4;  // fp32 row stride (floats)
-  static constexpr int LDH = BK + 8;  // bf16 row stride (elements): 20 or 12 dwords for BK 32/16
+  // bf16x6 planes: unpadded BK-element rows of 16-byte chunks, chunk index XOR-swizzled by
+  // swz(row) so that both the ds_write_b128 staging groups and the ds_read_b128 fragment
+  // groups ({0-3,12-15,20-27} rows) hit distinct banks.
   static constexpr size_t bytes =
-      MODE == MODE_F32 ? 2 * (size_t)(BM + BN) * LDF * 4 : 2 * 3 * (size_t)(BM + BN) * LDH * 2;
+      MODE == MODE_F32 ? 2 * (size_t)(BM + BN) * LDF * 4 : 2 * 3 * (size_t)(BM + BN) * BK * 2;
 };
+
+template <int BK>
+__device__ __forceinline__ int chunk_swz(int row) {
+  static_assert(BK == 16 || BK == 32, "bf16x6 tiles are 16 or 32 deep");
+  return BK == 16 ? (row >> 3) & 1 : (row >> 2) & 3;
+}
 
 template <int MODE, int BM, int BN, int BK, int WM, int WN, int EPI>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmArgs args) {
@@ -72,7 +80,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
   constexpr int A_LD = BM * C4 / NT;      // float4 loads per thread per k-tile
   constexpr int B_LD = BN * C4 / NT;
   using SM = GemmSmem<MODE, BM, BN, BK>;
-  static_assert(BM * C4 % NT == 0 && BN * C4 % NT == 0, "tile/threads mismatch");
+  static_assert(MODE != MODE_F32 || (BM * C4 % NT == 0 && BN * C4 % NT == 0), "tile/threads mismatch");
   static_assert(MODE == MODE_F32 || BK % 16 == 0, "bf16x6 needs BK % 16 == 0");
 
   __shared__ __attribute__((aligned(16))) char smem[SM::bytes];
@@ -103,8 +111,38 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
     }
   }
 
+  // bf16x6 staging items: 8 consecutive k of one row (A rows first, then W rows)
+  constexpr int NCH = BK / 8;
+  constexpr int X6_ITEMS = MODE == MODE_X6 ? (BM + BN) * NCH / NT : 1;
+  static_assert(MODE == MODE_F32 || (BM + BN) * NCH % NT == 0, "bf16x6 staging/threads mismatch");
+  f32x4 rx[X6_ITEMS][2];
   f32x4 ra[A_LD], rb[B_LD];
   auto gload = [&](int kt) {
+    if constexpr (MODE == MODE_X6) {
+      const int k0 = kt * BK;
+      const float* src;
+      int ld, kk;
+      if (k0 < args.K0) { src = A0; ld = args.lda0; kk = k0; }
+      else { src = A1; ld = args.lda1; kk = k0 - args.K0; }
+#pragma unroll
+      for (int i = 0; i < X6_ITEMS; ++i) {
+        const int q = tid + i * NT;
+        const float* p;
+        if (q < BM * NCH) {
+          int row = m0 + q / NCH;
+          row = row < args.R ? row : args.R - 1;
+          p = src + (size_t)row * ld + kk + (q % NCH) * 8;
+        } else {
+          const int qb = q - BM * NCH;
+          int col = n0 + qb / NCH;
+          col = col < args.Nout ? col : args.Nout - 1;
+          p = W + (size_t)col * args.ldw + k0 + (qb % NCH) * 8;
+        }
+        rx[i][0] = *reinterpret_cast<const f32x4*>(p);
+        rx[i][1] = *reinterpret_cast<const f32x4*>(p + 4);
+      }
+      return;
+    }
     const int k0 = kt * BK;
     const float* src;
     int ld, kk;
@@ -150,26 +188,29 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
         *reinterpret_cast<f32x4*>(&Bs[(q / C4) * SM::LDF + (q % C4) * 4]) = rb[i];
       }
     } else {
-      // three bf16 planes per operand: plane p of A at [p][BM][LDH], of B at [p][BN][LDH]
-      __bf16* As = reinterpret_cast<__bf16*>(smem) + (size_t)buf * 3 * (BM + BN) * SM::LDH;
-      __bf16* Bs = As + 3 * BM * SM::LDH;
-      auto put = [&](__bf16* base, int rows, int q, const f32x4& v) {
-        bf16x4 h, m, l;
+      // three bf16 planes per operand: plane p of A at [p][BM][BK], of W at [p][BN][BK]
+      __bf16* As = reinterpret_cast<__bf16*>(smem) + (size_t)buf * 3 * (BM + BN) * BK;
+      __bf16* Bs = As + 3 * BM * BK;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          __bf16 a, b, c;
-          split3(v[e], a, b, c);
-          h[e] = a; m[e] = b; l[e] = c;
+      for (int i = 0; i < X6_ITEMS; ++i) {
+        const int q = tid + i * NT;
+        const bool isA = q < BM * NCH;
+        const int qq = isA ? q : q - BM * NCH;
+        const int r = qq / NCH, c = qq % NCH;
+        __bf16* base = isA ? As : Bs;
+        const int rows = isA ? BM : BN;
+        bf16x8 h, m, l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          __bf16 a, b, cc;
+          split3(rx[i][e >> 2][e & 3], a, b, cc);
+          h[e] = a; m[e] = b; l[e] = cc;
         }
-        const int off = (q / C4) * SM::LDH + (q % C4) * 4;
-        *reinterpret_cast<bf16x4*>(base + off) = h;
-        *reinterpret_cast<bf16x4*>(base + rows * SM::LDH + off) = m;
-        *reinterpret_cast<bf16x4*>(base + 2 * rows * SM::LDH + off) = l;
-      };
-#pragma unroll
-      for (int i = 0; i < A_LD; ++i) put(As, BM, tid + i * NT, ra[i]);
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i) put(Bs, BN, tid + i * NT, rb[i]);
+        const int off = r * BK + ((c ^ chunk_swz<BK>(r)) * 8);
+        *reinterpret_cast<bf16x8*>(base + off) = h;
+        *reinterpret_cast<bf16x8*>(base + rows * BK + off) = m;
+        *reinterpret_cast<bf16x8*>(base + 2 * rows * BK + off) = l;
+      }
     }
   };
   auto compute = [&](int buf) {
@@ -194,19 +235,24 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
             for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][kk], b[j][kk], acc[i][j]);
       }
     } else {
-      const __bf16* as = reinterpret_cast<const __bf16*>(smem) + (size_t)buf * 3 * (BM + BN) * SM::LDH;
-      const __bf16* bs = as + 3 * BM * SM::LDH;
+      const __bf16* as = reinterpret_cast<const __bf16*>(smem) + (size_t)buf * 3 * (BM + BN) * BK;
+      const __bf16* bs = as + 3 * BM * BK;
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
         bf16x8 a[TM][3], b[TN][3];
+        const int c = 2 * s + half;
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
-            a[i][p] = *reinterpret_cast<const bf16x8*>(as + (p * BM + wm0 + i * 32 + l32) * SM::LDH + s * 16 + half * 8);
+          for (int i = 0; i < TM; ++i) {
+            const int r = wm0 + i * 32 + l32;
+            a[i][p] = *reinterpret_cast<const bf16x8*>(as + (p * BM + r) * BK + (c ^ chunk_swz<BK>(r)) * 8);
+          }
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            b[j][p] = *reinterpret_cast<const bf16x8*>(bs + (p * BN + wn0 + j * 32 + l32) * SM::LDH + s * 16 + half * 8);
+          for (int j = 0; j < TN; ++j) {
+            const int r = wn0 + j * 32 + l32;
+            b[j][p] = *reinterpret_cast<const bf16x8*>(bs + (p * BN + r) * BK + (c ^ chunk_swz<BK>(r)) * 8);
+          }
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -261,15 +307,21 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
     }
   } else {
     // Head-major scatter.  WN == 64 and n0 + wn0 is a multiple of 64, so the wave owns one
-    // (type, head) block: type t = col / 256, head = (col % 256) / 64, stored dim = j*32 + l32.
+    // (type t, head) block.  The packed weight rows (lightglue_api.cpp: head_perm) put dims
+    // 2*l32 (tile 0) and 2*l32+1 (tile 1) of the head in lane l32, so every store is a
+    // natural-order pair and the rotary partners meet in one lane.
+    //   self  (EPI_QKV_ROT):   t0 -> q fp32 (rotary), t1 -> k bf16 planes (rotary), t2 -> v planes
+    //   cross (EPI_CROSS_QKV): t0 -> qk fp32 * scale^0.5 and qk planes,             t1 -> v planes
     static_assert(WN == 64 && TN == 2, "head epilogues need 64-wide wave tiles");
     const HeadLayout& hl = args.hl;
     const int cbase = n0 + wn0;
     const int t = cbase / kDim, head = (cbase % kDim) / kHeadDim;
-    float* dst = t == 0 ? hl.q : (t == 1 ? hl.k : hl.v);
-    float b2[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) b2[j] = args.bias[cbase + j * 32 + l32];
+    const bool rot = EPI == EPI_QKV_ROT && t < 2;
+    const bool to_q = t == 0;
+    const bool to_kp = EPI == EPI_QKV_ROT ? t == 1 : t == 0;
+    const bool to_vp = EPI == EPI_QKV_ROT ? t == 2 : t == 1;
+    const float sc = (EPI == EPI_CROSS_QKV && t == 0) ? hl.qk_scale : 1.f;
+    const float be = args.bias[cbase + l32], bo = args.bias[cbase + 32 + l32];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -277,24 +329,30 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
         const int lr = wm0 + i * 32 + row32(r, half);
         const int row = m0 + lr;
         if (row >= args.R) continue;
-        const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1];
-        if constexpr (EPI == EPI_QKV_ROT) {
-          const float xe = acc[i][0][r] + b2[0];  // dim 2*l32   (even)
-          const float xo = acc[i][1][r] + b2[1];  // dim 2*l32+1 (odd)
-          if (t < 2) {
-            // t*cos + rotate_half(t)*sin, rotate_half(x)[2i] = -x[2i+1], [2i+1] = x[2i]
-            const float c = hl.cosb[(size_t)row * kFreq + l32];
-            const float s = hl.sinb[(size_t)row * kFreq + l32];
-            dst[off + l32] = add_rn(mul_rn(xe, c), mul_rn(-xo, s));
-            dst[off + 32 + l32] = add_rn(mul_rn(xo, c), mul_rn(xe, s));
-          } else {
-            dst[off + l32] = xe;
-            dst[off + 32 + l32] = xo;
-          }
-        } else {  // EPI_CROSS_QKV
-          const float sc = t == 0 ? hl.qk_scale : 1.f;
-#pragma unroll
-          for (int j = 0; j < TN; ++j) dst[off + j * 32 + l32] = (acc[i][j][r] + b2[j]) * sc;
+        const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + 2 * l32;
+        float xe = acc[i][0][r] + be;  // dim 2*l32   (even)
+        float xo = acc[i][1][r] + bo;  // dim 2*l32+1 (odd)
+        if (rot) {
+          // t*cos + rotate_half(t)*sin, rotate_half(x)[2i] = -x[2i+1], [2i+1] = x[2i]
+          const float c = hl.cosb[(size_t)row * kFreq + l32];
+          const float s = hl.sinb[(size_t)row * kFreq + l32];
+          const float e2 = add_rn(mul_rn(xe, c), mul_rn(-xo, s));
+          const float o2 = add_rn(mul_rn(xo, c), mul_rn(xe, s));
+          xe = e2;
+          xo = o2;
+        }
+        xe *= sc;
+        xo *= sc;
+        if (to_q) *reinterpret_cast<float2*>(hl.q + off) = make_float2(xe, xo);
+        if (to_kp || to_vp) {
+          __bf16* base = to_kp ? hl.kp : hl.vp;
+          __bf16 eh, em, el, oh, om, ol;
+          split3(xe, eh, em, el);
+          split3(xo, oh, om, ol);
+          typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<bf16x2*>(base + off) = bf16x2{eh, oh};
+          *reinterpret_cast<bf16x2*>(base + hl.pstride + off) = bf16x2{em, om};
+          *reinterpret_cast<bf16x2*>(base + 2 * hl.pstride + off) = bf16x2{el, ol};
         }
       }
   }

@@ -7,12 +7,16 @@ namespace lg {
 
 enum EpiKind { EPI_STORE = 0, EPI_QKV_ROT = 1, EPI_CROSS_QKV = 2, EPI_PROBE = 3 /* benchmarking only */ };
 
-// Head-major destination [set][b][h][n][64] for the QKV epilogues; set 0 = image 0 (B*M rows),
-// set 1 = image 1 (B*N rows), rows in GEMM order (image 0 rows first).
+// Head-major destinations [set][b][h][n][64] for the QKV epilogues; set 0 = image 0 (B*M rows),
+// set 1 = image 1 (B*N rows), rows in GEMM order (image 0 rows first).  All in natural dim order.
+//   q   fp32 queries (self) / qk (cross)
+//   kp  keys as three bf16 planes (bf16x6 split, plane p at kp + p*pstride): k (self) / qk (cross)
+//   vp  values as three bf16 planes
 struct HeadLayout {
   float* q;
-  float* k;
-  float* v;
+  __bf16* kp;
+  __bf16* vp;
+  long long pstride;  // elements between planes (= B*(M+N)*H*64)
   int B, H, M, N;
   const float* cosb;  // [rows][32] rotary cos table, by GEMM row
   const float* sinb;
@@ -42,10 +46,11 @@ hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, hipStream_t st);
 // Attention over head-major Q/K/V ([set][b][h][n][64]); O written row-major into ctx
 // [rows][256] at column h*64 (rows in GEMM order).  Two "sets" per launch (blockIdx.z).
 struct AttnSet {
-  const float* q;  // [B][H][Nq][64]
-  const float* k;  // [B][H][Nk][64]
-  const float* v;  // [B][H][Nk][64]
-  float* o;        // ctx + row_base*256
+  const float* q;    // [B][H][Nq][64] fp32
+  const __bf16* kp;  // [3 planes][B][H][Nk][64] bf16 (plane stride pstride)
+  const __bf16* vp;  // [3 planes][B][H][Nk][64] bf16
+  long long pstride;
+  float* o;          // ctx + row_base*256
   int Nq, Nk;
 };
 hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st);

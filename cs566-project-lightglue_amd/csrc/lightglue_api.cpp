@@ -111,12 +111,14 @@ struct lg_handle {
   int device;
   std::vector<Tensor> schema;
   std::map<std::string, int> index;
-  // where each schema tensor goes: destination offset (floats), or gather for Wqkv
+  // where each schema tensor goes: destination offset (floats) and how (0 copy, 1 gather rows
+  // through perm[0,768) (Wqkv), 2 gather through perm[768,1024) (to_qk / to_v))
   std::vector<size_t> dst;
+  std::vector<int> gkind;
   std::vector<LayerW> layers;
   size_t Wr, Wc, bc, Wi, bi, total;
   float* wbuf = nullptr;
-  int* perm = nullptr;  // Wqkv row permutation [768]
+  int* perm = nullptr;  // head_perm() [1024]
   bool loaded = false;
   // fold out_proj / to_out into ffn.0 at load time (env LG_FOLD_OUT_PROJ=0 disables)
   bool fold = true;
@@ -156,17 +158,20 @@ struct lg_handle {
 
 namespace {
 
-// Packed Wqkv row order: c' = t*256 + h*64 + j ; for q,k (t<2) j<32 -> dim 2j, j>=32 -> dim
-// 2(j-32)+1 (rotary partners in the same lane of the GEMM tile); v keeps natural dims.
-// Reference layout (lightglue.py:185): row = h*192 + dim*3 + t.
-std::vector<int> wqkv_perm(int H) {
-  std::vector<int> p(3 * D);
+// Packed projection row order c' = t*256 + h*64 + j with j < 32 -> dim 2j, j >= 32 -> dim
+// 2(j-32)+1: lane l32 of a 64-wide GEMM wave tile then holds the natural-order dim pair
+// (2*l32, 2*l32+1) -- the rotary partners -- so the epilogue stores pairs (gemm.hip).
+//   perm[0, 768):    Wqkv, reference layout row = h*192 + dim*3 + t (lightglue.py:185)
+//   perm[768, 1024): to_qk / to_v, reference layout row = h*64 + dim (lightglue.py:226)
+constexpr int kPermCross = 3 * D;
+std::vector<int> head_perm(int H) {
+  std::vector<int> p(4 * D);
+  auto dim = [](int j) { return j < 32 ? 2 * j : 2 * (j - 32) + 1; };
   for (int t = 0; t < 3; ++t)
     for (int h = 0; h < H; ++h)
-      for (int j = 0; j < 64; ++j) {
-        const int dim = t < 2 ? (j < 32 ? 2 * j : 2 * (j - 32) + 1) : j;
-        p[t * D + h * 64 + j] = h * 192 + dim * 3 + t;
-      }
+      for (int j = 0; j < 64; ++j) p[t * D + h * 64 + j] = h * 192 + dim(j) * 3 + t;
+  for (int h = 0; h < H; ++h)
+    for (int j = 0; j < 64; ++j) p[kPermCross + h * 64 + j] = h * 64 + dim(j);
   return p;
 }
 
@@ -209,8 +214,9 @@ void plan_layout(lg_handle* h) {
   }
   h->total = off;
 
-  // destination of each schema tensor (Wqkv weight/bias are gathered, marked by SIZE_MAX-1/-2)
+  // destination of each schema tensor (projection weights are gathered through head_perm)
   h->dst.assign(h->schema.size(), SIZE_MAX);
+  h->gkind.assign(h->schema.size(), 0);
   for (size_t k = 0; k < h->schema.size(); ++k) {
     const std::string& n = h->schema[k].name;
     size_t o = SIZE_MAX;
@@ -228,11 +234,12 @@ void plan_layout(lg_handle* h) {
         const bool self = r.rfind("self_attn.", 0) == 0;
         BlockW& w = self ? lw.self : lw.cross;
         const std::string f = r.substr(r.find('.') + 1);
-        if (f == "Wqkv.weight" || f == "Wqkv.bias") o = SIZE_MAX - 1;  // gathered
-        else if (f == "to_qk.weight") o = w.Wqkv;
-        else if (f == "to_qk.bias") o = w.bqkv;
-        else if (f == "to_v.weight") o = w.Wqkv + (size_t)D * D;
-        else if (f == "to_v.bias") o = w.bqkv + D;
+        if (f == "Wqkv.weight") { o = w.Wqkv; h->gkind[k] = 1; }
+        else if (f == "Wqkv.bias") { o = w.bqkv; h->gkind[k] = 1; }
+        else if (f == "to_qk.weight") { o = w.Wqkv; h->gkind[k] = 2; }
+        else if (f == "to_qk.bias") { o = w.bqkv; h->gkind[k] = 2; }
+        else if (f == "to_v.weight") { o = w.Wqkv + (size_t)D * D; h->gkind[k] = 2; }
+        else if (f == "to_v.bias") { o = w.bqkv + D; h->gkind[k] = 2; }
         else if (f == "out_proj.weight" || f == "to_out.weight") o = w.Wo;
         else if (f == "out_proj.bias" || f == "to_out.bias") o = w.bo;
         else if (f == "ffn.0.weight") o = w.W1;
@@ -260,7 +267,9 @@ void plan_layout(lg_handle* h) {
 
 // ------------------------------------------------------------------ forward workspace
 struct Work {
-  float *X, *X2, *cosb, *sinb, *cos2, *sin2, *size, *Q, *K, *V, *ctx, *msg, *H1, *md, *z, *tok, *sim, *aws;
+  float *X, *X2, *cosb, *sinb, *cos2, *sin2, *size, *Q, *ctx, *msg, *H1, *md, *z, *tok, *sim, *aws;
+  __bf16 *KP, *VP;  // bf16x6 planes of keys (qk) and values: 3 x R x 256
+  size_t R;
   int *flags, *pos, *ind0, *ind1, *ind0b, *ind1b, *counts;
   int64_t *m0c, *m1c;
   float *s0c, *s1c;
@@ -282,9 +291,10 @@ Work carve(char* base, int B, int M, int N, bool prune) {
   w.cosb = tf(R * 32);
   w.sinb = tf(R * 32);
   w.size = tf(4 * (size_t)B);
+  w.R = R;
   w.Q = tf(R * D);
-  w.K = tf(R * D);
-  w.V = tf(R * D);
+  w.KP = reinterpret_cast<__bf16*>(take(3 * R * D * 2));
+  w.VP = reinterpret_cast<__bf16*>(take(3 * R * D * 2));
   w.ctx = tf(R * D);
   w.msg = tf(R * D);
   w.H1 = tf(R * 2 * D);
@@ -356,9 +366,9 @@ int lg_create(const lg_config_t* cfg, int device, lg_handle_t** out) {
       return fail(LG_E_WEIGHTS, "internal: unplaced schema tensor " + n);
     }
   hipError_t e = hipMalloc(&h->wbuf, h->total * sizeof(float));
-  if (e == hipSuccess) e = hipMalloc(&h->perm, 3 * D * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&h->perm, 4 * D * sizeof(int));
   if (e == hipSuccess) {
-    auto p = wqkv_perm(cfg->num_heads);
+    auto p = head_perm(cfg->num_heads);
     e = hipMemcpy(h->perm, p.data(), p.size() * sizeof(int), hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) e = hipMemset(h->wbuf, 0, h->total * sizeof(float));
@@ -414,13 +424,12 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
   for (int i = 0; i < n; ++i) {
     const int k = h->index[names[i]];
     const std::string& name = h->schema[k].name;
-    if (h->dst[k] == SIZE_MAX - 1) {
-      int li = -1;
-      sscanf(name.c_str(), "transformers.%d.", &li);
+    if (h->gkind[k] != 0) {
       const bool is_w = name.size() > 6 && name.compare(name.size() - 6, 6, "weight") == 0;
-      float* dst = h->wbuf + (is_w ? h->layers[li].self.Wqkv : h->layers[li].self.bqkv);
-      hipError_t e = lg::gather_rows(dst, tensors[i], h->perm, 3 * D, is_w ? D : 1, st);
-      if (e != hipSuccess) return fail(LG_E_HIP, std::string("gather Wqkv: ") + hipGetErrorString(e));
+      const int rows = h->gkind[k] == 1 ? 3 * D : D;
+      const int* perm = h->perm + (h->gkind[k] == 1 ? 0 : kPermCross);
+      hipError_t e = lg::gather_rows(h->wbuf + h->dst[k], tensors[i], perm, rows, is_w ? D : 1, st);
+      if (e != hipSuccess) return fail(LG_E_HIP, std::string("gather ") + name + ": " + hipGetErrorString(e));
     } else {
       LG_HIP(hipMemcpyAsync(h->wbuf + h->dst[k], tensors[i], numels[i] * sizeof(float), hipMemcpyDeviceToDevice, st));
     }
@@ -548,18 +557,19 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
       g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wqkv; g.ldw = D; g.bias = Wb + bw.bqkv;
       g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D;
       g.hl.B = B; g.hl.H = H; g.hl.M = M; g.hl.N = N; g.hl.cosb = w.cosb; g.hl.sinb = w.sinb;
-      g.hl.q = w.Q; g.hl.k = w.K; g.hl.v = w.V;
+      g.hl.q = w.Q; g.hl.kp = w.KP; g.hl.vp = w.VP; g.hl.pstride = (long long)w.R * D;
       g.hl.qk_scale = std::sqrt(1.f / std::sqrt(64.f));  // scale**0.5 (lightglue.py:235)
       LG_HIP(gemm(g, blk == 0 ? EPI_QKV_ROT : EPI_CROSS_QKV, 1));
       const size_t img1 = (size_t)B * H * M * 64;
+      const long long ps = (long long)w.R * D;
       AttnSet a0, a1;
       if (blk == 0) {  // self: q/k/v of the same image, scale 1/sqrt(64) (SDPA default)
-        a0 = {w.Q, w.K, w.V, w.ctx, M, M};
-        a1 = {w.Q + img1, w.K + img1, w.V + img1, w.ctx + (size_t)B * M * D, N, N};
+        a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M};
+        a1 = {w.Q + img1, w.KP + img1, w.VP + img1, ps, w.ctx + (size_t)B * M * D, N, N};
         LG_HIP(attn(a0, a1, 0.125f, false));
-      } else {  // cross: QK in w.Q, V in w.K (t=1 of the 512-wide GEMM)
-        a0 = {w.Q, w.Q + img1, w.K + img1, w.ctx, M, N};
-        a1 = {w.Q + img1, w.Q, w.K, w.ctx + (size_t)B * M * D, N, M};
+      } else {  // cross: qk fp32 in w.Q and as planes in w.KP, v planes in w.VP
+        a0 = {w.Q, w.KP + img1, w.VP + img1, ps, w.ctx, M, N};
+        a1 = {w.Q + img1, w.KP, w.VP, ps, w.ctx + (size_t)B * M * D, N, M};
         LG_HIP(attn(a0, a1, 1.0f, true));
       }
       // out projection (skipped when folded into ffn.0 at load time: ffn.0 then reads ctx)

@@ -1,5 +1,5 @@
 // Micro-benchmark of attention variants (tools only; not shipped).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/kbench_attn.hip -o /tmp/ka && /tmp/ka
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/kbench_attn.hip -o /tmp/ka && /tmp/ka [N]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -16,6 +16,15 @@ __global__ void fill(float* p, size_t n, unsigned seed, float scale) {
     unsigned x = (unsigned)(i * 2654435761u) ^ seed;
     x ^= x >> 13; x *= 0x5bd1e995; x ^= x >> 15;
     p[i] = (((x & 0xffffff) / 16777216.0f) * 2.f - 1.f) * scale;
+  }
+}
+
+__global__ void split_planes(const float* x, __bf16* p, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < n) {
+    __bf16 h, m, l;
+    split3(x[i], h, m, l);
+    p[i] = h; p[n + i] = m; p[2 * n + i] = l;
   }
 }
 
@@ -43,16 +52,16 @@ __global__ void ref_attn(const float* Q, const float* K, const float* V, float* 
   for (int d = 0; d < 64; ++d) O[((size_t)b * N + q) * 256 + h * 64 + d] = (float)(o[d] / l);
 }
 
-template <int X6, int W, int KT>
+template <int P, int W, int KT>
 hipError_t launch_any(const AttnSet& a0, const AttnSet& a1, int B, int H, float scale) {
-  if (X6) return attention_x6_launch<W, KT>(a0, a1, B, H, scale, 0);
-  return attention_launch<W, KT>(a0, a1, B, H, scale, 0);
+  if (P) return attention_x6p_launch<W, KT>(a0, a1, B, H, scale, 0);
+  return attention_x6_launch<W, KT>(a0, a1, B, H, scale, 0);
 }
 
-template <int X6, int W, int KT>
+template <int P, int W, int KT>
 void run(const char* name, const AttnSet& a0, const AttnSet& a1, int B, int H, float scale, float* Oref, float* O, size_t on) {
   CK(hipMemset(O, 0, on * 4));
-  CK((launch_any<X6, W, KT>(a0, a1, B, H, scale)));
+  CK((launch_any<P, W, KT>(a0, a1, B, H, scale)));
   CK(hipDeviceSynchronize());
   std::vector<float> x(on), y(on);
   CK(hipMemcpy(x.data(), O, on * 4, hipMemcpyDeviceToHost));
@@ -63,7 +72,7 @@ void run(const char* name, const AttnSet& a0, const AttnSet& a1, int B, int H, f
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int it = 10;
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < it; ++i) CK((launch_any<X6, W, KT>(a0, a1, B, H, scale)));
+  for (int i = 0; i < it; ++i) CK((launch_any<P, W, KT>(a0, a1, B, H, scale)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -77,21 +86,24 @@ int main(int argc, char** argv) {
   const int B = 32, H = 4, N = argc > 1 ? atoi(argv[1]) : 2048;
   const size_t n = (size_t)B * H * N * 64;
   float *Q, *K, *V, *O, *Oref;
+  __bf16 *KP, *VP;
   CK(hipMalloc(&Q, 2 * n * 4)); CK(hipMalloc(&K, 2 * n * 4)); CK(hipMalloc(&V, 2 * n * 4));
+  CK(hipMalloc(&KP, 3 * 2 * n * 2)); CK(hipMalloc(&VP, 3 * 2 * n * 2));
   CK(hipMalloc(&O, 2 * n * 4)); CK(hipMalloc(&Oref, 2 * n * 4));
   fill<<<(2 * n + 255) / 256, 256>>>(Q, 2 * n, 1, 2.f);
   fill<<<(2 * n + 255) / 256, 256>>>(K, 2 * n, 2, 2.f);
   fill<<<(2 * n + 255) / 256, 256>>>(V, 2 * n, 3, 1.f);
+  split_planes<<<(2 * n + 255) / 256, 256>>>(K, KP, 2 * n);
+  split_planes<<<(2 * n + 255) / 256, 256>>>(V, VP, 2 * n);
   const float scale = 0.125f;
-  // reference for set 0 only (rows [0, B*N) of O)
   ref_attn<<<(B * H * N + 127) / 128, 128>>>(Q, K, V, Oref, B * H, H, N, scale);
   CK(hipDeviceSynchronize());
-  AttnSet a0{Q, K, V, O, N, N}, a1{Q + n, K + n, V + n, O + (size_t)B * N * 256, N, N};
+  const long long ps = 2 * (long long)n;
+  AttnSet a0{Q, KP, VP, ps, O, N, N}, a1{Q + n, KP + n, VP + n, ps, O + (size_t)B * N * 256, N, N};
   const size_t on = (size_t)B * N * 256;  // compare set 0
-  run<0, 8, 64>("f32 w8 kt64", a0, a1, B, H, scale, Oref, O, on);
-  run<1, 8, 64>("x6  w8 kt64", a0, a1, B, H, scale, Oref, O, on);
-  run<1, 4, 64>("x6  w4 kt64", a0, a1, B, H, scale, Oref, O, on);
-  run<1, 8, 32>("x6  w8 kt32", a0, a1, B, H, scale, Oref, O, on);
-  run<1, 4, 32>("x6  w4 kt32", a0, a1, B, H, scale, Oref, O, on);
+  run<0, 8, 64>("x6  w8 kt64", a0, a1, B, H, scale, Oref, O, on);
+  run<1, 8, 64>("x6p w8 kt64", a0, a1, B, H, scale, Oref, O, on);
+  run<1, 4, 32>("x6p w4 kt32", a0, a1, B, H, scale, Oref, O, on);
+  run<1, 4, 64>("x6p w4 kt64", a0, a1, B, H, scale, Oref, O, on);
   return 0;
 }

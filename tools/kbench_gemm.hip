@@ -83,13 +83,12 @@ int main() {
     const int it = 20;
     double ms;
     ms = run<MODE_F32, 256, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("f32 256x128x16 (8w)", ms, true);
-    ms = run<MODE_X6, 256, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x128x16 (8w)", ms, true);
-    ms = run<MODE_X6, 256, 128, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("x6  256x128x16 no store", ms, false);
-    ms = run<MODE_X6, 128, 128, 32, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x128x32 (4w)", ms, true);
-    ms = run<MODE_X6, 128, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x256x16 (8w)", ms, true);
-    ms = run<MODE_X6, 128, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x128x16 (4w)", ms, true);
     ms = run<MODE_X6, 256, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x256x16 (16w)", ms, true);
-    ms = run<MODE_X6, 128, 128, 32, 64, 32>(s, A, W, bias, Y, it); rep("x6  128x128x32 w64x32 (8w)", ms, true);
+    ms = run<MODE_X6, 256, 256, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("x6  256x256x16 no store", ms, false);
+    ms = run<MODE_X6, 128, 256, 32, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x256x32 (8w)", ms, true);
+    ms = run<MODE_X6, 256, 128, 32, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x128x32 (8w)", ms, true);
+    ms = run<MODE_X6, 128, 128, 32, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x128x32 (4w)", ms, true);
+    ms = run<MODE_X6, 256, 256, 16, 64, 128>(s, A, W, bias, Y, it); rep("x6  256x256x16 w64x128 (8w)", ms, true);
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(bias)); CK(hipFree(Y)); CK(hipFree(Yr)); CK(hipFree(Sr));
   }
   return 0;

@@ -32,9 +32,15 @@ from lightglue_amd.weights import synthetic_state_dict  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
-# The hot kernels compute fp32-accurate products as six bf16 MFMA products (bf16x6, DESIGN.md
-# §3), so their fp32-equivalent matrix peak is the bf16 dense peak / 6.
-X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
+# The hot kernels compute fp32-accurate products as three fp16 MFMA products (fp16x3, the default)
+# or six bf16 ones (bf16x6, the guarded fallback), so their fp32-equivalent matrix
+# peak is the fp16/bf16 dense peak / 3 (or / 6).
+PEAKS = {
+    "fp16x3": (BF16_MFMA_PEAK_TFLOPS / 3.0, "lg::attention_h3_kernel",
+               "fp32-equivalent: fp16 dense 2500 TF/s / 3 fp16 products per fp32 product (fp32 MFMA peak is 157.3)"),
+    "bf16x6": (BF16_MFMA_PEAK_TFLOPS / 6.0, "lg::attention_x6_kernel",
+               "fp32-equivalent: bf16 dense 2500 TF/s / 6 bf16 products per fp32 product (fp32 MFMA peak is 157.3)"),
+}
 HBM_PEAK_GBS = 8000.0
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
 
@@ -113,6 +119,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="pairs per GPU per step")
     ap.add_argument("--npts", type=int, default=2048)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work (0 = skip)")
+    ap.add_argument("--precision", default="auto", choices=["auto", "bf16x6"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,7 +133,7 @@ def main():
     device = torch.device("cuda", local)
 
     conf = {"filter_threshold": 0.1}
-    model = LightGlue(conf).eval().to(device)
+    model = LightGlue({**conf, "precision": args.precision}).eval().to(device)
     sd = synthetic_state_dict(conf, seed=0)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     B, N = args.batch, args.npts
@@ -167,7 +174,9 @@ def main():
 
     pairs = B * args.steps * world
     value = pairs / el
-    traffic, traffic_src = measured_traffic("lg::attention_x6_kernel")
+    prec = model.last_precision_used
+    peak, kname, peak_note = PEAKS[prec]
+    traffic, traffic_src = measured_traffic(kname)
     result = {
         "metric": "image-pairs/sec at N=2048 kpts, d=256; HPatches AUC@3px parity",
         "value": round(value, 3),
@@ -185,16 +194,17 @@ def main():
             "workload": "configs[2]: SuperPoint+LightGlue N=2048, 9 layers, no pruning, batch=32 per GPU",
             "npts": N, "descriptor_dim": 256, "n_layers": 9, "pairs_per_gpu_per_step": B,
             "global_batch": B * world, "parallelism": f"pair-sharded x{world} (+RCCL all-gather of matches)",
+            "matrix_operands": prec,
         },
         "achieved_tflops_total": round(total_flops_per_pair(N) * pairs / el / 1e12, 2),
         "roofline": {
-            "kernel": "lg::attention_x6_kernel (flash self/cross attention, bf16x6 on v_mfma_f32_32x32x16_bf16)",
+            "kernel": f"{kname} (flash self/cross attention, {prec} fp32-accurate products)",
             "bound": "mfma",
             "achieved": round(att_fl / (att_ms * 1e-3) / 1e12, 2) if att_ms > 0 else None,
-            "peak": round(X6_PEAK_TFLOPS, 1),
-            "peak_note": "fp32-equivalent: bf16 dense 2500 TF/s / 6 products per fp32 product (fp32 MFMA peak is 157.3)",
+            "peak": round(peak, 1),
+            "peak_note": peak_note,
             "unit": "TFLOP/s",
-            "frac": round(att_fl / (att_ms * 1e-3) / 1e12 / X6_PEAK_TFLOPS, 4) if att_ms > 0 else None,
+            "frac": round(att_fl / (att_ms * 1e-3) / 1e12 / peak, 4) if att_ms > 0 else None,
             "traffic": traffic,
             "traffic_source": traffic_src,
             "launches": att_n,

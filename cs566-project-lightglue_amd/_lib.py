@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LIGHTGLUE_MI355X_LIB", os.path.join(_HERE, "liblightglue_mi355x.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE = 0, -1, -2, -3, -4
 
@@ -32,6 +32,8 @@ EXPORTED_SYMBOLS = [
     "lg_profile_read",
 ]
 KERNEL_IDS = {"attention": 0, "gemm": 1, "assign": 2}
+# lg_config_t.precision (include/lightglue_mi355x.h): "auto" = fp16x3 with a guarded bf16x6 rerun
+PRECISIONS = {"auto": 0, "bf16x6": 1}
 
 
 class LGConfig(ctypes.Structure):
@@ -44,6 +46,7 @@ class LGConfig(ctypes.Structure):
         ("depth_confidence", ctypes.c_double),
         ("width_confidence", ctypes.c_double),
         ("filter_threshold", ctypes.c_double),
+        ("precision", ctypes.c_int32),
     ]
 
 
@@ -82,6 +85,7 @@ class LGOutputs(ctypes.Structure):
         ("stop_layer", ctypes.c_int32),
         ("kept0", ctypes.c_int32),
         ("kept1", ctypes.c_int32),
+        ("precision_used", ctypes.c_int32),
     ]
 
 

@@ -65,8 +65,8 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
   if (q_blk >= S.Nq) return;
   const int Nq = S.Nq, Nk = S.Nk;
   const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
-  const __bf16* Kp = S.kp + (size_t)bh * Nk * kHeadDim;
-  const __bf16* Vp = S.vp + (size_t)bh * Nk * kHeadDim;
+  const __bf16* Kp = static_cast<const __bf16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
+  const __bf16* Vp = static_cast<const __bf16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
   const long long ps = S.pstride;
   const int head = bh % H;
   const int b = bh / H;
@@ -228,27 +228,34 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
   }
 }
 
+
+__device__ __forceinline__ f16x4 tr_read_h(const _Float16* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(f16x4, v);
+}
+
 // ----------------------------------------------------------------------------------------
-// Software-pipelined variant: the scores of tile t+1 are computed while the softmax of tile t
-// runs, so the MFMA pipe and the VALU work of one wave overlap instead of alternating.
-//   iteration t:  [S(t+1) = K(t+1) Q^T  ||  exp / row-sum of S(t)]   then   [O += V(t) P(t),
-//                 P split just in time]   then stage K(t+2), V(t+1); one barrier.
-// K and V use separate two-slot rings offset by one tile (K(t+1) and V(t) are resident
-// together).  The running max / O rescale happen once per 64-key tile at the top of the
-// iteration, after the previous PV has retired.
+// fp16x3 variant (PREC_H3, common.h): the same tiling with half the MFMAs.
+//  * K and V arrive as two fp16 planes (h, l*2^11) from the QKV GEMM epilogue.
+//  * Each query row is scaled by 2^e (per lane: the query sits on the lane) so that
+//    max|q 2^e| lies in [8, 16); its pieces (h*2^11, l, h) stay in registers.  The S^T
+//    accumulator then holds 2^(11+e) q.k, and the per-lane factor scale*log2(e)*2^-(11+e)
+//    folds into the fma that feeds exp2 -- the softmax costs nothing extra.
+//  * P in [0, 1] is split in-register into (h*2^11, l, h); O accumulates 2^11 * P V and the
+//    2^-11 folds into the final 1/l.
 // ----------------------------------------------------------------------------------------
 template <int WAVES, int KT>
-__global__ __launch_bounds__(64 * WAVES) void attention_x6p_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
-                                                                    float scale_log2e) {
+__global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+                                                                   float scale_log2e) {
   constexpr int NT = 64 * WAVES;
   constexpr int QB = 32 * WAVES;
   constexpr int NSUB = KT / 32;
-  constexpr int KLD = kHeadDim + 8;
-  constexpr int CH = 3 * KT * 8;
-  constexpr int LDC = CH / NT;
+  constexpr int KLD = kHeadDim + 8;       // K plane row stride (fp16)
+  constexpr int CH = 2 * KT * 8;          // 16-byte chunks per tile per tensor (2 planes x KT rows x 8)
+  constexpr int LDC = CH / NT;            // chunks per thread per tensor
   static_assert(CH % NT == 0, "tile/threads mismatch");
-  __shared__ __attribute__((aligned(16))) __bf16 Ks[2][3][KT * KLD];
-  __shared__ __attribute__((aligned(16))) __bf16 Vs[2][3][KT * kHeadDim];
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[2][2][KT * KLD];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[2][2][KT * kHeadDim];
 
   const int item = xcd_chunk(blockIdx.x, gridDim.x);
   const int qb = item % nqb;
@@ -259,8 +266,8 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6p_kernel(AttnSet s0, A
   if (q_blk >= S.Nq) return;
   const int Nq = S.Nq, Nk = S.Nk;
   const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
-  const __bf16* Kp = S.kp + (size_t)bh * Nk * kHeadDim;
-  const __bf16* Vp = S.vp + (size_t)bh * Nk * kHeadDim;
+  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
+  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
   const long long ps = S.pstride;
   const int head = bh % H;
   const int b = bh / H;
@@ -268,97 +275,92 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6p_kernel(AttnSet s0, A
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5;
 
+  // Q^T B operand: k-step s, lane half h holds dims 16s + 8h + j (j = 0..7) of its query.
   const int qrow = min(q_blk + wave * 32 + l32, Nq - 1);
-  bf16x8 qp[3][4];
+  f16x8 qh[4], qhs[4], ql[4];
+  float c_lane;
   {
     const float* qr = Q + (size_t)qrow * kHeadDim + half * 8;
+    f32x4 x[4][2];
+    float mx = 0.f;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(qr + 16 * s);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(qr + 16 * s + 4);
+      x[s][0] = *reinterpret_cast<const f32x4*>(qr + 16 * s);
+      x[s][1] = *reinterpret_cast<const f32x4*>(qr + 16 * s + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[s][0][e]), fabsf(x[s][1][e])));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    int ex = 0;
+    if (mx > 0.f && mx <= 3.0e38f) {
+      int E;
+      (void)frexpf(mx, &E);  // mx = m 2^E, m in [0.5, 1)
+      ex = min(max(4 - E, -100), 100);
+    }
+    c_lane = ldexpf(scale_log2e, -(11 + ex));
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        __bf16 h, m, l;
-        split3(e < 4 ? x0[e] : x1[e - 4], h, m, l);
-        qp[0][s][e] = h; qp[1][s][e] = m; qp[2][s][e] = l;
+        _Float16 h, l;
+        split2h(ldexpf(x[s][e >> 2][e & 3], ex), h, l);
+        qh[s][e] = h;
+        ql[s][e] = l;
+        qhs[s][e] = (_Float16)((float)h * kLoScale);
       }
-    }
   }
 
-  bf16x8 rk[LDC], rv[LDC];
-  auto gload_k = [&](int t0) {
+  // tile staging: chunk c -> plane c / (KT*8), row (c / 8) % KT, 8-dim column block c % 8
+  f32x4 rk[LDC], rv[LDC];
+  auto gload = [&](int t0) {
 #pragma unroll
     for (int i = 0; i < LDC; ++i) {
       const int c = tid + i * NT;
       const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
-      rk[i] = *reinterpret_cast<const bf16x8*>(Kp + (size_t)p * ps + (size_t)min(t0 + r, Nk - 1) * kHeadDim + cb * 8);
+      const size_t src = (size_t)p * ps + (size_t)min(t0 + r, Nk - 1) * kHeadDim + cb * 8;
+      rk[i] = *reinterpret_cast<const f32x4*>(Kp + src);
+      rv[i] = *reinterpret_cast<const f32x4*>(Vp + src);
     }
   };
-  auto gload_v = [&](int t0) {
+  auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < LDC; ++i) {
       const int c = tid + i * NT;
       const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
-      rv[i] = *reinterpret_cast<const bf16x8*>(Vp + (size_t)p * ps + (size_t)min(t0 + r, Nk - 1) * kHeadDim + cb * 8);
+      *reinterpret_cast<f32x4*>(&Ks[buf][p][r * KLD + cb * 8]) = rk[i];
+      *reinterpret_cast<f32x4*>(&Vs[buf][p][r * kHeadDim + ((cb ^ (((r >> 1) & 1) << 2)) * 8)]) = rv[i];
     }
   };
-  auto sstore_k = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < LDC; ++i) {
-      const int c = tid + i * NT;
-      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
-      *reinterpret_cast<bf16x8*>(&Ks[buf][p][r * KLD + cb * 8]) = rk[i];
-    }
-  };
-  auto sstore_v = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < LDC; ++i) {
-      const int c = tid + i * NT;
-      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
-      *reinterpret_cast<bf16x8*>(&Vs[buf][p][r * kHeadDim + ((cb ^ (((r >> 1) & 1) << 2)) * 8)]) = rv[i];
-    }
-  };
-  auto scores = [&](int buf, f32x16 (&sc)[NSUB]) {
+
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tdim = ((lane >> 4) & 1) * 16 + 4 * tp;
+
+  f32x16 o0 = f32x16{0.f}, o1 = f32x16{0.f};  // O^T tiles (x 2^11): dims [0,32) and [32,64)
+  float m_run = -INFINITY;                    // running max of the raw (scaled) scores
+  float l_run = 0.f;
+
+  const int ntiles = (Nk + KT - 1) / KT;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const int t0 = t * KT;
+    if (t + 1 < ntiles) gload(t0 + KT);
+
+    // ---- S^T = K Q^T (x 2^(11+e))
+    f32x16 sc[NSUB];
 #pragma unroll
     for (int u = 0; u < NSUB; ++u) {
       sc[u] = f32x16{0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int off = (u * 32 + l32) * KLD + 16 * s + 8 * half;
-        const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(&Ks[buf][0][off]);
-        const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(&Ks[buf][1][off]);
-        const bf16x8 k2 = *reinterpret_cast<const bf16x8*>(&Ks[buf][2][off]);
-        sc[u] = mfma_x6(k0, k1, k2, qp[0][s], qp[1][s], qp[2][s], sc[u]);
+        const f16x8 k0 = *reinterpret_cast<const f16x8*>(&Ks[cur][0][off]);
+        const f16x8 k1 = *reinterpret_cast<const f16x8*>(&Ks[cur][1][off]);
+        sc[u] = mfma_h3(k0, k1, qhs[s], ql[s], qh[s], sc[u]);
       }
     }
-  };
-
-  const int tq = (lane & 15) >> 2, tp = lane & 3, tdim = ((lane >> 4) & 1) * 16 + 4 * tp;
-  f32x16 o0 = f32x16{0.f}, o1 = f32x16{0.f};
-  float m_run = -INFINITY;
-  float l_run = 0.f;
-
-  const int ntiles = (Nk + KT - 1) / KT;
-  // prologue: K(0) -> Ks[0], V(0) -> Vs[0]; S(0); then K(1) -> Ks[1]
-  gload_k(0);
-  gload_v(0);
-  sstore_k(0);
-  sstore_v(0);
-  __syncthreads();
-  if (ntiles > 1) gload_k(KT);
-  f32x16 sc[NSUB];
-  scores(0, sc);
-  if (ntiles > 1) sstore_k(1);
-  __syncthreads();
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int t0 = t * KT;
-    const int cur = t & 1;
-    // stage-in for the end of this iteration: K(t+2) -> Ks[cur], V(t+1) -> Vs[cur^1]
-    if (t + 2 < ntiles) gload_k(t0 + 2 * KT);
-    if (t + 1 < ntiles) gload_v(t0 + KT);
-
-    // ---- running max over the tile, rescale (previous PV has retired)
+    // ---- mask (last tile), online softmax
     if (t0 + KT > Nk) {
 #pragma unroll
       for (int u = 0; u < NSUB; ++u)
@@ -373,65 +375,62 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6p_kernel(AttnSet s0, A
       for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[u][r]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m_run, tmax);
-    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2e);
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c_lane);
     m_run = m_new;
-    const float mb = m_new * scale_log2e;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-
-    // ---- [S(t+1) MFMAs] || [exp / sum of S(t)]
-    f32x16 sn[NSUB];
-    if (t + 1 < ntiles) scores(cur ^ 1, sn);
+    const float mb = m_new * c_lane;
     float psum = 0.f;
 #pragma unroll
     for (int u = 0; u < NSUB; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], scale_log2e, -mb));
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c_lane, -mb));
         sc[u][r] = p;
         psum += p;
       }
     l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
 
-    // ---- [O += V(t) P(t)] with P split just in time
+    // ---- O^T += V^T P^T (x 2^11), 16 keys per MFMA step
 #pragma unroll
     for (int u = 0; u < NSUB; ++u)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8 p0, p1, p2;
+        f16x8 ph, phs, pl;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          __bf16 a, bb, c;
-          split3(sc[u][8 * s + j], a, bb, c);
-          p0[j] = a; p1[j] = bb; p2[j] = c;
+          _Float16 h, l;
+          split2h(sc[u][8 * s + j], h, l);
+          ph[j] = h;
+          pl[j] = l;
+          phs[j] = (_Float16)((float)h * kLoScale);
         }
+        // keys of element j: ka + j (j < 4), ka + 8 + (j - 4) (j >= 4); transposed-read row = ka + tq
         const int ka = u * 32 + 16 * s + 4 * half;
-        const int r0 = ka + tq, r1 = ka + 8 + tq;
-        const int sw = ((r0 >> 1) & 1) << 5;
+        const int r0 = ka + tq, r1 = ka + 8 + tq;  // r0, r1 share bit 1 (ka % 4 == 0)
+        const int sw = ((r0 >> 1) & 1) << 5;       // half swap, in dims
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
           const int dcol = (dt * 32 + tdim) ^ sw;
-          bf16x8 v[3];
+          f16x8 v[2];
 #pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            const bf16x4 lo = tr_read(&Vs[cur][p][r0 * kHeadDim + dcol]);
-            const bf16x4 hi = tr_read(&Vs[cur][p][r1 * kHeadDim + dcol]);
-            v[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          for (int p = 0; p < 2; ++p) {
+            const f16x4 lo = tr_read_h(&Vs[cur][p][r0 * kHeadDim + dcol]);
+            const f16x4 hi = tr_read_h(&Vs[cur][p][r1 * kHeadDim + dcol]);
+            v[p] = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           }
-          if (dt == 0) o0 = mfma_x6(v[0], v[1], v[2], p0, p1, p2, o0);
-          else o1 = mfma_x6(v[0], v[1], v[2], p0, p1, p2, o1);
+          if (dt == 0) o0 = mfma_h3(v[0], v[1], phs, pl, ph, o0);
+          else o1 = mfma_h3(v[0], v[1], phs, pl, ph, o1);
         }
       }
 
-    if (t + 2 < ntiles) sstore_k(cur);
-    if (t + 1 < ntiles) sstore_v(cur ^ 1);
+    if (t + 1 < ntiles) sstore(cur ^ 1);
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < NSUB; ++u) sc[u] = sn[u];
+    cur ^= 1;
   }
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.f / l_tot;
+  const float inv = ldexpf(1.f / l_tot, -11);  // 2^-11 exact: same rounding as (o 2^-11) / l
   const int q = q_blk + wave * 32 + l32;
   if (q < Nq) {
     float* orow = S.o + ((size_t)b * Nq + q) * kDim + head * kHeadDim;
@@ -446,14 +445,14 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6p_kernel(AttnSet s0, A
 }
 
 template <int WAVES, int KT>
-static hipError_t attention_x6p_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+static hipError_t attention_h3_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
   constexpr int QB = 32 * WAVES;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
   if (nq == 0 || B == 0) return hipSuccess;
   if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
   const int nqb = (nq + QB - 1) / QB;
   const int items = nqb * B * H * 2;
-  hipLaunchKernelGGL((attention_x6p_kernel<WAVES, KT>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
+  hipLaunchKernelGGL((attention_h3_kernel<WAVES, KT>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
                      scale * 1.4426950408889634f);
   return hipGetLastError();
 }
@@ -476,7 +475,8 @@ static hipError_t attention_x6_launch(const AttnSet& s0, const AttnSet& s1, int 
 #define LG_ATTN_CONFIG 8, 64
 #endif
 
-hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st) {
+  if (prec == PREC_H3) return attention_h3_launch<LG_ATTN_CONFIG>(s0, s1, B, H, scale, st);
   return attention_x6_launch<LG_ATTN_CONFIG>(s0, s1, B, H, scale, st);
 }
 

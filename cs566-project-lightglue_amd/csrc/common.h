@@ -1,4 +1,5 @@
-// Shared device helpers for the gfx950 kernels (wave64, f32-input MFMA).
+// Shared device helpers for the gfx950 kernels (wave64; fp32-accurate products on the
+// bf16 / fp16 matrix cores).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -61,6 +62,39 @@ __device__ __forceinline__ f32x16 mfma_x6(const bf16x8& a0, const bf16x8& a1, co
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c, 0, 0, 0);
+  return c;
+}
+
+// ---- fp16x3: fp32-accurate products on fp16 matrix cores (half the MFMAs of bf16x6) ------
+// x = h + l * 2^-11 with h = fp16(x) and l = fp16((x - h) * 2^11): the low piece is stored
+// pre-scaled so it stays a normal fp16 number; together they carry 22 significant bits
+// (probed on gfx950: v_mfma_f32_32x32x16_f16 keeps fp16 subnormal A/B inputs, products are exact
+// in the fp32 accumulator; tools/probe_f16_mfma.hip).  For a product the "y" side additionally
+// supplies h * 2^11 (exact: |h| <= 16 * 2^11 by construction), so that all three terms land in
+// ONE accumulator at the common scale 2^11:
+//   2^11 * (x . y) ~= x_h . (y_h 2^11) + x_h . y_l + x_l . y_h        (x_l y_l ~ 2^-22 dropped)
+// Operand ranges: |x| <= 65504 (checked where x is produced at run time);
+// y is scaled so |y| < 16 (weights: per matrix at load time; queries: per row; P <= 1).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr float kLoScale = 2048.f;    // 2^11
+constexpr float kF16Max = 65504.f;    // largest finite fp16
+
+__device__ __forceinline__ void split2h(float x, _Float16& h, _Float16& l) {
+  h = (_Float16)x;
+  l = (_Float16)((x - (float)h) * kLoScale);  // x - h is exact
+}
+
+__device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// acc += 2^11 * (x . y), x = (xh, xl), y = (yhs = yh * 2^11, yl, yh); smallest terms first
+__device__ __forceinline__ f32x16 mfma_h3(const f16x8& xh, const f16x8& xl, const f16x8& yhs, const f16x8& yl,
+                                          const f16x8& yh, f32x16 c) {
+  c = mfma16(xl, yh, c);
+  c = mfma16(xh, yl, c);
+  c = mfma16(xh, yhs, c);
   return c;
 }
 

@@ -179,6 +179,43 @@ hipError_t fold_out_proj(float* W1, float* b1, const float* Wo, const float* bo,
 // ----------------------------------------------------------------------------------------
 // weight repacking
 // ----------------------------------------------------------------------------------------
+// absmax over n floats -> *out (one block of 1024 threads; load time only)
+__global__ __launch_bounds__(1024) void absmax_kernel(const float* src, size_t n, float* out) {
+  __shared__ float red[16];
+  float m = 0.f;
+  for (size_t i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, fabsf(src[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t = fmaxf(t, red[w]);
+    *out = t;
+  }
+}
+
+hipError_t absmax(const float* src, size_t n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(absmax_kernel, dim3(1), dim3(1024), 0, st, src, n, out);
+  return hipGetLastError();
+}
+
+// fp16x3 weight planes (common.h): x = src * scale (a power of two), planes [3][n] =
+// (fp16(x) * 2^11, fp16((x - fp16(x)) * 2^11), fp16(x)).
+__global__ void split_weight_h3_kernel(const float* src, size_t n, float scale, _Float16* planes) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  _Float16 h, l;
+  split2h(src[i] * scale, h, l);
+  planes[i] = (_Float16)((float)h * kLoScale);
+  planes[n + i] = l;
+  planes[2 * n + i] = h;
+}
+
+hipError_t split_weight_h3(const float* src, size_t n, float scale, _Float16* planes, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(split_weight_h3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, n, scale, planes);
+  return hipGetLastError();
+}
 __global__ void gather_rows_kernel(float* dst, const float* src, const int* idx, int rows, int cols) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)rows * cols) return;

@@ -7,15 +7,22 @@ namespace lg {
 
 enum EpiKind { EPI_STORE = 0, EPI_QKV_ROT = 1, EPI_CROSS_QKV = 2, EPI_PROBE = 3 /* benchmarking only */ };
 
+// Operand formats of the fp32-accurate matrix-core arithmetic (common.h):
+//   PREC_H3  fp16x3 -- 3 fp16 MFMAs per product; runtime operands must satisfy |x| <= 65504
+//            (a device flag records any violation, lg_forward then reruns in PREC_X6)
+//   PREC_X6  bf16x6 -- 6 bf16 MFMAs per product; full fp32 range
+enum Prec { PREC_H3 = 0, PREC_X6 = 1 };
+
 // Head-major destinations [set][b][h][n][64] for the QKV epilogues; set 0 = image 0 (B*M rows),
 // set 1 = image 1 (B*N rows), rows in GEMM order (image 0 rows first).  All in natural dim order.
 //   q   fp32 queries (self) / qk (cross)
-//   kp  keys as three bf16 planes (bf16x6 split, plane p at kp + p*pstride): k (self) / qk (cross)
-//   vp  values as three bf16 planes
+//   kp  keys as operand planes (plane p at kp + p*pstride): k (self) / qk (cross)
+//       PREC_X6: three bf16 planes (h, m, l);  PREC_H3: two fp16 planes (h, l * 2^11)
+//   vp  values, same planes
 struct HeadLayout {
   float* q;
-  __bf16* kp;
-  __bf16* vp;
+  void* kp;
+  void* vp;
   long long pstride;  // elements between planes (= B*(M+N)*H*64)
   int B, H, M, N;
   const float* cosb;  // [rows][32] rotary cos table, by GEMM row
@@ -28,8 +35,12 @@ struct GemmArgs {
   int lda0, K0;
   const float* A1;  // [R][lda1], columns [K0, K) (nullable: K0 == K)
   int lda1;
-  const float* W;   // [Nout][ldw] (PyTorch Linear layout), k contiguous
+  const float* W;   // [Nout][ldw] (PyTorch Linear layout), k contiguous (PREC_X6)
   int ldw, K;
+  const _Float16* Wp;  // PREC_H3: three fp16 planes (h*2^11, l, h) of W * 2^sw, [3][Nout][ldw]
+  long long wps;       // elements between the planes
+  float acc_scale;     // PREC_H3: 2^-(11+sw) (accumulator -> value); 1 otherwise
+  int* ovf;            // PREC_H3: set to 1 if an A element is outside the fp16 range (nullable)
   const float* bias;  // [Nout] or null
   const float* res;   // residual [R][ldr] or null (EPI_STORE): Y = res + (acc + bias) * out_scale
   int ldr;
@@ -41,19 +52,19 @@ struct GemmArgs {
   HeadLayout hl;
 };
 
-hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, hipStream_t st);
+hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, int prec, hipStream_t st);
 
 // Attention over head-major Q/K/V ([set][b][h][n][64]); O written row-major into ctx
 // [rows][256] at column h*64 (rows in GEMM order).  Two "sets" per launch (blockIdx.z).
 struct AttnSet {
   const float* q;    // [B][H][Nq][64] fp32
-  const __bf16* kp;  // [3 planes][B][H][Nk][64] bf16 (plane stride pstride)
-  const __bf16* vp;  // [3 planes][B][H][Nk][64] bf16
+  const void* kp;    // [planes][B][H][Nk][64] (plane stride pstride): 3 bf16 (X6) / 2 fp16 (H3)
+  const void* vp;    // [planes][B][H][Nk][64]
   long long pstride;
   float* o;          // ctx + row_base*256
   int Nq, Nk;
 };
-hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st);
+hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st);
 
 // Positional encoding: normalised keypoints -> cos/sin tables [rows][32].
 struct PEArgs {
@@ -97,6 +108,11 @@ size_t filter_workspace_floats(int B, int M, int N);
 // Load-time fold of out_proj/to_out into ffn.0 (W1 [512][512], b1 [512], Wo [256][256], bo [256]);
 // tmp holds 512*256 + 512 floats.
 hipError_t fold_out_proj(float* W1, float* b1, const float* Wo, const float* bo, float* tmp, hipStream_t st);
+
+// fp16x3 weight planes (PREC_H3): absmax of n floats -> *out (one block), then
+// planes [3][n] = (h*2^11, l, h) of src * 2^sw.
+hipError_t absmax(const float* src, size_t n, float* out, hipStream_t st);
+hipError_t split_weight_h3(const float* src, size_t n, float scale, _Float16* planes, hipStream_t st);
 
 // Weight repacking: dst[r,:] = src[idx[r],:] (row length `cols`).
 hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st);

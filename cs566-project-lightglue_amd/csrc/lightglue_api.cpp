@@ -119,6 +119,14 @@ struct lg_handle {
   size_t Wr, Wc, bc, Wi, bi, total;
   float* wbuf = nullptr;
   int* perm = nullptr;  // head_perm() [1024]
+  // fp16x3 planes of every GEMM weight matrix (PREC_H3), keyed by the matrix's fp32 offset
+  struct Planes {
+    size_t off;       // halfs into wplanes
+    long long pstride;
+    float unscale;    // 2^-(11+sw)
+  };
+  std::map<size_t, Planes> planes;
+  _Float16* wplanes = nullptr;
   bool loaded = false;
   // fold out_proj / to_out into ffn.0 at load time (env LG_FOLD_OUT_PROJ=0 disables)
   bool fold = true;
@@ -268,9 +276,10 @@ void plan_layout(lg_handle* h) {
 // ------------------------------------------------------------------ forward workspace
 struct Work {
   float *X, *X2, *cosb, *sinb, *cos2, *sin2, *size, *Q, *ctx, *msg, *H1, *md, *z, *tok, *sim, *aws;
-  __bf16 *KP, *VP;  // bf16x6 planes of keys (qk) and values: 3 x R x 256
+  void *KP, *VP;  // operand planes of keys (qk) and values: 3 bf16 (X6) / 2 fp16 (H3) x R x 256
   size_t R;
   int *flags, *pos, *ind0, *ind1, *ind0b, *ind1b, *counts;
+  int* ovf;  // PREC_H3 fp16-range guard (gemm.hip)
   int64_t *m0c, *m1c;
   float *s0c, *s1c;
   size_t bytes;
@@ -293,8 +302,8 @@ Work carve(char* base, int B, int M, int N, bool prune) {
   w.size = tf(4 * (size_t)B);
   w.R = R;
   w.Q = tf(R * D);
-  w.KP = reinterpret_cast<__bf16*>(take(3 * R * D * 2));
-  w.VP = reinterpret_cast<__bf16*>(take(3 * R * D * 2));
+  w.KP = take(3 * R * D * 2);
+  w.VP = take(3 * R * D * 2);
   w.ctx = tf(R * D);
   w.msg = tf(R * D);
   w.H1 = tf(R * 2 * D);
@@ -303,6 +312,7 @@ Work carve(char* base, int B, int M, int N, bool prune) {
   w.tok = tf(R);
   w.sim = tf((size_t)B * M * N);
   w.aws = tf(lg::assign_workspace_floats(B, M, N));
+  w.ovf = ti(64);
   if (prune) {
     w.X2 = tf(R * D);
     w.cos2 = tf(R * 32);
@@ -329,6 +339,7 @@ lg::GemmArgs gemm_base() {
   lg::GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.out_scale = 1.f;
+  a.acc_scale = 1.f;
   return a;
 }
 
@@ -387,6 +398,7 @@ int lg_destroy(lg_handle_t* h) {
   (void)hipSetDevice(h->device);
   if (h->wbuf) (void)hipFree(h->wbuf);
   if (h->perm) (void)hipFree(h->perm);
+  if (h->wplanes) (void)hipFree(h->wplanes);
   for (auto& r : h->recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -445,6 +457,50 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
       }
     LG_HIP(hipFreeAsync(tmp, st));
   }
+  // fp16x3 planes (h*2^11, l, h) of every GEMM weight matrix, scaled per matrix by 2^sw so that
+  // max|W 2^sw| lies in [8, 16) (common.h, gemm.hip MODE_H3)
+  {
+    struct Mat { size_t off; int rows, K; };
+    std::vector<Mat> mats;
+    if (h->cfg.input_dim != D) mats.push_back({h->Wi, D, h->cfg.input_dim});
+    for (auto& lw : h->layers) {
+      for (int b = 0; b < 2; ++b) {
+        const BlockW& w = b == 0 ? lw.self : lw.cross;
+        mats.push_back({w.Wqkv, b == 0 ? 3 * D : 2 * D, D});
+        if (!h->fold) mats.push_back({w.Wo, D, D});
+        mats.push_back({w.W1, 2 * D, 2 * D});
+        mats.push_back({w.W2, D, 2 * D});
+      }
+      mats.push_back({lw.Wf, D, D});
+    }
+    size_t total = 0;
+    for (auto& m : mats) total += 3 * (size_t)m.rows * m.K;
+    if (h->wplanes) (void)hipFree(h->wplanes);
+    h->wplanes = nullptr;
+    h->planes.clear();
+    LG_HIP(hipMalloc((void**)&h->wplanes, total * sizeof(_Float16)));
+    float* dmax = nullptr;
+    LG_HIP(hipMallocAsync((void**)&dmax, mats.size() * sizeof(float), st));
+    for (size_t i = 0; i < mats.size(); ++i)
+      LG_HIP(lg::absmax(h->wbuf + mats[i].off, (size_t)mats[i].rows * mats[i].K, dmax + i, st));
+    std::vector<float> mx(mats.size());
+    LG_HIP(hipMemcpyAsync(mx.data(), dmax, mats.size() * sizeof(float), hipMemcpyDeviceToHost, st));
+    LG_HIP(hipStreamSynchronize(st));
+    LG_HIP(hipFreeAsync(dmax, st));
+    size_t off = 0;
+    for (size_t i = 0; i < mats.size(); ++i) {
+      int sw = 0;
+      if (mx[i] > 0.f && std::isfinite(mx[i])) {
+        int E;
+        (void)std::frexp(mx[i], &E);  // max = m 2^E, m in [0.5, 1)
+        sw = std::min(std::max(4 - E, -100), 100);
+      }
+      const size_t n = (size_t)mats[i].rows * mats[i].K;
+      LG_HIP(lg::split_weight_h3(h->wbuf + mats[i].off, n, std::ldexp(1.f, sw), h->wplanes + off, st));
+      h->planes[mats[i].off] = {off, (long long)n, std::ldexp(1.f, -(11 + sw))};
+      off += 3 * n;
+    }
+  }
   h->loaded = true;
   return LG_OK;
 }
@@ -455,8 +511,9 @@ int lg_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, si
   return LG_OK;
 }
 
-int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* workspace, size_t workspace_bytes,
-               void* stream) {
+// One full eval forward in operand format `prec` (lg::PREC_H3 / PREC_X6).
+static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* workspace,
+                        size_t workspace_bytes, void* stream, int prec) {
   using namespace lg;
   if (!h || !in || !out) return fail(LG_E_INVALID, "null argument");
   if (!h->loaded) return fail(LG_E_WEIGHTS, "weights not loaded");
@@ -483,16 +540,25 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
   const float* Wb = h->wbuf;
   int M = M0, N = N0;
   // launch wrappers that feed lg_profile_* (algorithmic flops / bytes per launch)
-  auto gemm = [&](const GemmArgs& g, int epi, int batch) -> hipError_t {
+  // weights of a Linear layer: fp32 (X6) and its fp16x3 planes (H3), by fp32 offset
+  auto setw = [&](GemmArgs& g, size_t off) {
+    g.W = Wb + off;
+    const auto& pl = h->planes.at(off);
+    g.Wp = h->wplanes + pl.off;
+    g.wps = pl.pstride;
+    g.acc_scale = prec == PREC_H3 ? pl.unscale : 1.f;
+    g.ovf = w.ovf;
+  };
+  auto gemm = [&](const GemmArgs& g, int epi, int batch, int p_gemm) -> hipError_t {
     const int p = h->prof_begin(LG_KERNEL_GEMM, st);
-    const hipError_t e = gemm_f32(g, epi, batch, st);
+    const hipError_t e = gemm_f32(g, epi, batch, p_gemm, st);
     const double R = g.R, K = g.K, O = g.Nout;
     h->prof_end(p, 2.0 * R * K * O * batch, 4.0 * (R * K + O * K + R * O) * batch, st);
     return e;
   };
   auto attn = [&](const AttnSet& a0, const AttnSet& a1, float scale, bool cross) -> hipError_t {
     const int p = h->prof_begin(LG_KERNEL_ATTENTION, st);
-    const hipError_t e = attention_f32(a0, a1, B, H, scale, st);
+    const hipError_t e = attention_f32(a0, a1, B, H, scale, prec, st);
     // self: 2 matmuls per image (QK^T, PV); cross: one shared sim + two PV (lightglue.py:236-242)
     const double hd = 64.0 * H * B;
     const double fl = cross ? 6.0 * a0.Nq * a0.Nk * hd : 4.0 * hd * ((double)a0.Nq * a0.Nk + (double)a1.Nq * a1.Nk);
@@ -511,12 +577,12 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
   // ---- input projection (lightglue.py:370-373,486-487)
   if (c.input_dim != D) {
     GemmArgs g = gemm_base();
-    g.W = Wb + h->Wi; g.ldw = c.input_dim; g.K = c.input_dim; g.K0 = c.input_dim;
+    setw(g, h->Wi); g.ldw = c.input_dim; g.K = c.input_dim; g.K0 = c.input_dim;
     g.bias = Wb + h->bi; g.ldy = D; g.Nout = D;
     g.A0 = in->descriptors0; g.lda0 = c.input_dim; g.R = B * M; g.Y = w.X;
-    LG_HIP(gemm(g, EPI_STORE, 1));
+    LG_HIP(gemm(g, EPI_STORE, 1, prec));
     g.A0 = in->descriptors1; g.R = B * N; g.Y = w.X + (size_t)B * M * D;
-    LG_HIP(gemm(g, EPI_STORE, 1));
+    LG_HIP(gemm(g, EPI_STORE, 1, prec));
   } else {
     LG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
     LG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
@@ -538,6 +604,7 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
     LG_HIP(positional_encoding(p, st));
   }
 
+  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.ovf, 0, sizeof(int), st));
   if (do_prune) {
     LG_HIP(iota_fill(w.ind0, M, st));
     LG_HIP(iota_fill(w.ind1, N, st));
@@ -554,41 +621,44 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
       const BlockW& bw = blk == 0 ? lw.self : lw.cross;
       // QKV projection with fused rotary (self) / scale (cross) and head-major scatter
       GemmArgs g = gemm_base();
-      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wqkv; g.ldw = D; g.bias = Wb + bw.bqkv;
+      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; setw(g, bw.Wqkv); g.ldw = D; g.bias = Wb + bw.bqkv;
       g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D;
       g.hl.B = B; g.hl.H = H; g.hl.M = M; g.hl.N = N; g.hl.cosb = w.cosb; g.hl.sinb = w.sinb;
       g.hl.q = w.Q; g.hl.kp = w.KP; g.hl.vp = w.VP; g.hl.pstride = (long long)w.R * D;
       g.hl.qk_scale = std::sqrt(1.f / std::sqrt(64.f));  // scale**0.5 (lightglue.py:235)
-      LG_HIP(gemm(g, blk == 0 ? EPI_QKV_ROT : EPI_CROSS_QKV, 1));
+      LG_HIP(gemm(g, blk == 0 ? EPI_QKV_ROT : EPI_CROSS_QKV, 1, prec));
       const size_t img1 = (size_t)B * H * M * 64;
       const long long ps = (long long)w.R * D;
       AttnSet a0, a1;
+      // planes are 2-byte elements in both formats (bf16 / fp16)
+      const void* kp1 = static_cast<const char*>(w.KP) + 2 * img1;
+      const void* vp1 = static_cast<const char*>(w.VP) + 2 * img1;
       if (blk == 0) {  // self: q/k/v of the same image, scale 1/sqrt(64) (SDPA default)
         a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M};
-        a1 = {w.Q + img1, w.KP + img1, w.VP + img1, ps, w.ctx + (size_t)B * M * D, N, N};
+        a1 = {w.Q + img1, kp1, vp1, ps, w.ctx + (size_t)B * M * D, N, N};
         LG_HIP(attn(a0, a1, 0.125f, false));
       } else {  // cross: qk fp32 in w.Q and as planes in w.KP, v planes in w.VP
-        a0 = {w.Q, w.KP + img1, w.VP + img1, ps, w.ctx, M, N};
+        a0 = {w.Q, kp1, vp1, ps, w.ctx, M, N};
         a1 = {w.Q + img1, w.KP, w.VP, ps, w.ctx + (size_t)B * M * D, N, M};
         LG_HIP(attn(a0, a1, 1.0f, true));
       }
       // out projection (skipped when folded into ffn.0 at load time: ffn.0 then reads ctx)
       if (!h->fold) {
         g = gemm_base();
-        g.A0 = w.ctx; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wo; g.ldw = D; g.bias = Wb + bw.bo;
+        g.A0 = w.ctx; g.lda0 = D; g.K0 = D; g.K = D; setw(g, bw.Wo); g.ldw = D; g.bias = Wb + bw.bo;
         g.R = R; g.Nout = D; g.Y = w.msg; g.ldy = D;
-        LG_HIP(gemm(g, EPI_STORE, 1));
+        LG_HIP(gemm(g, EPI_STORE, 1, prec));
       }
       // FFN: Linear(cat[x, msg]) -> LN -> GELU -> Linear + residual
       g = gemm_base();
       g.A0 = w.X; g.lda0 = D; g.K0 = D; g.A1 = h->fold ? w.ctx : w.msg; g.lda1 = D; g.K = 2 * D;
-      g.W = Wb + bw.W1; g.ldw = 2 * D; g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
-      LG_HIP(gemm(g, EPI_STORE, 1));
+      setw(g, bw.W1); g.ldw = 2 * D; g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
+      LG_HIP(gemm(g, EPI_STORE, 1, prec));
       LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, st));
       g = gemm_base();
-      g.A0 = w.H1; g.lda0 = 2 * D; g.K0 = 2 * D; g.K = 2 * D; g.W = Wb + bw.W2; g.ldw = 2 * D; g.bias = Wb + bw.b2;
+      g.A0 = w.H1; g.lda0 = 2 * D; g.K0 = 2 * D; g.K = 2 * D; setw(g, bw.W2); g.ldw = 2 * D; g.bias = Wb + bw.b2;
       g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
-      LG_HIP(gemm(g, EPI_STORE, 1));
+      LG_HIP(gemm(g, EPI_STORE, 1, prec));
     }
     if (i == L - 1) break;
 
@@ -640,21 +710,22 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
   out->stop_layer = stop;
   out->kept0 = M;
   out->kept1 = N;
+  out->precision_used = prec;
 
   // ---- assignment head of the last executed layer (lightglue.py:549-551, MatchAssignment :306-315)
   const LayerW& la = h->layers[stop];
   const int R = B * (M + N);
   {
     GemmArgs g = gemm_base();
-    g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + la.Wf; g.ldw = D; g.bias = Wb + la.bf;
+    g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; setw(g, la.Wf); g.ldw = D; g.bias = Wb + la.bf;
     g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
-    LG_HIP(gemm(g, EPI_STORE, 1));
+    LG_HIP(gemm(g, EPI_STORE, 1, prec));
     LG_HIP(gemv_256(w.X, Wb + la.wm, Wb + la.bm, w.z, R, 0, st));
     g = gemm_base();
     g.A0 = w.md; g.lda0 = D; g.K0 = D; g.K = D; g.sA = (long long)M * D;
     g.W = w.md + (size_t)B * M * D; g.ldw = D; g.sW = (long long)N * D;
     g.R = M; g.Nout = N; g.Y = w.sim; g.ldy = N; g.sY = (long long)M * N;
-    LG_HIP(gemm(g, EPI_STORE, B));
+    LG_HIP(gemm(g, EPI_STORE, B, PREC_X6));  // both operands are run-time values: full range
   }
   AssignArgs aa;
   aa.sim = w.sim; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = out->log_assignment; aa.ws = w.aws;
@@ -674,6 +745,23 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
     LG_HIP(hipMemcpyAsync(out->ref_descriptors1, w.X + (size_t)B * M * D, sizeof(float) * B * N * D,
                           hipMemcpyDeviceToDevice, st));
   return LG_OK;
+}
+
+int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* workspace, size_t workspace_bytes,
+               void* stream) {
+  if (!h || !in || !out) return fail(LG_E_INVALID, "null argument");
+  const int first = h->cfg.precision == LG_PREC_X6 ? lg::PREC_X6 : lg::PREC_H3;
+  int rc = forward_pass(h, in, out, workspace, workspace_bytes, stream, first);
+  if (rc != LG_OK || first != lg::PREC_H3) return rc;
+  // fp16-range guard: an operand outside the fp16 range makes the fp16x3 result unreliable;
+  // recompute the whole forward in bf16x6 (full fp32 range) -- rare by design
+  const Work w = carve((char*)workspace, in->B, in->M, in->N, prune_enabled(h->cfg));
+  int flag = 0;
+  hipStream_t st = (hipStream_t)stream;
+  LG_HIP(hipMemcpyAsync(&flag, w.ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+  LG_HIP(hipStreamSynchronize(st));
+  if (flag) rc = forward_pass(h, in, out, workspace, workspace_bytes, stream, lg::PREC_X6);
+  return rc;
 }
 
 int lg_profile_enable(lg_handle_t* h, int enable) {

@@ -108,8 +108,14 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+# Extension keys (no reference counterpart).  "precision": matrix-core operand format of the HIP
+# kernels, both fp32-accurate -- "auto" (fp16x3 with a guarded bf16x6 rerun) or "bf16x6"
+# (DESIGN.md §3).
+EXTENSION_CONF = {"precision": "auto"}
+
+
 class LightGlue(nn.Module):
-    default_conf = DEFAULT_CONF
+    default_conf = {**DEFAULT_CONF, **EXTENSION_CONF}
     required_data_keys = ["keypoints0", "keypoints1", "descriptors0", "descriptors1"]
     url = "https://github.com/cvg/LightGlue/releases/download/{}/{}_lightglue.pth"
 
@@ -175,6 +181,7 @@ class LightGlue(nn.Module):
             float(c.depth_confidence),
             float(c.width_confidence),
             float(c.filter_threshold),
+            _lib.PRECISIONS[str(c.precision)],
         )
 
     def _ensure_handle(self, device):
@@ -271,12 +278,13 @@ class LightGlue(nn.Module):
         if self._ws is None or self._ws.numel() < ws_bytes.value or self._ws.device != device:
             self._ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=device)
         inp = _lib.LGInputs(b, m, n, *[_ptr(t) for t in (k0, k1, d0, d1, s0, s1, sc0, o0, sc1, o1)])
-        out = _lib.LGOutputs(*[_ptr(t) for t in (m0, m1, ms0, ms1, la, rd0, rd1, p0, p1)], 0, 0, 0)
+        out = _lib.LGOutputs(*[_ptr(t) for t in (m0, m1, ms0, ms1, la, rd0, rd1, p0, p1)], 0, 0, 0, 0)
         stream = torch.cuda.current_stream(device).cuda_stream
         _lib.check(
             lib.lg_forward(self._handle, ctypes.byref(inp), ctypes.byref(out), _ptr(self._ws), ws_bytes.value, ctypes.c_void_p(stream)),
             "lg_forward",
         )
+        self.last_precision_used = "fp16x3" if out.precision_used == 0 else "bf16x6"
         kept0, kept1 = out.kept0, out.kept1
         if kept0 != m or kept1 != n:  # log_assignment was written for the kept points
             la = la.view(-1)[: b * (kept0 + 1) * (kept1 + 1)].view(b, kept0 + 1, kept1 + 1)

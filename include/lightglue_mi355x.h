@@ -14,8 +14,9 @@
  *   - Every pointer argument marked "device" is caller-allocated HIP device memory on the
  *     handle's device (torch CUDA tensors on ROCm); the library never frees caller memory.
  *   - All device work is stream-ordered on `stream` (a hipStream_t; NULL = default stream).
- *     lg_forward synchronises the stream only when pruning / early stop is enabled (the kept
- *     point counts decide launch sizes, as the reference's torch.where does).
+ *     lg_forward synchronises the stream when pruning / early stop is enabled (the kept point
+ *     counts decide launch sizes, as the reference's torch.where does) and, with
+ *     LG_PREC_AUTO, once at the end to read the fp16-range guard.
  *   - Functions return 0 on success and a negative LG_E* code on failure; lg_last_error()
  *     returns a thread-local message for the last failure on the calling thread.
  *   - A handle belongs to one device; it is not re-entrant (one forward at a time), separate
@@ -32,7 +33,7 @@
 extern "C" {
 #endif
 
-#define LG_ABI_VERSION 1
+#define LG_ABI_VERSION 2
 
 enum {
   LG_OK = 0,
@@ -56,7 +57,14 @@ typedef struct {
   double filter_threshold;  /* match threshold, strict '>' (lightglue.py:333) */
   /* doubles: the reference keeps these as Python floats and derives thresholds in double
    * (e.g. 1 - width_confidence, :590) before the fp32 comparison. */
+  int32_t precision;        /* matrix-core operand format (no reference counterpart; both are
+                             * fp32-accurate):
+                             *   LG_PREC_AUTO  fp16x3, guarded: if any run-time operand leaves the
+                             *                 fp16 range the forward is recomputed in bf16x6
+                             *   LG_PREC_X6    always bf16x6 */
 } lg_config_t;
+
+enum { LG_PREC_AUTO = 0, LG_PREC_X6 = 1 };
 
 typedef struct {
   int32_t B, M, N;              /* pairs, keypoints in image 0 / image 1 */
@@ -84,6 +92,7 @@ typedef struct {
   int64_t* prune1;              /* device [B,N] or NULL */
   int32_t stop_layer;           /* host out: index of the last executed layer */
   int32_t kept0, kept1;         /* host out: M', N' after width pruning (= M, N without) */
+  int32_t precision_used;       /* host out: 0 = fp16x3, 1 = bf16x6 (LG_PREC_X6, or the guarded rerun) */
 } lg_outputs_t;
 
 int lg_abi_version(void);

@@ -4,6 +4,8 @@ Bar (BASELINE north star): match indices bit-exact, matching scores
 log-assignment |d| <= 1e-3 (fp32 vs fp64 already differs by 2.2e-3), prune counts exact.
 Rows/columns whose fp64 top-1/top-2 margin is below NEAR_TIE (fixture keys margin0/margin1) are
 reported separately and allowed to flip; with the committed recipe there are none.
+Both matrix-core operand formats are held to the same bar: "auto" (fp16x3, the default) and
+"bf16x6" (the guarded fallback).
 """
 import numpy as np
 import pytest
@@ -19,10 +21,10 @@ LA_TOL = 1e-3
 pytestmark = pytest.mark.gpu
 
 
-def _model(conf, sd):
+def _model(conf, sd, precision="auto"):
     from lightglue_amd import LightGlue
 
-    m = LightGlue(dict(conf)).eval().cuda()
+    m = LightGlue({**dict(conf), "precision": precision}).eval().cuda()
     res = m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     assert not res.missing_keys and not res.unexpected_keys
     return m
@@ -68,16 +70,36 @@ def check_against_golden(pred, g):
         np.testing.assert_allclose(pred["ref_descriptors1"][:, :, :k1].cpu().numpy(), g["ref_descriptors1"], atol=2e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("precision", ["auto", "bf16x6"])
 @pytest.mark.parametrize("name", case_names())
-def test_forward_matches_reference_golden(name):
+def test_forward_matches_reference_golden(name, precision):
     g = load(name)
     conf, sd, data = case_inputs(g["meta"])
-    model = _model(conf, sd)
+    model = _model(conf, sd, precision)
     with torch.no_grad():
         pred = model(_gpu_data(data))
     torch.cuda.synchronize()
+    assert model.last_precision_used == ("fp16x3" if precision == "auto" else "bf16x6")
     assert pred["stop_layer"] + 1 == int(g["n_layers_run"])
     check_against_golden(pred, g)
+
+
+def test_fp16_range_guard_reruns_in_bf16x6():
+    """Descriptors beyond the fp16 range (|x| > 65504) trip the guard: the forward is recomputed
+    in bf16x6 and gives exactly the bf16x6 result."""
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1}
+    sd = synthetic_state_dict(conf, seed=0)
+    data = synthetic_pair(B=1, M=128, N=120, seed=2)
+    data["descriptors0"] = data["descriptors0"] * np.float32(2.0e5)
+    auto, x6 = _model(conf, sd, "auto"), _model(conf, sd, "bf16x6")
+    with torch.no_grad():
+        a = auto(_gpu_data(data))
+        b = x6(_gpu_data(data))
+    assert auto.last_precision_used == "bf16x6"
+    for k in ("matches0", "matches1", "matching_scores0", "matching_scores1", "log_assignment"):
+        assert torch.equal(a[k], b[k]), k
 
 
 def test_forward_batched_equals_single():

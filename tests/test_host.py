@@ -36,10 +36,12 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 
 def test_ctypes_structs_match_header_layout():
-    # lg_config_t: 5 x int32 then 3 doubles (8-byte aligned) -> 48 bytes
-    assert ctypes.sizeof(_lib.LGConfig) == 48
+    # lg_config_t: 5 x int32, pad, 3 doubles, int32 precision, pad -> 56 bytes
+    assert ctypes.sizeof(_lib.LGConfig) == 56
+    assert _lib.LGConfig.precision.offset == 48
     assert ctypes.sizeof(_lib.LGInputs) == 16 + 10 * 8
-    assert ctypes.sizeof(_lib.LGOutputs) == 9 * 8 + 12 + 4
+    # lg_outputs_t: 9 pointers, stop_layer, kept0, kept1, precision_used
+    assert ctypes.sizeof(_lib.LGOutputs) == 9 * 8 + 16
 
 
 def test_error_path_without_gpu_reports_message():

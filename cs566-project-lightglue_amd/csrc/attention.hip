@@ -1,4 +1,5 @@
-// Flash-style fp32-accurate attention on gfx950 bf16 matrix cores (bf16x6, see common.h).
+// Flash-style fp32-accurate attention on gfx950 matrix cores: fp16x3 (PREC_H3, default) and
+// bf16x6 (PREC_X6) operand formats, see common.h.
 //
 //   O = softmax(Q K^T * scale) V      per (set, pair, head); never materialises the N x N scores.
 //
@@ -229,33 +230,42 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
 }
 
 
-__device__ __forceinline__ f16x4 tr_read_h(const _Float16* p) {
-  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
-  return __builtin_bit_cast(f16x4, v);
-}
-
 // ----------------------------------------------------------------------------------------
-// fp16x3 variant (PREC_H3, common.h): the same tiling with half the MFMAs.
+// fp16x3 attention (PREC_H3, common.h): the bf16x6 tiling above with half the MFMAs.
 //  * K and V arrive as two fp16 planes (h, l*2^11) from the QKV GEMM epilogue.
 //  * Each query row is scaled by 2^e (per lane: the query sits on the lane) so that
 //    max|q 2^e| lies in [8, 16); its pieces (h*2^11, l, h) stay in registers.  The S^T
 //    accumulator then holds 2^(11+e) q.k, and the per-lane factor scale*log2(e)*2^-(11+e)
 //    folds into the fma that feeds exp2 -- the softmax costs nothing extra.
-//  * P in [0, 1] is split in-register into (h*2^11, l, h); O accumulates 2^11 * P V and the
-//    2^-11 folds into the final 1/l.
+//  * Lazy max: a query's softmax reference is raised only when a tile would push its
+//    probabilities above 2^3 (p <= 8 keeps p_h * 2^11 inside fp16); otherwise the O / l rescale
+//    is skipped for the whole wave (ballot) -- after the first tiles it almost always is.
+//  * P is split in-register with fp16 arithmetic: p_h = fp16(p), p_h 2^11 by an fp16 multiply
+//    (exact), p_l = fp16(p 2^11 - p_h 2^11) in one mixed-precision fma (exact before its
+//    rounding); O accumulates 2^11 * P V and the 2^-11 folds into the final 1/l.
+//  * Tree reductions for the tile max / sum; per-lane LDS offsets hoisted out of the loop.
+//  * The context is written straight into the plane image that ffn.0 consumes (common.h).
+// DIAG (tools/kbench_attn.hip only, never instantiated by the library): 1 = no softmax VALU,
+// 2 = no MFMAs -- to split the loop's time between the two pipes.
 // ----------------------------------------------------------------------------------------
-template <int WAVES, int KT>
-__global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
-                                                                   float scale_log2e) {
+__device__ __forceinline__ f16x4 tr_read_h(const _Float16* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(f16x4, v);
+}
+
+template <int WAVES, int KT, int OCC, int DIAG = 0>
+__global__ __launch_bounds__(64 * WAVES, OCC) void attention_h3_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+                                                                        float scale_log2e) {
   constexpr int NT = 64 * WAVES;
   constexpr int QB = 32 * WAVES;
   constexpr int NSUB = KT / 32;
   constexpr int KLD = kHeadDim + 8;       // K plane row stride (fp16)
   constexpr int CH = 2 * KT * 8;          // 16-byte chunks per tile per tensor (2 planes x KT rows x 8)
   constexpr int LDC = CH / NT;            // chunks per thread per tensor
+  constexpr int KPL = KT * KLD, VPL = KT * kHeadDim;  // plane sizes (elements)
   static_assert(CH % NT == 0, "tile/threads mismatch");
-  __shared__ __attribute__((aligned(16))) _Float16 Ks[2][2][KT * KLD];
-  __shared__ __attribute__((aligned(16))) _Float16 Vs[2][2][KT * kHeadDim];
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[2 * 2 * KPL];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[2 * 2 * VPL];
 
   const int item = xcd_chunk(blockIdx.x, gridDim.x);
   const int qb = item % nqb;
@@ -275,7 +285,8 @@ __global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, At
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5;
 
-  // Q^T B operand: k-step s, lane half h holds dims 16s + 8h + j (j = 0..7) of its query.
+  // Q^T B operand: k-step s, lane half h holds dims 16s + 8h + j (j = 0..7) of its query,
+  // scaled by 2^ex so that the row max lies in [8, 16).
   const int qrow = min(q_blk + wave * 32 + l32, Nq - 1);
   f16x8 qh[4], qhs[4], ql[4];
   float c_lane;
@@ -306,7 +317,7 @@ __global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, At
         split2h(ldexpf(x[s][e >> 2][e & 3], ex), h, l);
         qh[s][e] = h;
         ql[s][e] = l;
-        qhs[s][e] = (_Float16)((float)h * kLoScale);
+        qhs[s][e] = h * (_Float16)kLoScale;
       }
   }
 
@@ -327,15 +338,21 @@ __global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, At
     for (int i = 0; i < LDC; ++i) {
       const int c = tid + i * NT;
       const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
-      *reinterpret_cast<f32x4*>(&Ks[buf][p][r * KLD + cb * 8]) = rk[i];
-      *reinterpret_cast<f32x4*>(&Vs[buf][p][r * kHeadDim + ((cb ^ (((r >> 1) & 1) << 2)) * 8)]) = rv[i];
+      *reinterpret_cast<f32x4*>(&Ks[(buf * 2 + p) * KPL + r * KLD + cb * 8]) = rk[i];
+      *reinterpret_cast<f32x4*>(&Vs[(buf * 2 + p) * VPL + r * kHeadDim + ((cb ^ (((r >> 1) & 1) << 2)) * 8)]) = rv[i];
     }
   };
 
+  // per-lane LDS offsets: K fragment row l32, dims 8*half..; transposed V reads: 16-lane group
+  // g = lane >> 4 covers dims (g & 1) * 16 + 4p of lane half h = g >> 1, rows ka + tq (+8)
   const int tq = (lane & 15) >> 2, tp = lane & 3, tdim = ((lane >> 4) & 1) * 16 + 4 * tp;
+  const int sw = ((tq >> 1) & 1) << 5;  // V half swap of rows with key bit 1 set (ka % 4 == 0)
+  const int koff = l32 * KLD + 8 * half;
+  const int voff0 = (4 * half + tq) * kHeadDim + (tdim ^ sw);
+  const int voff1 = (4 * half + tq) * kHeadDim + ((32 + tdim) ^ sw);
 
   f32x16 o0 = f32x16{0.f}, o1 = f32x16{0.f};  // O^T tiles (x 2^11): dims [0,32) and [32,64)
-  float m_run = -INFINITY;                    // running max of the raw (scaled) scores
+  float m_use = -INFINITY;                    // softmax reference (raw score units), raised lazily
   float l_run = 0.f;
 
   const int ntiles = (Nk + KT - 1) / KT;
@@ -346,6 +363,8 @@ __global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, At
   for (int t = 0; t < ntiles; ++t) {
     const int t0 = t * KT;
     if (t + 1 < ntiles) gload(t0 + KT);
+    const _Float16* Kc = Ks + cur * 2 * KPL + koff;
+    const _Float16* Vc = Vs + cur * 2 * VPL;
 
     // ---- S^T = K Q^T (x 2^(11+e))
     f32x16 sc[NSUB];
@@ -354,42 +373,61 @@ __global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, At
       sc[u] = f32x16{0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int off = (u * 32 + l32) * KLD + 16 * s + 8 * half;
-        const f16x8 k0 = *reinterpret_cast<const f16x8*>(&Ks[cur][0][off]);
-        const f16x8 k1 = *reinterpret_cast<const f16x8*>(&Ks[cur][1][off]);
-        sc[u] = mfma_h3(k0, k1, qhs[s], ql[s], qh[s], sc[u]);
+        const int off = u * 32 * KLD + 16 * s;
+        const f16x8 k0 = *reinterpret_cast<const f16x8*>(Kc + off);
+        const f16x8 k1 = *reinterpret_cast<const f16x8*>(Kc + KPL + off);
+        if constexpr (DIAG == 2) {
+          sc[u][s] += (float)k0[0] + (float)k1[1];
+        } else {
+          sc[u] = mfma_h3(k0, k1, qhs[s], ql[s], qh[s], sc[u]);
+        }
       }
     }
-    // ---- mask (last tile), online softmax
-    if (t0 + KT > Nk) {
+    if constexpr (DIAG != 1) {
+      if (t0 + KT > Nk) {  // mask keys past the end (last tile only)
+#pragma unroll
+        for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (t0 + u * 32 + row32(r, half) >= Nk) sc[u][r] = -INFINITY;
+      }
+      // ---- tile max (tree), lazy reference raise
+      float mr[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float m = sc[0][r];
+#pragma unroll
+        for (int u = 1; u < NSUB; ++u) m = fmaxf(m, sc[u][r]);
+        mr[r] = m;
+      }
+#pragma unroll
+      for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+        for (int r = 0; r < w; ++r) mr[r] = fmaxf(mr[r], mr[r + w]);
+      const float tmax = fmaxf(mr[0], __shfl_xor(mr[0], 32, 64));
+      const bool need = (tmax - m_use) * c_lane > 3.f;
+      if (__ballot(need) != 0ull) {
+        const float m_new = need ? tmax : m_use;
+        const float alpha = __builtin_amdgcn_exp2f((m_use - m_new) * c_lane);
+        m_use = m_new;
+        l_run *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      }
+      const float mb = m_use * c_lane;
+      float ps8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ps8[i] = 0.f;
 #pragma unroll
       for (int u = 0; u < NSUB; ++u)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (t0 + u * 32 + row32(r, half) >= Nk) sc[u][r] = -INFINITY;
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c_lane, -mb));
+          sc[u][r] = p;
+          ps8[(u * 16 + r) & 7] += p;
+        }
+      l_run += ((ps8[0] + ps8[1]) + (ps8[2] + ps8[3])) + ((ps8[4] + ps8[5]) + (ps8[6] + ps8[7]));
     }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < NSUB; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[u][r]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c_lane);
-    m_run = m_new;
-    const float mb = m_new * c_lane;
-    float psum = 0.f;
-#pragma unroll
-    for (int u = 0; u < NSUB; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c_lane, -mb));
-        sc[u][r] = p;
-        psum += p;
-      }
-    l_run = l_run * alpha + psum;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
 
     // ---- O^T += V^T P^T (x 2^11), 16 keys per MFMA step
 #pragma unroll
@@ -397,30 +435,38 @@ __global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, At
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         f16x8 ph, phs, pl;
+        if constexpr (DIAG == 1) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          _Float16 h, l;
-          split2h(sc[u][8 * s + j], h, l);
-          ph[j] = h;
-          pl[j] = l;
-          phs[j] = (_Float16)((float)h * kLoScale);
-        }
-        // keys of element j: ka + j (j < 4), ka + 8 + (j - 4) (j >= 4); transposed-read row = ka + tq
-        const int ka = u * 32 + 16 * s + 4 * half;
-        const int r0 = ka + tq, r1 = ka + 8 + tq;  // r0, r1 share bit 1 (ka % 4 == 0)
-        const int sw = ((r0 >> 1) & 1) << 5;       // half swap, in dims
+          for (int j = 0; j < 8; ++j) ph[j] = phs[j] = pl[j] = (_Float16)sc[u][8 * s + j];
+        } else {
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const int dcol = (dt * 32 + tdim) ^ sw;
-          f16x8 v[2];
-#pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            const f16x4 lo = tr_read_h(&Vs[cur][p][r0 * kHeadDim + dcol]);
-            const f16x4 hi = tr_read_h(&Vs[cur][p][r1 * kHeadDim + dcol]);
-            v[p] = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          for (int j = 0; j < 8; ++j) {
+            const float p = sc[u][8 * s + j];
+            const _Float16 h = (_Float16)p;
+            const _Float16 hs = h * (_Float16)kLoScale;
+            ph[j] = h;
+            phs[j] = hs;
+            pl[j] = (_Float16)fmaf(p, kLoScale, -(float)hs);
           }
-          if (dt == 0) o0 = mfma_h3(v[0], v[1], phs, pl, ph, o0);
-          else o1 = mfma_h3(v[0], v[1], phs, pl, ph, o1);
+        }
+        // keys of element j: ka + j (j < 4), ka + 8 + (j - 4) (j >= 4), ka = u*32 + 16s + 4*half
+        const int vr = (u * 32 + 16 * s) * kHeadDim;
+        f16x8 v[2][2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const f16x4 a0 = tr_read_h(Vc + p * VPL + vr + voff0);
+          const f16x4 a1 = tr_read_h(Vc + p * VPL + vr + 8 * kHeadDim + voff0);
+          const f16x4 b0 = tr_read_h(Vc + p * VPL + vr + voff1);
+          const f16x4 b1 = tr_read_h(Vc + p * VPL + vr + 8 * kHeadDim + voff1);
+          v[0][p] = f16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          v[1][p] = f16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        }
+        if constexpr (DIAG == 2) {
+          o0[s] += (float)v[0][0][1] + (float)v[0][1][2] + (float)ph[3] + (float)pl[4] + (float)phs[5];
+          o1[s] += (float)v[1][0][1] + (float)v[1][1][2];
+        } else {
+          o0 = mfma_h3(v[0][0], v[0][1], phs, pl, ph, o0);
+          o1 = mfma_h3(v[1][0], v[1][1], phs, pl, ph, o1);
         }
       }
 
@@ -433,18 +479,29 @@ __global__ __launch_bounds__(64 * WAVES) void attention_h3_kernel(AttnSet s0, At
   const float inv = ldexpf(1.f / l_tot, -11);  // 2^-11 exact: same rounding as (o 2^-11) / l
   const int q = q_blk + wave * 32 + l32;
   if (q < Nq) {
-    float* orow = S.o + ((size_t)b * Nq + q) * kDim + head * kHeadDim;
+    // context row into the plane image (K = 256): register r = 4g + e holds dim 8g + 4*half + e
+    // (+32 for o1); 4 consecutive dims = 8 bytes per plane.  |o| <= max|v| <= 65504 (v checked).
+    const int orow = S.o_row0 + b * Nq + q;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 a = {o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv, o0[4 * g + 3] * inv};
-      f32x4 c = {o1[4 * g] * inv, o1[4 * g + 1] * inv, o1[4 * g + 2] * inv, o1[4 * g + 3] * inv};
-      *reinterpret_cast<f32x4*>(orow + 8 * g + 4 * half) = a;
-      *reinterpret_cast<f32x4*>(orow + 32 + 8 * g + 4 * half) = c;
-    }
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          _Float16 a, c;
+          split2h((hf ? o1 : o0)[4 * g + e] * inv, a, c);
+          h[e] = a;
+          l[e] = c;
+        }
+        const size_t off = plane_off(orow, head * kHeadDim + hf * 32 + 8 * g + 4 * half, S.o_rows_pad);
+        *reinterpret_cast<f16x4*>(S.op + off) = h;
+        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+      }
   }
 }
 
-template <int WAVES, int KT>
+template <int WAVES, int KT, int OCC, int DIAG = 0>
 static hipError_t attention_h3_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
   constexpr int QB = 32 * WAVES;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
@@ -452,8 +509,8 @@ static hipError_t attention_h3_launch(const AttnSet& s0, const AttnSet& s1, int 
   if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
   const int nqb = (nq + QB - 1) / QB;
   const int items = nqb * B * H * 2;
-  hipLaunchKernelGGL((attention_h3_kernel<WAVES, KT>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
-                     scale * 1.4426950408889634f);
+  hipLaunchKernelGGL((attention_h3_kernel<WAVES, KT, OCC, DIAG>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H,
+                     nqb, scale * 1.4426950408889634f);
   return hipGetLastError();
 }
 
@@ -474,9 +531,16 @@ static hipError_t attention_x6_launch(const AttnSet& s0, const AttnSet& s1, int 
 // WAVES, KT: 8 waves (256 queries) per workgroup, 64-key tiles (tools/kbench_attn.hip).
 #define LG_ATTN_CONFIG 8, 64
 #endif
+#ifndef LG_ATTN_H3_CONFIG
+// WAVES, KT, min waves per SIMD (tools/kbench_attn.hip)
+#define LG_ATTN_H3_CONFIG 8, 64, 2
+#endif
 
 hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st) {
-  if (prec == PREC_H3) return attention_h3_launch<LG_ATTN_CONFIG>(s0, s1, B, H, scale, st);
+  if (prec == PREC_H3) {
+    if (!s0.op || !s1.op) return hipErrorInvalidValue;
+    return attention_h3_launch<LG_ATTN_H3_CONFIG>(s0, s1, B, H, scale, st);
+  }
   return attention_x6_launch<LG_ATTN_CONFIG>(s0, s1, B, H, scale, st);
 }
 

@@ -83,39 +83,65 @@ hipError_t kpt_extent(const float* kpts, int B, int n, float* size_out, hipStrea
 // ffn.1 LayerNorm(512, eps 1e-5) + ffn.2 GELU(erf) (lightglue.py:171-176), in place.
 // One wave per row: lane holds columns [4l, 4l+4) and [256+4l, 256+4l+4).
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ln_gelu_kernel(float* x, const float* g, const float* bta, int rows) {
+__global__ __launch_bounds__(256) void ln_gelu_kernel(float* x, const float* g, const float* bta, int rows,
+                                                      _Float16* planes, int rows_pad, int* ovf) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  float* xr = x + (size_t)row * 512;
-  f32x4 v0 = *reinterpret_cast<f32x4*>(xr + lane * 4);
-  f32x4 v1 = *reinterpret_cast<f32x4*>(xr + 256 + lane * 4);
-  float s = (v0[0] + v0[1]) + (v0[2] + v0[3]) + (v1[0] + v1[1]) + (v1[2] + v1[3]);
-  const float mean = wave_sum(s) * (1.f / 512.f);
-  float q = 0.f;
+  bool bad = false;
+  if (row < rows) {
+    float* xr = x + (size_t)row * 512;
+    f32x4 v0 = *reinterpret_cast<f32x4*>(xr + lane * 4);
+    f32x4 v1 = *reinterpret_cast<f32x4*>(xr + 256 + lane * 4);
+    float s = (v0[0] + v0[1]) + (v0[2] + v0[3]) + (v1[0] + v1[1]) + (v1[2] + v1[3]);
+    const float mean = wave_sum(s) * (1.f / 512.f);
+    float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float d0 = v0[i] - mean, d1 = v1[i] - mean;
-    q += d0 * d0 + d1 * d1;
-  }
-  const float var = wave_sum(q) * (1.f / 512.f);
-  const float rstd = 1.f / sqrtf(var + 1e-5f);
-  const f32x4 g0 = *reinterpret_cast<const f32x4*>(g + lane * 4), g1 = *reinterpret_cast<const f32x4*>(g + 256 + lane * 4);
-  const f32x4 b0 = *reinterpret_cast<const f32x4*>(bta + lane * 4), b1 = *reinterpret_cast<const f32x4*>(bta + 256 + lane * 4);
+    for (int i = 0; i < 4; ++i) {
+      const float d0 = v0[i] - mean, d1 = v1[i] - mean;
+      q += d0 * d0 + d1 * d1;
+    }
+    const float var = wave_sum(q) * (1.f / 512.f);
+    const float rstd = 1.f / sqrtf(var + 1e-5f);
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(g + lane * 4), g1 = *reinterpret_cast<const f32x4*>(g + 256 + lane * 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(bta + lane * 4), b1 = *reinterpret_cast<const f32x4*>(bta + 256 + lane * 4);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float y0 = (v0[i] - mean) * rstd * g0[i] + b0[i];
-    float y1 = (v1[i] - mean) * rstd * g1[i] + b1[i];
-    v0[i] = 0.5f * y0 * (1.f + erff(y0 * 0.70710678118654752f));
-    v1[i] = 0.5f * y1 * (1.f + erff(y1 * 0.70710678118654752f));
+    for (int i = 0; i < 4; ++i) {
+      float y0 = (v0[i] - mean) * rstd * g0[i] + b0[i];
+      float y1 = (v1[i] - mean) * rstd * g1[i] + b1[i];
+      v0[i] = 0.5f * y0 * (1.f + erff(y0 * 0.70710678118654752f));
+      v1[i] = 0.5f * y1 * (1.f + erff(y1 * 0.70710678118654752f));
+    }
+    if (!planes) {
+      *reinterpret_cast<f32x4*>(xr + lane * 4) = v0;
+      *reinterpret_cast<f32x4*>(xr + 256 + lane * 4) = v1;
+    } else {
+      // plane image (K = 512): 4 consecutive columns = 8 bytes per plane
+      const size_t ps = (size_t)rows_pad * 512;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const f32x4 v = hf ? v1 : v0;
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bad |= !(fabsf(v[e]) <= kF16Max);
+          _Float16 a, b;
+          split2h(v[e], a, b);
+          h[e] = a;
+          l[e] = b;
+        }
+        const size_t off = plane_off(row, hf * 256 + lane * 4, rows_pad);
+        *reinterpret_cast<f16x4*>(planes + off) = h;
+        *reinterpret_cast<f16x4*>(planes + ps + off) = l;
+      }
+    }
   }
-  *reinterpret_cast<f32x4*>(xr + lane * 4) = v0;
-  *reinterpret_cast<f32x4*>(xr + 256 + lane * 4) = v1;
+  if (ovf && __ballot(bad) != 0ull && lane == 0) atomicOr(ovf, 1);
 }
 
-hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, hipStream_t st) {
+hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, _Float16* planes, int rows_pad,
+                              int* ovf, hipStream_t st) {
   if (rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(ln_gelu_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, g, b, rows);
+  hipLaunchKernelGGL(ln_gelu_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, g, b, rows, planes, rows_pad, ovf);
   return hipGetLastError();
 }
 
@@ -199,23 +225,28 @@ hipError_t absmax(const float* src, size_t n, float* out, hipStream_t st) {
   return hipGetLastError();
 }
 
-// fp16x3 weight planes (common.h): x = src * scale (a power of two), planes [3][n] =
-// (fp16(x) * 2^11, fp16((x - fp16(x)) * 2^11), fp16(x)).
-__global__ void split_weight_h3_kernel(const float* src, size_t n, float scale, _Float16* planes) {
+// fp16x3 weight plane image (common.h) of W [rows][K] * scale (a power of two, so that
+// max|W * scale| < 16 and the h * 2^11 piece the GEMM forms in registers stays finite).
+__global__ void split_weight_h3_kernel(const float* src, int rows, int K, float scale, _Float16* planes) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= (size_t)rows * K) return;
+  const int r = (int)(i / K), k = (int)(i % K);
   _Float16 h, l;
   split2h(src[i] * scale, h, l);
-  planes[i] = (_Float16)((float)h * kLoScale);
-  planes[n + i] = l;
-  planes[2 * n + i] = h;
+  const size_t off = plane_off(r, k, rows);
+  planes[off] = h;
+  planes[(size_t)rows * K + off] = l;
 }
 
-hipError_t split_weight_h3(const float* src, size_t n, float scale, _Float16* planes, hipStream_t st) {
+hipError_t split_weight_h3(const float* src, int rows, int K, float scale, _Float16* planes, hipStream_t st) {
+  const size_t n = (size_t)rows * K;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(split_weight_h3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, n, scale, planes);
+  if (K % kKB) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(split_weight_h3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, rows, K, scale,
+                     planes);
   return hipGetLastError();
 }
+
 __global__ void gather_rows_kernel(float* dst, const float* src, const int* idx, int rows, int cols) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)rows * cols) return;

@@ -12,19 +12,12 @@
 //   MatchAssignment.final_proj / d^.25 :304,308-310 -> EPI_STORE with out_scale 0.25
 //   MatchAssignment einsum bmd,bnd->bmn :311 -> EPI_STORE, batched over pairs (blockIdx.z)
 //
-// Two arithmetic modes, both fp32-accurate (common.h):
-//  * MODE_H3 (default): fp16x3 on v_mfma_f32_32x32x16_f16.  W is split ONCE at load time into
-//    three fp16 planes (h*2^11, l, h) of W*2^sw (sw per matrix puts max|W*2^sw| in [8, 16)); the
-//    A tile is split into two fp16 planes (h, l*2^11) while it is staged into LDS.  Three MFMAs
-//    per 32x32x16 block; the accumulator holds 2^(11+sw) * A.W, removed in the epilogue.  A
-//    elements beyond the fp16 range set args.ovf (lg_forward then reruns in MODE_X6).
-//  * MODE_X6: "bf16x6" on v_mfma_f32_32x32x16_bf16.  Both operands are split into three bf16
-//    pieces x = x0 + x1 + x2 when the k-tile is staged, and the product is accumulated as the
-//    six terms of weight >= 2^-18 (a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0, small terms first).
-//    Full fp32 range; used for the similarity GEMM (both operands produced at run time) and
-//    for the guarded rerun.
-// Emulated on the golden cases (tools/numerics_study.py), both land as close to the reference
-// as an fp32 FMA chain does (fp16 without the pre-scaled low piece, or bf16x3, do not).
+// Arithmetic: "bf16x6" on v_mfma_f32_32x32x16_bf16 (common.h).  Both fp32 operands are split
+// into three bf16 pieces x = x0 + x1 + x2 when the k-tile is staged, and the product is
+// accumulated as the six terms of weight >= 2^-18 (a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0,
+// small terms first).  Full fp32 range.  This kernel serves the similarity GEMM (both operands
+// produced at run time, full range) and every linear of the PREC_X6 forward; the PREC_H3 linears
+// run on plane images in gemm_h3.hip.
 // Tiling: BM x BN block tile, BK-deep k-tiles, one wave per WM x WN sub-tile of 32x32 MFMA
 // tiles; LDS images of unpadded rows with XOR-swizzled 16-byte chunks (conflict-free
 // ds_write_b128 / ds_read_b128 groups);
@@ -35,7 +28,7 @@
 
 namespace lg {
 
-enum GemmMode { MODE_H3 = 0, MODE_X6 = 1 };
+enum GemmMode { MODE_X6 = 1 };
 
 __device__ __forceinline__ int xcd_remap(int id, int n) {
   const int xcd = id & 7, local = id >> 3;
@@ -63,10 +56,8 @@ struct GemmSmem {
   // Unpadded BK-element rows of 16-byte chunks, chunk index XOR-swizzled by swz(row) so that
   // both the ds_write_b128 staging groups and the ds_read_b128 fragment groups
   // ({0-3,12-15,20-27} rows) hit distinct banks.
-  //   X6: A and W as three bf16 planes each          [3][BM][BK] + [3][BN][BK]
-  //   H3: A as two fp16 planes (h, l), W as three    [2][BM][BK] + [3][BN][BK]
-  static constexpr int APL = MODE == MODE_X6 ? 3 : 2;
-  static constexpr size_t buf_elems = (size_t)(APL * BM + 3 * BN) * BK;
+  // A and W as three bf16 planes each: [3][BM][BK] + [3][BN][BK]
+  static constexpr size_t buf_elems = (size_t)(3 * BM + 3 * BN) * BK;
   static constexpr size_t bytes = 2 * buf_elems * 2;
 };
 
@@ -101,7 +92,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
 
   const float* A0 = args.A0 + z * args.sA;
   const float* A1 = args.A1 ? args.A1 + z * args.sA1 : nullptr;
-  const float* W = args.W ? args.W + z * args.sW : nullptr;
+  const float* W = args.W + z * args.sW;
 
   if constexpr (EPI == EPI_QKV_ROT || EPI == EPI_CROSS_QKV) {
     for (int r = tid; r < BM; r += NT) {
@@ -112,17 +103,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
     }
   }
 
-  // Staging items (one 16-byte LDS chunk per plane each):
-  //   X6: 8 consecutive k of one A row or W row (fp32, split into 3 bf16 planes)
-  //   H3: 8 consecutive k of one A row (fp32, split into 2 fp16 planes), or of one W row of
-  //       one pre-split fp16 plane (copied)
+  // Staging items: 8 consecutive k of one A row or W row (fp32, split into 3 bf16 planes)
   constexpr int NCH = BK / 8;
   constexpr int A_ITEMS = BM * NCH;
-  constexpr int W_ITEMS = (MODE == MODE_X6 ? 1 : 3) * BN * NCH;
+  constexpr int W_ITEMS = BN * NCH;
   constexpr int ITEMS = (A_ITEMS + W_ITEMS) / NT;
   static_assert((A_ITEMS + W_ITEMS) % NT == 0 && A_ITEMS % 64 == 0, "staging/threads mismatch");
   f32x4 rx[ITEMS][2];
-  bool bad = false;  // H3: an A element outside the fp16 range
   auto gload = [&](int kt) {
     const int k0 = kt * BK;
     const float* src;
@@ -138,19 +125,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
         const float* p = src + (size_t)row * ld + kk + (q % NCH) * 8;
         rx[i][0] = *reinterpret_cast<const f32x4*>(p);
         rx[i][1] = *reinterpret_cast<const f32x4*>(p + 4);
-      } else if constexpr (MODE == MODE_X6) {
+      } else {
         const int qb = q - A_ITEMS;
         int col = n0 + qb / NCH;
         col = col < args.Nout ? col : args.Nout - 1;
         const float* p = W + (size_t)col * args.ldw + k0 + (qb % NCH) * 8;
         rx[i][0] = *reinterpret_cast<const f32x4*>(p);
         rx[i][1] = *reinterpret_cast<const f32x4*>(p + 4);
-      } else {
-        const int qb = q - A_ITEMS;
-        const int pl = qb / (BN * NCH), rq = qb % (BN * NCH);
-        int col = n0 + rq / NCH;
-        col = col < args.Nout ? col : args.Nout - 1;
-        rx[i][0] = *reinterpret_cast<const f32x4*>(args.Wp + pl * args.wps + (size_t)col * args.ldw + k0 + (rq % NCH) * 8);
       }
     }
   };
@@ -162,112 +143,54 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{0.f};
 
   auto sstore = [&](int buf) {
-    if constexpr (MODE == MODE_X6) {
-      __bf16* As = reinterpret_cast<__bf16*>(smem) + (size_t)buf * SM::buf_elems;
-      __bf16* Bs = As + 3 * BM * BK;
+    __bf16* As = reinterpret_cast<__bf16*>(smem) + (size_t)buf * SM::buf_elems;
+    __bf16* Bs = As + 3 * BM * BK;
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const int q = tid + i * NT;
-        const bool isA = q < A_ITEMS;
-        const int qq = isA ? q : q - A_ITEMS;
-        const int r = qq / NCH, c = qq % NCH;
-        __bf16* base = isA ? As : Bs;
-        const int rows = isA ? BM : BN;
-        bf16x8 h, m, l;
+    for (int i = 0; i < ITEMS; ++i) {
+      const int q = tid + i * NT;
+      const bool isA = q < A_ITEMS;
+      const int qq = isA ? q : q - A_ITEMS;
+      const int r = qq / NCH, c = qq % NCH;
+      __bf16* base = isA ? As : Bs;
+      const int rows = isA ? BM : BN;
+      bf16x8 h, m, l;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          __bf16 a, b, cc;
-          split3(rx[i][e >> 2][e & 3], a, b, cc);
-          h[e] = a; m[e] = b; l[e] = cc;
-        }
-        const int off = r * BK + ((c ^ chunk_swz<BK>(r)) * 8);
-        *reinterpret_cast<bf16x8*>(base + off) = h;
-        *reinterpret_cast<bf16x8*>(base + rows * BK + off) = m;
-        *reinterpret_cast<bf16x8*>(base + 2 * rows * BK + off) = l;
+      for (int e = 0; e < 8; ++e) {
+        __bf16 a, b, cc;
+        split3(rx[i][e >> 2][e & 3], a, b, cc);
+        h[e] = a; m[e] = b; l[e] = cc;
       }
-    } else {
-      _Float16* As = reinterpret_cast<_Float16*>(smem) + (size_t)buf * SM::buf_elems;
-      _Float16* Bs = As + 2 * BM * BK;
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const int q = tid + i * NT;
-        if (q < A_ITEMS) {
-          const int r = q / NCH, c = q % NCH;
-          f16x8 h, l;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float x = rx[i][e >> 2][e & 3];
-            bad |= !(fabsf(x) <= kF16Max);
-            _Float16 a, b;
-            split2h(x, a, b);
-            h[e] = a; l[e] = b;
-          }
-          const int off = r * BK + ((c ^ chunk_swz<BK>(r)) * 8);
-          *reinterpret_cast<f16x8*>(As + off) = h;
-          *reinterpret_cast<f16x8*>(As + BM * BK + off) = l;
-        } else {
-          const int qb = q - A_ITEMS;
-          const int pl = qb / (BN * NCH), rq = qb % (BN * NCH);
-          const int r = rq / NCH, c = rq % NCH;
-          *reinterpret_cast<f32x4*>(Bs + (pl * BN + r) * BK + ((c ^ chunk_swz<BK>(r)) * 8)) = rx[i][0];
-        }
-      }
+      const int off = r * BK + ((c ^ chunk_swz<BK>(r)) * 8);
+      *reinterpret_cast<bf16x8*>(base + off) = h;
+      *reinterpret_cast<bf16x8*>(base + rows * BK + off) = m;
+      *reinterpret_cast<bf16x8*>(base + 2 * rows * BK + off) = l;
     }
   };
   auto compute = [&](int buf) {
-    if constexpr (MODE == MODE_X6) {
-      const __bf16* as = reinterpret_cast<const __bf16*>(smem) + (size_t)buf * SM::buf_elems;
-      const __bf16* bs = as + 3 * BM * BK;
+    const __bf16* as = reinterpret_cast<const __bf16*>(smem) + (size_t)buf * SM::buf_elems;
+    const __bf16* bs = as + 3 * BM * BK;
 #pragma unroll
-      for (int s = 0; s < BK / 16; ++s) {
-        bf16x8 a[TM][3], b[TN][3];
-        const int c = 2 * s + half;
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 a[TM][3], b[TN][3];
+      const int c = 2 * s + half;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < 3; ++p) {
 #pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            const int r = wm0 + i * 32 + l32;
-            a[i][p] = *reinterpret_cast<const bf16x8*>(as + (p * BM + r) * BK + (c ^ chunk_swz<BK>(r)) * 8);
-          }
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int r = wn0 + j * 32 + l32;
-            b[j][p] = *reinterpret_cast<const bf16x8*>(bs + (p * BN + r) * BK + (c ^ chunk_swz<BK>(r)) * 8);
-          }
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm0 + i * 32 + l32;
+          a[i][p] = *reinterpret_cast<const bf16x8*>(as + (p * BM + r) * BK + (c ^ chunk_swz<BK>(r)) * 8);
         }
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = mfma_x6(a[i][0], a[i][1], a[i][2], b[j][0], b[j][1], b[j][2], acc[i][j]);
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn0 + j * 32 + l32;
+          b[j][p] = *reinterpret_cast<const bf16x8*>(bs + (p * BN + r) * BK + (c ^ chunk_swz<BK>(r)) * 8);
+        }
       }
-    } else {
-      const _Float16* as = reinterpret_cast<const _Float16*>(smem) + (size_t)buf * SM::buf_elems;
-      const _Float16* bs = as + 2 * BM * BK;
 #pragma unroll
-      for (int s = 0; s < BK / 16; ++s) {
-        f16x8 a[TM][2], b[TN][3];
-        const int c = 2 * s + half;
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            const int r = wm0 + i * 32 + l32;
-            a[i][p] = *reinterpret_cast<const f16x8*>(as + (p * BM + r) * BK + (c ^ chunk_swz<BK>(r)) * 8);
-          }
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int r = wn0 + j * 32 + l32;
-            b[j][p] = *reinterpret_cast<const f16x8*>(bs + (p * BN + r) * BK + (c ^ chunk_swz<BK>(r)) * 8);
-          }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = mfma_h3(a[i][0], a[i][1], b[j][0], b[j][1], b[j][2], acc[i][j]);
-      }
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = mfma_x6(a[i][0], a[i][1], a[i][2], b[j][0], b[j][1], b[j][2], acc[i][j]);
     }
   };
 
@@ -308,7 +231,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm0 + i * 32 + row32(r, half);
           if (row >= args.R) continue;
-          float v = fmaf(acc[i][j][r], args.acc_scale, bj) * args.out_scale;
+          float v = (acc[i][j][r] + bj) * args.out_scale;
           if (args.res) v = args.res[(size_t)row * args.ldr + col] + v;
           Y[(size_t)row * args.ldy + col] = v;
         }
@@ -338,8 +261,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
         const int row = m0 + lr;
         if (row >= args.R) continue;
         const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + 2 * l32;
-        float xe = fmaf(acc[i][0][r], args.acc_scale, be);  // dim 2*l32   (even)
-        float xo = fmaf(acc[i][1][r], args.acc_scale, bo);  // dim 2*l32+1 (odd)
+        float xe = acc[i][0][r] + be;  // dim 2*l32   (even)
+        float xo = acc[i][1][r] + bo;  // dim 2*l32+1 (odd)
         if (rot) {
           // t*cos + rotate_half(t)*sin, rotate_half(x)[2i] = -x[2i+1], [2i+1] = x[2i]
           const float c = hl.cosb[(size_t)row * kFreq + l32];
@@ -353,30 +276,16 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
         xo *= sc;
         if (to_q) *reinterpret_cast<float2*>(hl.q + off) = make_float2(xe, xo);
         if (to_kp || to_vp) {
-          if constexpr (MODE == MODE_X6) {
-            __bf16* base = static_cast<__bf16*>(to_kp ? hl.kp : hl.vp);
-            __bf16 eh, em, el, oh, om, ol;
-            split3(xe, eh, em, el);
-            split3(xo, oh, om, ol);
-            typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-            *reinterpret_cast<bf16x2*>(base + off) = bf16x2{eh, oh};
-            *reinterpret_cast<bf16x2*>(base + hl.pstride + off) = bf16x2{em, om};
-            *reinterpret_cast<bf16x2*>(base + 2 * hl.pstride + off) = bf16x2{el, ol};
-          } else {
-            _Float16* base = static_cast<_Float16*>(to_kp ? hl.kp : hl.vp);
-            bad |= !(fabsf(xe) <= kF16Max) || !(fabsf(xo) <= kF16Max);
-            _Float16 eh, el, oh, ol;
-            split2h(xe, eh, el);
-            split2h(xo, oh, ol);
-            typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-            *reinterpret_cast<f16x2*>(base + off) = f16x2{eh, oh};
-            *reinterpret_cast<f16x2*>(base + hl.pstride + off) = f16x2{el, ol};
-          }
+          __bf16* base = static_cast<__bf16*>(to_kp ? hl.kp : hl.vp);
+          __bf16 eh, em, el, oh, om, ol;
+          split3(xe, eh, em, el);
+          split3(xo, oh, om, ol);
+          typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<bf16x2*>(base + off) = bf16x2{eh, oh};
+          *reinterpret_cast<bf16x2*>(base + hl.pstride + off) = bf16x2{em, om};
+          *reinterpret_cast<bf16x2*>(base + 2 * hl.pstride + off) = bf16x2{el, ol};
         }
       }
-  }
-  if constexpr (MODE == MODE_H3) {
-    if (args.ovf && __ballot(bad) != 0ull && lane == 0) atomicOr(args.ovf, 1);
   }
 }
 
@@ -396,16 +305,11 @@ static hipError_t launch(const GemmArgs& a, int batch, hipStream_t st) {
 #define LG_GEMM_TILE 256, 256, 16, 64, 64
 #endif
 
-hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, int prec, hipStream_t st) {
-  if (prec == PREC_H3 && !a.Wp) return hipErrorInvalidValue;
-  if (prec != PREC_H3 && !a.W) return hipErrorInvalidValue;
-  switch (epi * 2 + (prec == PREC_H3 ? 0 : 1)) {
-    case EPI_STORE * 2: return launch<MODE_H3, LG_GEMM_TILE, EPI_STORE>(a, batch, st);
-    case EPI_STORE * 2 + 1: return launch<MODE_X6, LG_GEMM_TILE, EPI_STORE>(a, batch, st);
-    case EPI_QKV_ROT * 2: return launch<MODE_H3, LG_GEMM_TILE, EPI_QKV_ROT>(a, batch, st);
-    case EPI_QKV_ROT * 2 + 1: return launch<MODE_X6, LG_GEMM_TILE, EPI_QKV_ROT>(a, batch, st);
-    case EPI_CROSS_QKV * 2: return launch<MODE_H3, LG_GEMM_TILE, EPI_CROSS_QKV>(a, batch, st);
-    case EPI_CROSS_QKV * 2 + 1: return launch<MODE_X6, LG_GEMM_TILE, EPI_CROSS_QKV>(a, batch, st);
+hipError_t gemm_x6(const GemmArgs& a, int epi, int batch, hipStream_t st) {
+  switch (epi) {
+    case EPI_STORE: return launch<MODE_X6, LG_GEMM_TILE, EPI_STORE>(a, batch, st);
+    case EPI_QKV_ROT: return launch<MODE_X6, LG_GEMM_TILE, EPI_QKV_ROT>(a, batch, st);
+    case EPI_CROSS_QKV: return launch<MODE_X6, LG_GEMM_TILE, EPI_CROSS_QKV>(a, batch, st);
   }
   return hipErrorInvalidValue;
 }

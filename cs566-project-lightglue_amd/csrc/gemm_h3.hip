@@ -1,0 +1,339 @@
+// fp16x3 "linear" GEMM on plane images (PREC_H3), gfx950 LDS-DMA pipeline.
+//
+//   Y[r, c] = epilogue( (sum_k A[r, k] * W[c, k]) + bias[c] )      fp32-accurate (common.h)
+//
+// Replaces every nn.Linear of the LightGlue forward (reference lightglue.py) in the default
+// operand format:
+//   SelfBlock.Wqkv        :168,184   -> EPI_QKV_ROT  (+ rotary :36-43,187-188, head-major scatter :185-186)
+//   CrossBlock.to_qk/to_v :203-204,223-228,235 -> EPI_CROSS_QKV (one GEMM, 512 outputs, qk * scale^0.5)
+//   ffn.0 on cat([x,msg]) :172,191,247-248 -> EPI_STORE, A = [x | ctx] (the cat is never built;
+//                                            out_proj / to_out folded in at load time)
+//   ffn.3 + residual      :175,191   -> EPI_STORE with res, writing x in fp32 AND as a plane image
+//   MatchAssignment.final_proj / d^.25 :304,308-310 -> EPI_STORE, out_scale 0.25
+//   input_proj            :370-373,486-487 -> EPI_STORE (fp32 + plane image)
+//
+// Operands: A and W arrive as plane images -- the two fp16 pieces of the fp32 matrix, k-blocked
+// by 32 and chunk-swizzled exactly like the LDS tile (common.h).  The producers write them (the
+// previous GEMM's epilogue, the attention epilogue, the LayerNorm+GELU kernel; W at load time,
+// pre-scaled by 2^sw), so this kernel does no conversion: every k-tile is four contiguous
+// 16 KiB blocks (A h, A l, W h, W l) copied HBM/L2 -> LDS by global_load_lds_dwordx4 (one
+// 1 KiB wave-instruction each, 4 per wave), double-buffered, one k-tile in flight while the
+// other is multiplied.  The third piece of W (h * 2^11) is formed in registers (one packed fp16
+// multiply per fragment register), and the product is accumulated as three fp16 MFMAs per
+// 32x32x16 block (common.h mfma_h3).
+// Tile: 256 x 256 x 32, 16 waves as 4 x 4 of 64 x 64 (2 x 2 MFMA tiles each); 128 KiB LDS,
+// one workgroup per CU; blockIdx -> tile through a bijective XCD remap so the column tiles of
+// one row panel share an XCD's L2.
+#include "common.h"
+#include "kernels.h"
+
+namespace lg {
+
+namespace {
+constexpr int TB = 256;                    // row / column tile
+constexpr int NT = 1024;                   // 16 waves
+
+typedef __attribute__((address_space(3))) char lds_char;
+
+__device__ __forceinline__ int xcd_remap_h3(int id, int n) {
+  const int xcd = id & 7, local = id >> 3;
+  const int base = n >> 3, extra = n & 7;
+  return xcd * base + (xcd < extra ? xcd : extra) + local;
+}
+
+// one global_load_lds_dwordx4: lane i copies 16 bytes from gsrc (per lane) to LDS byte address
+// lds + 16 i (lds wave-uniform).  Inline asm: the compiler neither counts it nor orders LDS
+// reads behind it -- the k-loop waits for it with explicit vmcnt + barrier.
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+
+__device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, int& base, int& stride) {
+  if (row < hl.B * hl.M) {
+    const int b = row / hl.M, n = row - b * hl.M;
+    base = (b * hl.H * hl.M + n) * kHeadDim;
+    stride = hl.M * kHeadDim;
+  } else {
+    const int r2 = row - hl.B * hl.M;
+    const int b = r2 / hl.N, n = r2 - b * hl.N;
+    base = hl.B * hl.H * hl.M * kHeadDim + (b * hl.H * hl.N + n) * kHeadDim;
+    stride = hl.N * kHeadDim;
+  }
+}
+}  // namespace
+
+// LDS image of one k-tile: four plane tiles (A h, A l, W h, W l) of 256 rows x BK fp16, rows of
+// BK*2 bytes, 16-byte chunk c of row r at c ^ lds_swz(r) (conflict-free ds_read_b128 groups)
+template <int BK>
+__device__ __forceinline__ int lds_swz(int r) {
+  return BK == 32 ? plane_swz(r) : (r >> 3) & 1;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int EPI, int BK, int NSTAGE>
+__global__ __launch_bounds__(NT) void gemm_h3_kernel(GemmH3Args g) {
+  constexpr int PT_BYTES = TB * BK * 2;      // one plane tile
+  constexpr int STAGE_BYTES = 4 * PT_BYTES;  // A h, A l, W h, W l
+  constexpr int DMA_PER_WAVE = STAGE_BYTES / 1024 / 16;
+  constexpr int CPR = BK / 8;                // 16-byte chunks per row
+  static_assert(BK == 16 || BK == 32, "k-tile");
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, half = lane >> 5;
+  const int wm0 = (wave >> 2) * 64, wn0 = (wave & 3) * 64;
+
+  const int num_m = (g.R + TB - 1) / TB, num_n = g.Nout / TB;
+  const int tile = xcd_remap_h3(blockIdx.x, num_m * num_n);
+  const int tm = tile / num_n, tn = tile - tm * num_n;
+  const int m0 = tm * TB, n0 = tn * TB;
+  const int nk = g.K / BK, nk0 = g.K0 / BK;
+
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)smem);
+
+  // k-tile kt -> stage: wave w copies the 1 KiB blocks q = DMA_PER_WAVE*w + i of the stage
+  // (tensor, plane and block wave-uniform).  Lane i of a block lands on LDS chunk position
+  // i % CPR of local row blk*(1024/(BK*2)) + i / CPR; it fetches the k-chunk stored there
+  // (LDS swizzle) from its place in the HBM plane image (image swizzle, common.h).
+  auto issue = [&](int kt, int stage) {
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; ++i) {
+      const int q = wave * DMA_PER_WAVE + i;
+      constexpr int QPT = PT_BYTES / 1024;  // blocks per plane tile
+      const int tensor = q / (2 * QPT), pl = (q / QPT) & 1, blk = q % QPT;
+      const int r = blk * (1024 / (BK * 2)) + lane / CPR;  // row in the tile
+      const int c = (lane % CPR) ^ lds_swz<BK>(r);         // k-chunk within the k-tile
+      const int k = kt * BK + c * 8;                       // column of A / W
+      const _Float16* src;
+      if (tensor == 0) {
+        const bool first = k < g.K0;
+        const PlaneRef& A = first ? g.A0 : g.A1;
+        src = A.p + pl * A.ps + plane_off(m0 + r, first ? k : k - g.K0, A.rows_pad);
+      } else {
+        src = g.W.p + pl * g.W.ps + plane_off(n0 + r, k, g.W.rows_pad);
+      }
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + stage * STAGE_BYTES + (tensor * 2 + pl) * PT_BYTES + blk * 1024);
+      dma16(src, dst);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0.f};
+
+  auto frag = [&](const char* st, int t, int r, int c) {
+    return *reinterpret_cast<const f16x8*>(st + t * PT_BYTES + r * (BK * 2) + ((c ^ lds_swz<BK>(r)) << 4));
+  };
+  auto compute = [&](int stage) {
+    const char* st = smem + stage * STAGE_BYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int c = 2 * s + half;
+      f16x8 ah[2], al[2], wh[2], wl[2], whs[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm0 + i * 32 + l32;
+        ah[i] = frag(st, 0, r, c);
+        al[i] = frag(st, 1, r, c);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn0 + j * 32 + l32;
+        wh[j] = frag(st, 2, r, c);
+        wl[j] = frag(st, 3, r, c);
+        whs[j] = wh[j] * (_Float16)kLoScale;  // exact: |W_h| < 16
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_h3(ah[i], al[i], whs[j], wl[j], wh[j], acc[i][j]);
+    }
+  };
+
+  // ring of NSTAGE stages, NSTAGE-1 k-tiles in flight; one barrier per k-tile:
+  //   wait for my copies of tile kt -> barrier (everyone's copies landed AND everyone finished
+  //   reading stage (kt-1) % NSTAGE) -> refill that stage with tile kt+NSTAGE-1 -> multiply tile kt
+#pragma unroll
+  for (int p = 0; p < NSTAGE - 1; ++p)
+    if (p < nk) issue(p, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(NSTAGE - 1, nk - kt) - 1;  // my tiles in flight beyond kt
+    if (ahead >= 3) wait_vm<3 * DMA_PER_WAVE>();
+    else if (ahead == 2) wait_vm<2 * DMA_PER_WAVE>();
+    else if (ahead == 1) wait_vm<DMA_PER_WAVE>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of the stage to be refilled
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    compute(kt % NSTAGE);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // ------------------------------------------------------------------ epilogues
+  bool bad = false;
+  if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn0 + j * 32 + l32;
+      const float bj = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + i * 32 + row32(r, half);
+          float v = fmaf(acc[i][j][r], g.acc_scale, bj) * g.out_scale;
+          if (row < g.R && g.res) v = g.res[(size_t)row * g.ldr + col] + v;
+          if (g.Y && row < g.R) g.Y[(size_t)row * g.ldy + col] = v;
+          if (g.Yp) {
+            // plane image: lanes (2m, 2m+1) exchange pieces; the even lane stores the h pair,
+            // the odd lane the l pair (4 bytes each)
+            _Float16 h, l;
+            split2h(v, h, l);
+            bad |= row < g.R && !(fabsf(v) <= kF16Max);
+            const uint32_t mine = (uint32_t)__builtin_bit_cast(uint16_t, h) |
+                                  ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
+            const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+            const bool odd = l32 & 1;
+            const uint32_t word = odd ? ((other >> 16) | (mine & 0xffff0000u)) : ((mine & 0xffffu) | (other << 16));
+            if (row < g.R)
+              *reinterpret_cast<uint32_t*>(g.Yp + (odd ? g.yps : 0) + plane_off(row, col & ~1, g.yrows_pad)) = word;
+          }
+        }
+    }
+  } else {
+    // Head-major scatter (see gemm.hip): the wave's 64 columns are one (type t, head) block and
+    // lane l32 holds dims 2*l32 (tile 0) and 2*l32+1 (tile 1) -- the rotary partners.
+    //   self  (EPI_QKV_ROT):   t0 -> q fp32 (rotary), t1 -> k planes (rotary), t2 -> v planes
+    //   cross (EPI_CROSS_QKV): t0 -> qk fp32 * scale^0.5 and qk planes,        t1 -> v planes
+    int* rowinfo = reinterpret_cast<int*>(smem);  // the k-loop ended with a barrier
+    for (int r = tid; r < TB; r += NT) {
+      int base = 0, stride = 0;
+      if (m0 + r < g.R) head_row_base_h3(g.hl, m0 + r, base, stride);
+      rowinfo[2 * r] = base;
+      rowinfo[2 * r + 1] = stride;
+    }
+    __syncthreads();
+    const HeadLayout& hl = g.hl;
+    const int cbase = n0 + wn0;
+    const int t = cbase / kDim, head = (cbase % kDim) / kHeadDim;
+    const bool rot = EPI == EPI_QKV_ROT && t < 2;
+    const bool to_q = t == 0;
+    const bool to_kp = EPI == EPI_QKV_ROT ? t == 1 : t == 0;
+    const bool to_vp = EPI == EPI_QKV_ROT ? t == 2 : t == 1;
+    const float sc = (EPI == EPI_CROSS_QKV && t == 0) ? hl.qk_scale : 1.f;
+    const float be = g.bias[cbase + l32], bo = g.bias[cbase + 32 + l32];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = wm0 + i * 32 + row32(r, half);
+        const int row = m0 + lr;
+        if (row >= g.R) continue;
+        const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + 2 * l32;
+        float xe = fmaf(acc[i][0][r], g.acc_scale, be);  // dim 2*l32   (even)
+        float xo = fmaf(acc[i][1][r], g.acc_scale, bo);  // dim 2*l32+1 (odd)
+        if (rot) {
+          // t*cos + rotate_half(t)*sin, rotate_half(x)[2i] = -x[2i+1], [2i+1] = x[2i]
+          const float c = hl.cosb[(size_t)row * kFreq + l32];
+          const float s = hl.sinb[(size_t)row * kFreq + l32];
+          const float e2 = add_rn(mul_rn(xe, c), mul_rn(-xo, s));
+          const float o2 = add_rn(mul_rn(xo, c), mul_rn(xe, s));
+          xe = e2;
+          xo = o2;
+        }
+        xe *= sc;
+        xo *= sc;
+        if (to_q) *reinterpret_cast<float2*>(hl.q + off) = make_float2(xe, xo);
+        if (to_kp || to_vp) {
+          _Float16* base = static_cast<_Float16*>(to_kp ? hl.kp : hl.vp);
+          bad |= !(fabsf(xe) <= kF16Max) || !(fabsf(xo) <= kF16Max);
+          _Float16 eh, el, oh, ol;
+          split2h(xe, eh, el);
+          split2h(xo, oh, ol);
+          typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<f16x2*>(base + off) = f16x2{eh, oh};
+          *reinterpret_cast<f16x2*>(base + hl.pstride + off) = f16x2{el, ol};
+        }
+      }
+  }
+  if (g.ovf && __ballot(bad) != 0ull && lane == 0) atomicOr(g.ovf, 1);
+}
+
+#ifndef LG_GEMM_H3_PIPE
+// BK, stages (tools/kbench_gemm.hip)
+#define LG_GEMM_H3_PIPE 32, 2
+#endif
+
+template <int BK, int NSTAGE>
+hipError_t gemm_h3_launch(const GemmH3Args& a, int epi, hipStream_t st) {
+  const int blocks = ((a.R + TB - 1) / TB) * (a.Nout / TB);
+  switch (epi) {
+    case EPI_STORE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_STORE, BK, NSTAGE>), dim3(blocks), dim3(NT), 0, st, a); break;
+    case EPI_QKV_ROT: hipLaunchKernelGGL((gemm_h3_kernel<EPI_QKV_ROT, BK, NSTAGE>), dim3(blocks), dim3(NT), 0, st, a); break;
+    case EPI_CROSS_QKV: hipLaunchKernelGGL((gemm_h3_kernel<EPI_CROSS_QKV, BK, NSTAGE>), dim3(blocks), dim3(NT), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
+  if (a.R <= 0) return hipSuccess;
+  if (a.Nout % TB || a.K % kKB || a.K0 % kKB || a.K0 <= 0 || a.K0 > a.K || (a.K0 < a.K && !a.A1.p) || !a.A0.p ||
+      !a.W.p || a.A0.rows_pad < ((a.R + TB - 1) / TB) * TB || (a.K0 < a.K && a.A1.rows_pad < ((a.R + TB - 1) / TB) * TB) ||
+      a.W.rows_pad != a.Nout || (a.Yp && a.yrows_pad < a.R))
+    return hipErrorInvalidValue;
+  return gemm_h3_launch<LG_GEMM_H3_PIPE>(a, epi, st);
+}
+
+// fp32 rows -> plane image; one thread per 8-element chunk
+__global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
+                                      int* ovf) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nch = K / 8;
+  bool bad = false;
+  if (i < (size_t)R * nch) {
+    const int r = (int)(i / nch), c = (int)(i % nch);
+    const float* p = x + (size_t)r * ld + c * 8;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(p), v1 = *reinterpret_cast<const f32x4*>(p + 4);
+    f16x8 h, l;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = e < 4 ? v0[e] : v1[e - 4];
+      bad |= !(fabsf(v) <= kF16Max);
+      _Float16 a, b;
+      split2h(v, a, b);
+      h[e] = a;
+      l[e] = b;
+    }
+    const size_t off = plane_off(row0 + r, c * 8, rows_pad);
+    *reinterpret_cast<f16x8*>(planes + off) = h;
+    *reinterpret_cast<f16x8*>(planes + (size_t)rows_pad * K + off) = l;
+  }
+  if (ovf && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+}
+
+hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0, int* ovf,
+                          hipStream_t st) {
+  if (R <= 0) return hipSuccess;
+  if (K % kKB || rows_pad < row0 + R) return hipErrorInvalidValue;
+  const size_t n = (size_t)R * (K / 8);
+  hipLaunchKernelGGL(rows_to_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, R, K, ld, planes,
+                     rows_pad, row0, ovf);
+  return hipGetLastError();
+}
+
+}  // namespace lg

@@ -35,12 +35,8 @@ struct GemmArgs {
   int lda0, K0;
   const float* A1;  // [R][lda1], columns [K0, K) (nullable: K0 == K)
   int lda1;
-  const float* W;   // [Nout][ldw] (PyTorch Linear layout), k contiguous (PREC_X6)
+  const float* W;   // [Nout][ldw] (PyTorch Linear layout), k contiguous
   int ldw, K;
-  const _Float16* Wp;  // PREC_H3: three fp16 planes (h*2^11, l, h) of W * 2^sw, [3][Nout][ldw]
-  long long wps;       // elements between the planes
-  float acc_scale;     // PREC_H3: 2^-(11+sw) (accumulator -> value); 1 otherwise
-  int* ovf;            // PREC_H3: set to 1 if an A element is outside the fp16 range (nullable)
   const float* bias;  // [Nout] or null
   const float* res;   // residual [R][ldr] or null (EPI_STORE): Y = res + (acc + bias) * out_scale
   int ldr;
@@ -52,7 +48,40 @@ struct GemmArgs {
   HeadLayout hl;
 };
 
-hipError_t gemm_f32(const GemmArgs& a, int epi, int batch, int prec, hipStream_t st);
+// bf16x6 GEMM on fp32 operands (gemm.hip): the PREC_X6 linears and the similarity GEMM.
+hipError_t gemm_x6(const GemmArgs& a, int epi, int batch, hipStream_t st);
+
+// fp16x3 "linear" GEMM on plane images (common.h, gemm_h3.hip):
+//   Y = epilogue(A . W^T * acc_scale + bias), A = [A0 | A1] plane images, W = plane image of
+//   W * 2^sw (acc_scale = 2^-(11+sw)).  R rows (image rows_pad >= R, multiple of 256),
+//   Nout a multiple of 256, K0 and K multiples of 32.
+struct PlaneRef {
+  const _Float16* p;  // plane 0; plane 1 at p + ps
+  long long ps;       // elements between the two planes (= rows_pad * K)
+  int rows_pad;
+};
+struct GemmH3Args {
+  PlaneRef A0, A1;  // A1 used for k >= K0 (nullable p when K0 == K)
+  int K0, K;
+  PlaneRef W;       // rows_pad = Nout
+  int R, Nout;
+  float acc_scale, out_scale;
+  const float* bias;  // [Nout] or null
+  const float* res;   // EPI_STORE: Y = res + (...) (nullable), row stride ldr
+  int ldr;
+  float* Y;           // EPI_STORE fp32 output (nullable), row stride ldy
+  int ldy;
+  _Float16* Yp;       // EPI_STORE: also write Y as a plane image (nullable), with its rows_pad
+  long long yps;
+  int yrows_pad;
+  int* ovf;           // set to 1 when a value written into Yp / K, V planes leaves the fp16 range
+  HeadLayout hl;      // EPI_QKV_ROT / EPI_CROSS_QKV
+};
+hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st);
+// fp32 rows [R][K] (row stride ld) -> rows row0 .. row0+R-1 of a plane image (rows_pad), with
+// the fp16-range guard
+hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0, int* ovf,
+                          hipStream_t st);
 
 // Attention over head-major Q/K/V ([set][b][h][n][64]); O written row-major into ctx
 // [rows][256] at column h*64 (rows in GEMM order).  Two "sets" per launch (blockIdx.z).
@@ -61,8 +90,11 @@ struct AttnSet {
   const void* kp;    // [planes][B][H][Nk][64] (plane stride pstride): 3 bf16 (X6) / 2 fp16 (H3)
   const void* vp;    // [planes][B][H][Nk][64]
   long long pstride;
-  float* o;          // ctx + row_base*256
+  float* o;          // ctx + row_base*256 (PREC_X6)
   int Nq, Nk;
+  _Float16* op;      // PREC_H3: ctx plane image (K = 256), rows of this set start at o_row0
+  long long ops;
+  int o_rows_pad, o_row0;
 };
 hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st);
 
@@ -83,7 +115,9 @@ hipError_t positional_encoding(const PEArgs& a, hipStream_t st);
 // size = 1 + max - min of each pair's keypoints (normalize_keypoints fallback, lightglue.py:25-26)
 hipError_t kpt_extent(const float* kpts, int B, int n, float* size_out, hipStream_t st);
 
-hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, hipStream_t st);
+// In place (planes == null, PREC_X6) or into a plane image of K = 512 (PREC_H3).
+hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, _Float16* planes, int rows_pad,
+                              int* ovf, hipStream_t st);
 // y[r] = dot(x[r,:256], w) + b ; optional sigmoid
 hipError_t gemv_256(const float* x, const float* w, const float* b, float* y, int rows, int sigmoid, hipStream_t st);
 
@@ -109,10 +143,10 @@ size_t filter_workspace_floats(int B, int M, int N);
 // tmp holds 512*256 + 512 floats.
 hipError_t fold_out_proj(float* W1, float* b1, const float* Wo, const float* bo, float* tmp, hipStream_t st);
 
-// fp16x3 weight planes (PREC_H3): absmax of n floats -> *out (one block), then
-// planes [3][n] = (h*2^11, l, h) of src * 2^sw.
+// fp16x3 weight planes (PREC_H3): absmax of n floats -> *out (one block), then the plane image
+// of W [rows][K] * scale (rows_pad = rows).
 hipError_t absmax(const float* src, size_t n, float* out, hipStream_t st);
-hipError_t split_weight_h3(const float* src, size_t n, float scale, _Float16* planes, hipStream_t st);
+hipError_t split_weight_h3(const float* src, int rows, int K, float scale, _Float16* planes, hipStream_t st);
 
 // Weight repacking: dst[r,:] = src[idx[r],:] (row length `cols`).
 hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st);

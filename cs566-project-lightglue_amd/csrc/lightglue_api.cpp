@@ -119,11 +119,12 @@ struct lg_handle {
   size_t Wr, Wc, bc, Wi, bi, total;
   float* wbuf = nullptr;
   int* perm = nullptr;  // head_perm() [1024]
-  // fp16x3 planes of every GEMM weight matrix (PREC_H3), keyed by the matrix's fp32 offset
+  // fp16x3 plane images of every GEMM weight matrix (PREC_H3), keyed by the fp32 offset
   struct Planes {
-    size_t off;       // halfs into wplanes
-    long long pstride;
-    float unscale;    // 2^-(11+sw)
+    size_t off;         // halfs into wplanes
+    long long pstride;  // rows * K
+    int rows;
+    float unscale;      // 2^-(11+sw)
   };
   std::map<size_t, Planes> planes;
   _Float16* wplanes = nullptr;
@@ -277,16 +278,21 @@ void plan_layout(lg_handle* h) {
 struct Work {
   float *X, *X2, *cosb, *sinb, *cos2, *sin2, *size, *Q, *ctx, *msg, *H1, *md, *z, *tok, *sim, *aws;
   void *KP, *VP;  // operand planes of keys (qk) and values: 3 bf16 (X6) / 2 fp16 (H3) x R x 256
+  // PREC_H3 plane images (common.h), rows_pad rows: x, context, message (unfolded out_proj),
+  // FFN hidden, input descriptors (input_dim != 256)
+  _Float16 *Xp, *Cp, *Mp, *Hp, *Dp;
+  int rows_pad;
   size_t R;
   int *flags, *pos, *ind0, *ind1, *ind0b, *ind1b, *counts;
-  int* ovf;  // PREC_H3 fp16-range guard (gemm.hip)
+  int* ovf;  // PREC_H3 fp16-range guard
   int64_t *m0c, *m1c;
   float *s0c, *s1c;
   size_t bytes;
 };
 
-Work carve(char* base, int B, int M, int N, bool prune) {
+Work carve(char* base, int B, int M, int N, bool prune, int din) {
   const size_t R = (size_t)B * (M + N);
+  const size_t RP = (R + 255) / 256 * 256;
   Work w{};
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -296,17 +302,24 @@ Work carve(char* base, int B, int M, int N, bool prune) {
   };
   auto tf = [&](size_t n) { return reinterpret_cast<float*>(take(n * sizeof(float))); };
   auto ti = [&](size_t n) { return reinterpret_cast<int*>(take(n * sizeof(int))); };
+  auto th = [&](size_t n) { return reinterpret_cast<_Float16*>(take(n * sizeof(_Float16))); };
   w.X = tf(R * D);
   w.cosb = tf(R * 32);
   w.sinb = tf(R * 32);
   w.size = tf(4 * (size_t)B);
   w.R = R;
+  w.rows_pad = (int)RP;
   w.Q = tf(R * D);
   w.KP = take(3 * R * D * 2);
   w.VP = take(3 * R * D * 2);
   w.ctx = tf(R * D);
   w.msg = tf(R * D);
   w.H1 = tf(R * 2 * D);
+  w.Xp = th(2 * RP * D);
+  w.Cp = th(2 * RP * D);
+  w.Mp = th(2 * RP * D);
+  w.Hp = th(2 * RP * 2 * D);
+  w.Dp = din != D ? th(2 * RP * din) : nullptr;
   w.md = tf(R * D);
   w.z = tf(R);
   w.tok = tf(R);
@@ -339,7 +352,13 @@ lg::GemmArgs gemm_base() {
   lg::GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.out_scale = 1.f;
-  a.acc_scale = 1.f;
+  return a;
+}
+
+lg::GemmH3Args gemm_h3_base() {
+  lg::GemmH3Args a;
+  memset(&a, 0, sizeof(a));
+  a.out_scale = 1.f;
   return a;
 }
 
@@ -457,8 +476,8 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
       }
     LG_HIP(hipFreeAsync(tmp, st));
   }
-  // fp16x3 planes (h*2^11, l, h) of every GEMM weight matrix, scaled per matrix by 2^sw so that
-  // max|W 2^sw| lies in [8, 16) (common.h, gemm.hip MODE_H3)
+  // fp16x3 plane images (common.h) of every GEMM weight matrix, scaled per matrix by 2^sw so
+  // that max|W 2^sw| lies in [8, 16) (gemm_h3.hip forms the third piece, h * 2^11, in registers)
   {
     struct Mat { size_t off; int rows, K; };
     std::vector<Mat> mats;
@@ -474,7 +493,7 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
       mats.push_back({lw.Wf, D, D});
     }
     size_t total = 0;
-    for (auto& m : mats) total += 3 * (size_t)m.rows * m.K;
+    for (auto& m : mats) total += 2 * (size_t)m.rows * m.K;
     if (h->wplanes) (void)hipFree(h->wplanes);
     h->wplanes = nullptr;
     h->planes.clear();
@@ -496,9 +515,9 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
         sw = std::min(std::max(4 - E, -100), 100);
       }
       const size_t n = (size_t)mats[i].rows * mats[i].K;
-      LG_HIP(lg::split_weight_h3(h->wbuf + mats[i].off, n, std::ldexp(1.f, sw), h->wplanes + off, st));
-      h->planes[mats[i].off] = {off, (long long)n, std::ldexp(1.f, -(11 + sw))};
-      off += 3 * n;
+      LG_HIP(lg::split_weight_h3(h->wbuf + mats[i].off, mats[i].rows, mats[i].K, std::ldexp(1.f, sw), h->wplanes + off, st));
+      h->planes[mats[i].off] = {off, (long long)n, mats[i].rows, std::ldexp(1.f, -(11 + sw))};
+      off += 2 * n;
     }
   }
   h->loaded = true;
@@ -507,7 +526,7 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
 
 int lg_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
   if (!h || !bytes || B < 0 || M < 0 || N < 0) return fail(LG_E_INVALID, "bad argument");
-  *bytes = carve(nullptr, B, M, N, prune_enabled(h->cfg)).bytes;
+  *bytes = carve(nullptr, B, M, N, prune_enabled(h->cfg), h->cfg.input_dim).bytes;
   return LG_OK;
 }
 
@@ -531,31 +550,38 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   const bool do_stop = c.depth_confidence > 0.f, do_prune = c.width_confidence > 0.f;
   if ((do_stop || do_prune) && B != 1) return fail(LG_E_INVALID, "pruning / early stop require batch size 1");
   if (do_prune && (!out->prune0 || !out->prune1)) return fail(LG_E_INVALID, "prune0/prune1 outputs required with pruning");
-  const Work need = carve(nullptr, B, M0, N0, prune_enabled(c));
+  const Work need = carve(nullptr, B, M0, N0, prune_enabled(c), c.input_dim);
   if (!workspace || workspace_bytes < need.bytes)
     return fail(LG_E_WORKSPACE, "workspace too small: need " + std::to_string(need.bytes));
   LG_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
-  Work w = carve((char*)workspace, B, M0, N0, prune_enabled(c));
+  Work w = carve((char*)workspace, B, M0, N0, prune_enabled(c), c.input_dim);
   const float* Wb = h->wbuf;
   int M = M0, N = N0;
+  const int RP = w.rows_pad;
   // launch wrappers that feed lg_profile_* (algorithmic flops / bytes per launch)
-  // weights of a Linear layer: fp32 (X6) and its fp16x3 planes (H3), by fp32 offset
-  auto setw = [&](GemmArgs& g, size_t off) {
-    g.W = Wb + off;
-    const auto& pl = h->planes.at(off);
-    g.Wp = h->wplanes + pl.off;
-    g.wps = pl.pstride;
-    g.acc_scale = prec == PREC_H3 ? pl.unscale : 1.f;
-    g.ovf = w.ovf;
-  };
-  auto gemm = [&](const GemmArgs& g, int epi, int batch, int p_gemm) -> hipError_t {
+  auto gemm = [&](const GemmArgs& g, int epi, int batch) -> hipError_t {
     const int p = h->prof_begin(LG_KERNEL_GEMM, st);
-    const hipError_t e = gemm_f32(g, epi, batch, p_gemm, st);
+    const hipError_t e = gemm_x6(g, epi, batch, st);
     const double R = g.R, K = g.K, O = g.Nout;
     h->prof_end(p, 2.0 * R * K * O * batch, 4.0 * (R * K + O * K + R * O) * batch, st);
     return e;
   };
+  auto gemmh = [&](const GemmH3Args& g, int epi) -> hipError_t {
+    const int p = h->prof_begin(LG_KERNEL_GEMM, st);
+    const hipError_t e = gemm_h3(g, epi, st);
+    const double R = g.R, K = g.K, O = g.Nout;
+    h->prof_end(p, 2.0 * R * K * O, 4.0 * (R * K + O * K + R * O), st);
+    return e;
+  };
+  // fp16x3 plane image of a packed weight matrix (by its fp32 offset) / of a workspace tensor
+  auto wplanes = [&](GemmH3Args& g, size_t off) {
+    const auto& pl = h->planes.at(off);
+    g.W = {h->wplanes + pl.off, pl.pstride, pl.rows};
+    g.acc_scale = pl.unscale;
+    g.ovf = w.ovf;
+  };
+  auto image = [&](_Float16* p, int K) { return PlaneRef{p, (long long)RP * K, RP}; };
   auto attn = [&](const AttnSet& a0, const AttnSet& a1, float scale, bool cross) -> hipError_t {
     const int p = h->prof_begin(LG_KERNEL_ATTENTION, st);
     const hipError_t e = attention_f32(a0, a1, B, H, scale, prec, st);
@@ -574,18 +600,31 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     return e;
   };
 
-  // ---- input projection (lightglue.py:370-373,486-487)
+  // ---- input projection (lightglue.py:370-373,486-487); H3 also builds x's plane image
+  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.ovf, 0, sizeof(int), st));
   if (c.input_dim != D) {
-    GemmArgs g = gemm_base();
-    setw(g, h->Wi); g.ldw = c.input_dim; g.K = c.input_dim; g.K0 = c.input_dim;
-    g.bias = Wb + h->bi; g.ldy = D; g.Nout = D;
-    g.A0 = in->descriptors0; g.lda0 = c.input_dim; g.R = B * M; g.Y = w.X;
-    LG_HIP(gemm(g, EPI_STORE, 1, prec));
-    g.A0 = in->descriptors1; g.R = B * N; g.Y = w.X + (size_t)B * M * D;
-    LG_HIP(gemm(g, EPI_STORE, 1, prec));
+    if (prec == PREC_H3) {
+      const int din = c.input_dim;
+      LG_HIP(rows_to_planes(in->descriptors0, B * M, din, din, w.Dp, RP, 0, w.ovf, st));
+      LG_HIP(rows_to_planes(in->descriptors1, B * N, din, din, w.Dp, RP, B * M, w.ovf, st));
+      GemmH3Args g = gemm_h3_base();
+      g.A0 = image(w.Dp, din); g.K0 = din; g.K = din; wplanes(g, h->Wi);
+      g.bias = Wb + h->bi; g.R = B * (M + N); g.Nout = D; g.Y = w.X; g.ldy = D;
+      g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP;
+      LG_HIP(gemmh(g, EPI_STORE));
+    } else {
+      GemmArgs g = gemm_base();
+      g.W = Wb + h->Wi; g.ldw = c.input_dim; g.K = c.input_dim; g.K0 = c.input_dim;
+      g.bias = Wb + h->bi; g.ldy = D; g.Nout = D;
+      g.A0 = in->descriptors0; g.lda0 = c.input_dim; g.R = B * M; g.Y = w.X;
+      LG_HIP(gemm(g, EPI_STORE, 1));
+      g.A0 = in->descriptors1; g.R = B * N; g.Y = w.X + (size_t)B * M * D;
+      LG_HIP(gemm(g, EPI_STORE, 1));
+    }
   } else {
     LG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
     LG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
+    if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, B * (M + N), D, D, w.Xp, RP, 0, w.ovf, st));
   }
 
   // ---- keypoint normalisation + positional encoding (lightglue.py:455-456,490-494)
@@ -604,7 +643,6 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     LG_HIP(positional_encoding(p, st));
   }
 
-  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.ovf, 0, sizeof(int), st));
   if (do_prune) {
     LG_HIP(iota_fill(w.ind0, M, st));
     LG_HIP(iota_fill(w.ind1, N, st));
@@ -620,45 +658,73 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     for (int blk = 0; blk < 2; ++blk) {
       const BlockW& bw = blk == 0 ? lw.self : lw.cross;
       // QKV projection with fused rotary (self) / scale (cross) and head-major scatter
-      GemmArgs g = gemm_base();
-      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; setw(g, bw.Wqkv); g.ldw = D; g.bias = Wb + bw.bqkv;
-      g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D;
-      g.hl.B = B; g.hl.H = H; g.hl.M = M; g.hl.N = N; g.hl.cosb = w.cosb; g.hl.sinb = w.sinb;
-      g.hl.q = w.Q; g.hl.kp = w.KP; g.hl.vp = w.VP; g.hl.pstride = (long long)w.R * D;
-      g.hl.qk_scale = std::sqrt(1.f / std::sqrt(64.f));  // scale**0.5 (lightglue.py:235)
-      LG_HIP(gemm(g, blk == 0 ? EPI_QKV_ROT : EPI_CROSS_QKV, 1, prec));
+      HeadLayout hl;
+      hl.B = B; hl.H = H; hl.M = M; hl.N = N; hl.cosb = w.cosb; hl.sinb = w.sinb;
+      hl.q = w.Q; hl.kp = w.KP; hl.vp = w.VP; hl.pstride = (long long)w.R * D;
+      hl.qk_scale = std::sqrt(1.f / std::sqrt(64.f));  // scale**0.5 (lightglue.py:235)
+      const int epi_qkv = blk == 0 ? EPI_QKV_ROT : EPI_CROSS_QKV;
+      if (prec == PREC_H3) {
+        GemmH3Args g = gemm_h3_base();
+        g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, bw.Wqkv); g.bias = Wb + bw.bqkv;
+        g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D; g.hl = hl;
+        LG_HIP(gemmh(g, epi_qkv));
+      } else {
+        GemmArgs g = gemm_base();
+        g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wqkv; g.ldw = D; g.bias = Wb + bw.bqkv;
+        g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D; g.hl = hl;
+        LG_HIP(gemm(g, epi_qkv, 1));
+      }
       const size_t img1 = (size_t)B * H * M * 64;
       const long long ps = (long long)w.R * D;
       AttnSet a0, a1;
       // planes are 2-byte elements in both formats (bf16 / fp16)
       const void* kp1 = static_cast<const char*>(w.KP) + 2 * img1;
       const void* vp1 = static_cast<const char*>(w.VP) + 2 * img1;
+      float* ctx1 = w.ctx + (size_t)B * M * D;
       if (blk == 0) {  // self: q/k/v of the same image, scale 1/sqrt(64) (SDPA default)
-        a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M};
-        a1 = {w.Q + img1, kp1, vp1, ps, w.ctx + (size_t)B * M * D, N, N};
-        LG_HIP(attn(a0, a1, 0.125f, false));
+        a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M, w.Cp, (long long)RP * D, RP, 0};
+        a1 = {w.Q + img1, kp1, vp1, ps, ctx1, N, N, w.Cp, (long long)RP * D, RP, B * M};
       } else {  // cross: qk fp32 in w.Q and as planes in w.KP, v planes in w.VP
-        a0 = {w.Q, kp1, vp1, ps, w.ctx, M, N};
-        a1 = {w.Q + img1, w.KP, w.VP, ps, w.ctx + (size_t)B * M * D, N, M};
-        LG_HIP(attn(a0, a1, 1.0f, true));
+        a0 = {w.Q, kp1, vp1, ps, w.ctx, M, N, w.Cp, (long long)RP * D, RP, 0};
+        a1 = {w.Q + img1, w.KP, w.VP, ps, ctx1, N, M, w.Cp, (long long)RP * D, RP, B * M};
       }
-      // out projection (skipped when folded into ffn.0 at load time: ffn.0 then reads ctx)
-      if (!h->fold) {
+      LG_HIP(attn(a0, a1, blk == 0 ? 0.125f : 1.0f, blk == 1));
+      if (prec == PREC_H3) {
+        // out projection (skipped when folded into ffn.0 at load time: ffn.0 then reads ctx)
+        if (!h->fold) {
+          GemmH3Args g = gemm_h3_base();
+          g.A0 = image(w.Cp, D); g.K0 = D; g.K = D; wplanes(g, bw.Wo); g.bias = Wb + bw.bo;
+          g.R = R; g.Nout = D; g.Yp = w.Mp; g.yps = (long long)RP * D; g.yrows_pad = RP;
+          LG_HIP(gemmh(g, EPI_STORE));
+        }
+        // FFN: Linear(cat[x, msg]) -> LN -> GELU -> Linear + residual (x also as plane image)
+        GemmH3Args g = gemm_h3_base();
+        g.A0 = image(w.Xp, D); g.K0 = D; g.A1 = image(h->fold ? w.Cp : w.Mp, D); g.K = 2 * D;
+        wplanes(g, bw.W1); g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
+        LG_HIP(gemmh(g, EPI_STORE));
+        LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, w.Hp, RP, w.ovf, st));
+        g = gemm_h3_base();
+        g.A0 = image(w.Hp, 2 * D); g.K0 = 2 * D; g.K = 2 * D; wplanes(g, bw.W2); g.bias = Wb + bw.b2;
+        g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
+        g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP;
+        LG_HIP(gemmh(g, EPI_STORE));
+      } else {
+        if (!h->fold) {
+          GemmArgs g = gemm_base();
+          g.A0 = w.ctx; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wo; g.ldw = D; g.bias = Wb + bw.bo;
+          g.R = R; g.Nout = D; g.Y = w.msg; g.ldy = D;
+          LG_HIP(gemm(g, EPI_STORE, 1));
+        }
+        GemmArgs g = gemm_base();
+        g.A0 = w.X; g.lda0 = D; g.K0 = D; g.A1 = h->fold ? w.ctx : w.msg; g.lda1 = D; g.K = 2 * D;
+        g.W = Wb + bw.W1; g.ldw = 2 * D; g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
+        LG_HIP(gemm(g, EPI_STORE, 1));
+        LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, nullptr, 0, nullptr, st));
         g = gemm_base();
-        g.A0 = w.ctx; g.lda0 = D; g.K0 = D; g.K = D; setw(g, bw.Wo); g.ldw = D; g.bias = Wb + bw.bo;
-        g.R = R; g.Nout = D; g.Y = w.msg; g.ldy = D;
-        LG_HIP(gemm(g, EPI_STORE, 1, prec));
+        g.A0 = w.H1; g.lda0 = 2 * D; g.K0 = 2 * D; g.K = 2 * D; g.W = Wb + bw.W2; g.ldw = 2 * D; g.bias = Wb + bw.b2;
+        g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
+        LG_HIP(gemm(g, EPI_STORE, 1));
       }
-      // FFN: Linear(cat[x, msg]) -> LN -> GELU -> Linear + residual
-      g = gemm_base();
-      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.A1 = h->fold ? w.ctx : w.msg; g.lda1 = D; g.K = 2 * D;
-      setw(g, bw.W1); g.ldw = 2 * D; g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
-      LG_HIP(gemm(g, EPI_STORE, 1, prec));
-      LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, st));
-      g = gemm_base();
-      g.A0 = w.H1; g.lda0 = 2 * D; g.K0 = 2 * D; g.K = 2 * D; setw(g, bw.W2); g.ldw = 2 * D; g.bias = Wb + bw.b2;
-      g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
-      LG_HIP(gemm(g, EPI_STORE, 1, prec));
     }
     if (i == L - 1) break;
 
@@ -705,6 +771,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       N = N2;
       if (M == 0 || N == 0)
         return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size (all keypoints pruned)");
+      if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, M + N, D, D, w.Xp, RP, 0, w.ovf, st));
     }
   }
   out->stop_layer = stop;
@@ -716,16 +783,24 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   const LayerW& la = h->layers[stop];
   const int R = B * (M + N);
   {
-    GemmArgs g = gemm_base();
-    g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; setw(g, la.Wf); g.ldw = D; g.bias = Wb + la.bf;
-    g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
-    LG_HIP(gemm(g, EPI_STORE, 1, prec));
+    if (prec == PREC_H3) {
+      GemmH3Args g = gemm_h3_base();
+      g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, la.Wf); g.bias = Wb + la.bf;
+      g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
+      LG_HIP(gemmh(g, EPI_STORE));
+    } else {
+      GemmArgs g = gemm_base();
+      g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + la.Wf; g.ldw = D; g.bias = Wb + la.bf;
+      g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
+      LG_HIP(gemm(g, EPI_STORE, 1));
+    }
     LG_HIP(gemv_256(w.X, Wb + la.wm, Wb + la.bm, w.z, R, 0, st));
-    g = gemm_base();
+    // similarity: both operands are run-time values -> bf16x6 (full fp32 range)
+    GemmArgs g = gemm_base();
     g.A0 = w.md; g.lda0 = D; g.K0 = D; g.K = D; g.sA = (long long)M * D;
     g.W = w.md + (size_t)B * M * D; g.ldw = D; g.sW = (long long)N * D;
     g.R = M; g.Nout = N; g.Y = w.sim; g.ldy = N; g.sY = (long long)M * N;
-    LG_HIP(gemm(g, EPI_STORE, B, PREC_X6));  // both operands are run-time values: full range
+    LG_HIP(gemm(g, EPI_STORE, B));
   }
   AssignArgs aa;
   aa.sim = w.sim; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = out->log_assignment; aa.ws = w.aws;
@@ -755,7 +830,7 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
   if (rc != LG_OK || first != lg::PREC_H3) return rc;
   // fp16-range guard: an operand outside the fp16 range makes the fp16x3 result unreliable;
   // recompute the whole forward in bf16x6 (full fp32 range) -- rare by design
-  const Work w = carve((char*)workspace, in->B, in->M, in->N, prune_enabled(h->cfg));
+  const Work w = carve((char*)workspace, in->B, in->M, in->N, prune_enabled(h->cfg), h->cfg.input_dim);
   int flag = 0;
   hipStream_t st = (hipStream_t)stream;
   LG_HIP(hipMemcpyAsync(&flag, w.ovf, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -7,12 +7,39 @@
 #include <vector>
 
 #include "../cs566-project-lightglue_amd/csrc/gemm.hip"
+#include "../cs566-project-lightglue_amd/csrc/elementwise.hip"
+#include "../cs566-project-lightglue_amd/csrc/gemm_h3.hip"
 
 using namespace lg;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
 
 struct Shape { int R, K, N; const char* name; };
+
+static _Float16* g_planes = nullptr;  // plane image of W * 2^sw
+static _Float16* g_aplanes = nullptr; // plane image of A
+static float g_unscale = 1.f;
+
+template <int BK = 32, int NS = 2, int EPI = EPI_STORE>
+double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out, _Float16* Yp) {
+  GemmH3Args a;
+  memset(&a, 0, sizeof(a));
+  a.A0 = {g_aplanes, (long long)s.R * s.K, s.R}; a.K0 = s.K; a.K = s.K;
+  a.W = {g_planes, (long long)s.N * s.K, s.N}; a.R = s.R; a.Nout = s.N;
+  a.acc_scale = g_unscale; a.out_scale = 1.f; a.bias = bias; a.Y = Y; a.ldy = s.N;
+  if (planes_out) { a.Yp = Yp; a.yps = (long long)s.R * s.N; a.yrows_pad = s.R; }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK((gemm_h3_launch<BK, NS>(a, EPI, 0)));
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK((gemm_h3_launch<BK, NS>(a, EPI, 0)));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
 
 template <int MODE, int BM, int BN, int BK, int WM, int WN, int EPI = EPI_STORE>
 double run(const Shape& s, float* A, float* W, float* bias, float* Y, int iters) {
@@ -65,6 +92,14 @@ int main() {
     fill<<<(s.N * (size_t)s.K + 255) / 256, 256>>>(W, (size_t)s.N * s.K, 2);
     fill<<<(s.N + 255) / 256, 256>>>(bias, s.N, 3);
     ref64<<<(RR * s.N + 255) / 256, 256>>>(A, W, bias, Yr, Sr, RR, s.K, s.N);
+    CK(hipMalloc(&g_planes, (size_t)2 * s.N * s.K * 2));
+    CK(hipMalloc(&g_aplanes, (size_t)2 * s.R * s.K * 2));
+    // fill() draws from [-1, 1): max|W| < 1 -> scale 2^3 puts max|W 2^sw| in [4, 8) (< 16)
+    CK(split_weight_h3(W, s.N, s.K, 8.f, g_planes, 0));
+    CK(rows_to_planes(A, s.R, s.K, s.K, g_aplanes, s.R, 0, nullptr, 0));
+    g_unscale = ldexpf(1.f, -(11 + 3));
+    _Float16* Yp;
+    CK(hipMalloc(&Yp, (size_t)2 * s.R * s.N * 2));
     CK(hipDeviceSynchronize());
     std::vector<double> yr((size_t)RR * s.N), sr((size_t)RR * s.N);
     CK(hipMemcpy(yr.data(), Yr, yr.size() * 8, hipMemcpyDeviceToHost));
@@ -82,13 +117,14 @@ int main() {
     };
     const int it = 20;
     double ms;
-    ms = run<MODE_F32, 256, 128, 16, 64, 64>(s, A, W, bias, Y, it); rep("f32 256x128x16 (8w)", ms, true);
     ms = run<MODE_X6, 256, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x256x16 (16w)", ms, true);
-    ms = run<MODE_X6, 256, 256, 16, 64, 64, EPI_PROBE>(s, A, W, bias, Y, it); rep("x6  256x256x16 no store", ms, false);
-    ms = run<MODE_X6, 128, 256, 32, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x256x32 (8w)", ms, true);
-    ms = run<MODE_X6, 256, 128, 32, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x128x32 (8w)", ms, true);
-    ms = run<MODE_X6, 128, 128, 32, 64, 64>(s, A, W, bias, Y, it); rep("x6  128x128x32 (4w)", ms, true);
-    ms = run<MODE_X6, 256, 256, 16, 64, 128>(s, A, W, bias, Y, it); rep("x6  256x256x16 w64x128 (8w)", ms, true);
+    ms = run_h3<32, 2>(s, bias, Y, it, false, Yp); rep("h3  planes bk32 x2", ms, true);
+    ms = run_h3<16, 4>(s, bias, Y, it, false, Yp); rep("h3  planes bk16 x4", ms, true);
+    ms = run_h3<16, 3>(s, bias, Y, it, false, Yp); rep("h3  planes bk16 x3", ms, true);
+    ms = run_h3<16, 2>(s, bias, Y, it, false, Yp); rep("h3  planes bk16 x2", ms, true);
+    ms = run_h3<32, 2>(s, bias, Y, it, true, Yp); rep("h3  bk32 x2 + plane-image out", ms, true);
+    CK(hipFree(Yp)); CK(hipFree(g_aplanes));
+    CK(hipFree(g_planes));
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(bias)); CK(hipFree(Y)); CK(hipFree(Yr)); CK(hipFree(Sr));
   }
   return 0;

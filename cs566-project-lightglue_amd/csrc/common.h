@@ -100,11 +100,12 @@ __device__ __forceinline__ f32x16 mfma_h3(const f16x8& xh, const f16x8& xl, cons
 
 // ---- fp16x3 operand images in HBM ("plane images") ----------------------------------------
 // A [rows][K] fp32 matrix that feeds the fp16x3 GEMM (gemm_h3.hip) is stored as its two fp16
-// pieces, k-blocked and pre-swizzled exactly like the GEMM's LDS tile, so that a k-tile of 256
-// rows is one contiguous 16 KiB block per plane and the GEMM stages it with plain LDS-DMA copies:
+// pieces, k-blocked and pre-swizzled exactly like the GEMM's LDS tile, so that a k-tile of a row
+// tile is one contiguous block per plane and the GEMM stages it with plain LDS-DMA copies:
 //   [plane 0 (h) | plane 1 (l * 2^11)][K / 32 kblocks][rows_pad][32]
-// with the 16-byte chunk c (k = 8c..8c+7 of the kblock) of row r stored at chunk c ^ swz(r).
-// rows_pad is a multiple of 256 (the GEMM row tile).
+// i.e. 64-byte rows of four 16-byte chunks; chunk c (k = 8c..8c+7 of the kblock) of row r is
+// stored at chunk c ^ plane_swz(r) (the swizzle that makes the GEMM's ds_read_b128 fragment
+// groups {0-3,12-15,20-27} conflict-free).  rows_pad is a multiple of 256 (the GEMM row tile).
 constexpr int kKB = 32;  // k-block (columns per plane row)
 __device__ __forceinline__ int plane_swz(int row) { return (row >> 2) & 3; }
 // element offset of (row, k) inside one plane of an image with `rows_pad` rows

@@ -16,22 +16,23 @@
 // by 32 and chunk-swizzled exactly like the LDS tile (common.h).  The producers write them (the
 // previous GEMM's epilogue, the attention epilogue, the LayerNorm+GELU kernel; W at load time,
 // pre-scaled by 2^sw), so this kernel does no conversion: every k-tile is four contiguous
-// 16 KiB blocks (A h, A l, W h, W l) copied HBM/L2 -> LDS by global_load_lds_dwordx4 (one
-// 1 KiB wave-instruction each, 4 per wave), double-buffered, one k-tile in flight while the
-// other is multiplied.  The third piece of W (h * 2^11) is formed in registers (one packed fp16
-// multiply per fragment register), and the product is accumulated as three fp16 MFMAs per
-// 32x32x16 block (common.h mfma_h3).
-// Tile: 256 x 256 x 32, 16 waves as 4 x 4 of 64 x 64 (2 x 2 MFMA tiles each); 128 KiB LDS,
-// one workgroup per CU; blockIdx -> tile through a bijective XCD remap so the column tiles of
-// one row panel share an XCD's L2.
+// blocks (A h, A l, W h, W l) copied HBM/L2 -> LDS by global_load_lds_dwordx4 (1 KiB per
+// wave-instruction, uniform base in SGPRs) into a ring of LDS stages, NSTAGE-1 k-tiles in
+// flight.  The third piece of W (h * 2^11) is formed in registers (one packed fp16 multiply per
+// fragment register), and the product is accumulated as three fp16 MFMAs per 32x32x16 block
+// (common.h mfma_h3).
+// Tile: BM x 256 x 32, BM/16 waves as (BM/64) x 4 of 64 x 64 (2 x 2 MFMA tiles each); at
+// BM = 256, two 64 KiB stages fill 128 KiB of LDS, one workgroup per CU (tools/kbench_gemm.hip:
+// 256 x 256 x 32 beat 128 x 256 at two workgroups per CU and every k-tile of 16 with 2-4
+// stages).  blockIdx -> tile through a bijective XCD remap so the column tiles of one row panel
+// share an XCD's L2.
 #include "common.h"
 #include "kernels.h"
 
 namespace lg {
 
 namespace {
-constexpr int TB = 256;                    // row / column tile
-constexpr int NT = 1024;                   // 16 waves
+constexpr int TB = 256;  // column tile; rows_pad granule
 
 typedef __attribute__((address_space(3))) char lds_char;
 
@@ -41,14 +42,15 @@ __device__ __forceinline__ int xcd_remap_h3(int id, int n) {
   return xcd * base + (xcd < extra ? xcd : extra) + local;
 }
 
-// one global_load_lds_dwordx4: lane i copies 16 bytes from gsrc (per lane) to LDS byte address
-// lds + 16 i (lds wave-uniform).  Inline asm: the compiler neither counts it nor orders LDS
-// reads behind it -- the k-loop waits for it with explicit vmcnt + barrier.
-__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+// one global_load_lds_dwordx4: lane i copies the 16 bytes at base + voff (base wave-uniform,
+// in SGPRs; voff per lane) to LDS byte address lds + 16 i (lds wave-uniform).  Inline asm: the
+// compiler neither counts it nor orders LDS reads behind it -- the k-loop waits for it with an
+// explicit vmcnt + barrier.
+__device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t lds) {
   unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(gsrc), "s"(lds)
+               : "v"(voff), "s"(base), "s"(lds)
                : "memory");
 }
 
@@ -66,63 +68,59 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 }
 }  // namespace
 
-// LDS image of one k-tile: four plane tiles (A h, A l, W h, W l) of 256 rows x BK fp16, rows of
-// BK*2 bytes, 16-byte chunk c of row r at c ^ lds_swz(r) (conflict-free ds_read_b128 groups)
-template <int BK>
-__device__ __forceinline__ int lds_swz(int r) {
-  return BK == 32 ? plane_swz(r) : (r >> 3) & 1;
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int EPI, int BK, int NSTAGE>
-__global__ __launch_bounds__(NT) void gemm_h3_kernel(GemmH3Args g) {
-  constexpr int PT_BYTES = TB * BK * 2;      // one plane tile
-  constexpr int STAGE_BYTES = 4 * PT_BYTES;  // A h, A l, W h, W l
-  constexpr int DMA_PER_WAVE = STAGE_BYTES / 1024 / 16;
-  constexpr int CPR = BK / 8;                // 16-byte chunks per row
-  static_assert(BK == 16 || BK == 32, "k-tile");
+template <int EPI, int BM, int NSTAGE>
+__global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
+  constexpr int BN = TB;                     // column tile
+  constexpr int NW = BM / 16;                // waves: (BM/64) x 4 of 64 x 64
+  constexpr int BK = kKB;                    // k-tile = one k-block of the plane images (32)
+  constexpr int APT = BM * BK * 2;           // one A plane tile (bytes)
+  constexpr int WPT = BN * BK * 2;           // one W plane tile
+  constexpr int STAGE_BYTES = 2 * APT + 2 * WPT;
+  constexpr int PIECES = STAGE_BYTES / 1024; // 1 KiB LDS-DMA pieces per stage
+  constexpr int PPW = PIECES / NW;
+  static_assert(PIECES % NW == 0, "pieces per wave");
   __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE_BYTES];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, half = lane >> 5;
   const int wm0 = (wave >> 2) * 64, wn0 = (wave & 3) * 64;
 
-  const int num_m = (g.R + TB - 1) / TB, num_n = g.Nout / TB;
+  const int num_m = (g.R + BM - 1) / BM, num_n = g.Nout / BN;
   const int tile = xcd_remap_h3(blockIdx.x, num_m * num_n);
   const int tm = tile / num_n, tn = tile - tm * num_n;
-  const int m0 = tm * TB, n0 = tn * TB;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int nk = g.K / BK, nk0 = g.K0 / BK;
 
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)smem);
 
-  // k-tile kt -> stage: wave w copies the 1 KiB blocks q = DMA_PER_WAVE*w + i of the stage
-  // (tensor, plane and block wave-uniform).  Lane i of a block lands on LDS chunk position
-  // i % CPR of local row blk*(1024/(BK*2)) + i / CPR; it fetches the k-chunk stored there
-  // (LDS swizzle) from its place in the HBM plane image (image swizzle, common.h).
+  // k-tile kt of a plane image is one contiguous block per plane (the tile's rows of k-block kt),
+  // already in the LDS tile's swizzled layout: staging is a straight copy.  The stage is cut into
+  // 1 KiB pieces [A h | A l | W h | W l]; wave w copies pieces PPW*w .. PPW*w + PPW-1.
+  const uint32_t voff = lane * 16;
   auto issue = [&](int kt, int stage) {
 #pragma unroll
-    for (int i = 0; i < DMA_PER_WAVE; ++i) {
-      const int q = wave * DMA_PER_WAVE + i;
-      constexpr int QPT = PT_BYTES / 1024;  // blocks per plane tile
-      const int tensor = q / (2 * QPT), pl = (q / QPT) & 1, blk = q % QPT;
-      const int r = blk * (1024 / (BK * 2)) + lane / CPR;  // row in the tile
-      const int c = (lane % CPR) ^ lds_swz<BK>(r);         // k-chunk within the k-tile
-      const int k = kt * BK + c * 8;                       // column of A / W
-      const _Float16* src;
-      if (tensor == 0) {
-        const bool first = k < g.K0;
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;  // wave-uniform
+      const char* src;
+      if (q < 2 * (APT / 1024)) {
+        const int pl = q / (APT / 1024), pc = q % (APT / 1024);
+        const bool first = kt < nk0;
         const PlaneRef& A = first ? g.A0 : g.A1;
-        src = A.p + pl * A.ps + plane_off(m0 + r, first ? k : k - g.K0, A.rows_pad);
+        const int kb = first ? kt : kt - nk0;
+        src = reinterpret_cast<const char*>(A.p + pl * A.ps + ((size_t)kb * A.rows_pad + m0) * BK) + pc * 1024;
       } else {
-        src = g.W.p + pl * g.W.ps + plane_off(n0 + r, k, g.W.rows_pad);
+        const int qw = q - 2 * (APT / 1024);
+        const int pl = qw / (WPT / 1024), pc = qw % (WPT / 1024);
+        src = reinterpret_cast<const char*>(g.W.p + pl * g.W.ps + ((size_t)kt * g.W.rows_pad + n0) * BK) + pc * 1024;
       }
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + stage * STAGE_BYTES + (tensor * 2 + pl) * PT_BYTES + blk * 1024);
-      dma16(src, dst);
+      dma16(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
     }
   };
 
@@ -132,8 +130,9 @@ __global__ __launch_bounds__(NT) void gemm_h3_kernel(GemmH3Args g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0.f};
 
-  auto frag = [&](const char* st, int t, int r, int c) {
-    return *reinterpret_cast<const f16x8*>(st + t * PT_BYTES + r * (BK * 2) + ((c ^ lds_swz<BK>(r)) << 4));
+  // fragment (row r, 16-byte k-chunk c) of the plane tile at byte offset t0 of a stage
+  auto frag = [&](const char* st, int t0, int r, int c) {
+    return *reinterpret_cast<const f16x8*>(st + t0 + r * (BK * 2) + ((c ^ plane_swz(r)) << 4));
   };
   auto compute = [&](int stage) {
     const char* st = smem + stage * STAGE_BYTES;
@@ -145,13 +144,13 @@ __global__ __launch_bounds__(NT) void gemm_h3_kernel(GemmH3Args g) {
       for (int i = 0; i < 2; ++i) {
         const int r = wm0 + i * 32 + l32;
         ah[i] = frag(st, 0, r, c);
-        al[i] = frag(st, 1, r, c);
+        al[i] = frag(st, APT, r, c);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int r = wn0 + j * 32 + l32;
-        wh[j] = frag(st, 2, r, c);
-        wl[j] = frag(st, 3, r, c);
+        wh[j] = frag(st, 2 * APT, r, c);
+        wl[j] = frag(st, 2 * APT + WPT, r, c);
         whs[j] = wh[j] * (_Float16)kLoScale;  // exact: |W_h| < 16
       }
 #pragma unroll
@@ -161,19 +160,18 @@ __global__ __launch_bounds__(NT) void gemm_h3_kernel(GemmH3Args g) {
     }
   };
 
-  // ring of NSTAGE stages, NSTAGE-1 k-tiles in flight; one barrier per k-tile:
-  //   wait for my copies of tile kt -> barrier (everyone's copies landed AND everyone finished
-  //   reading stage (kt-1) % NSTAGE) -> refill that stage with tile kt+NSTAGE-1 -> multiply tile kt
+  // ring of NSTAGE stages, NSTAGE-1 k-tiles in flight; one barrier per k-tile: wait for my
+  // copies of tile kt -> barrier (everyone's copies landed AND everyone is done reading stage
+  // (kt-1) % NSTAGE) -> refill that stage with tile kt+NSTAGE-1 -> multiply tile kt
 #pragma unroll
   for (int p = 0; p < NSTAGE - 1; ++p)
     if (p < nk) issue(p, p);
   for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(NSTAGE - 1, nk - kt) - 1;  // my tiles in flight beyond kt
-    if (ahead >= 3) wait_vm<3 * DMA_PER_WAVE>();
-    else if (ahead == 2) wait_vm<2 * DMA_PER_WAVE>();
-    else if (ahead == 1) wait_vm<DMA_PER_WAVE>();
+    const int ahead = min(NSTAGE - 2, nk - 1 - kt);  // my k-tiles in flight beyond kt
+    if (NSTAGE >= 4 && ahead >= 2) wait_vm<2 * PPW>();
+    else if (NSTAGE >= 3 && ahead >= 1) wait_vm<PPW>();
     else wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of the stage to be refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
@@ -185,34 +183,85 @@ __global__ __launch_bounds__(NT) void gemm_h3_kernel(GemmH3Args g) {
 
   // ------------------------------------------------------------------ epilogues
   bool bad = false;
-  if constexpr (EPI == EPI_STORE) {
+  if constexpr (EPI == EPI_PROBE) {
+    // timing probe (tools/kbench_gemm.hip): keeps the accumulators live, stores nothing
+    float t = 0.f;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn0 + j * 32 + l32;
-      const float bj = g.bias ? g.bias[col] : 0.f;
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+    if (t == 1234.5678f) g.Y[tid] = t;
+  } else if constexpr (EPI == EPI_STORE) {
+    // Transposed through LDS (free after the k-loop; 8 KiB per wave per 32-row pass) so that every
+    // lane owns 8 consecutive columns of a row: fp32 stores, residual loads and plane-image
+    // stores are then 16 bytes per lane.  LDS element (r, c) of a pass at r*64 + (c ^ 4*(r&1))
+    // (conflict-free ds_write_b32 rows and ds_read_b128 groups).
+    static_assert(NW * 32 * 64 * 4 <= NSTAGE * STAGE_BYTES, "epilogue scratch");
+    float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
+    const int cq = (lane & 7) * 8;                     // first of the lane's 8 columns (in the wave tile)
+    const int col0 = n0 + wn0 + cq;
+    f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+    if (g.bias) {
+      b0 = *reinterpret_cast<const f32x4*>(g.bias + col0);
+      b1 = *reinterpret_cast<const f32x4*>(g.bias + col0 + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm0 + i * 32 + row32(r, half);
-          float v = fmaf(acc[i][j][r], g.acc_scale, bj) * g.out_scale;
-          if (row < g.R && g.res) v = g.res[(size_t)row * g.ldr + col] + v;
-          if (g.Y && row < g.R) g.Y[(size_t)row * g.ldy + col] = v;
+          const int rr = row32(r, half), c = j * 32 + l32;
+          ep[rr * 64 + (c ^ ((rr & 1) << 2))] = acc[i][j][r];
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int rr = (lane >> 3) + 8 * k;
+        const int row = m0 + wm0 + i * 32 + rr;
+        const int sw = (rr & 1) << 2;
+        f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
+        f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
+        if (row < g.R) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v0[e] = fmaf(v0[e], g.acc_scale, b0[e]) * g.out_scale;
+            v1[e] = fmaf(v1[e], g.acc_scale, b1[e]) * g.out_scale;
+          }
+          if (g.res) {
+            const float* rp = g.res + (size_t)row * g.ldr + col0;
+            const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp), r1 = *reinterpret_cast<const f32x4*>(rp + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v0[e] = r0[e] + v0[e];
+              v1[e] = r1[e] + v1[e];
+            }
+          }
+          if (g.Y) {
+            float* yp = g.Y + (size_t)row * g.ldy + col0;
+            *reinterpret_cast<f32x4*>(yp) = v0;
+            *reinterpret_cast<f32x4*>(yp + 4) = v1;
+          }
           if (g.Yp) {
-            // plane image: lanes (2m, 2m+1) exchange pieces; the even lane stores the h pair,
-            // the odd lane the l pair (4 bytes each)
-            _Float16 h, l;
-            split2h(v, h, l);
-            bad |= row < g.R && !(fabsf(v) <= kF16Max);
-            const uint32_t mine = (uint32_t)__builtin_bit_cast(uint16_t, h) |
-                                  ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
-            const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
-            const bool odd = l32 & 1;
-            const uint32_t word = odd ? ((other >> 16) | (mine & 0xffff0000u)) : ((mine & 0xffffu) | (other << 16));
-            if (row < g.R)
-              *reinterpret_cast<uint32_t*>(g.Yp + (odd ? g.yps : 0) + plane_off(row, col & ~1, g.yrows_pad)) = word;
+            f16x8 h, l;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float v = e < 4 ? v0[e] : v1[e - 4];
+              bad |= !(fabsf(v) <= kF16Max);
+              _Float16 a, c;
+              split2h(v, a, c);
+              h[e] = a;
+              l[e] = c;
+            }
+            const size_t off = plane_off(row, col0, g.yrows_pad);
+            *reinterpret_cast<f16x8*>(g.Yp + off) = h;
+            *reinterpret_cast<f16x8*>(g.Yp + g.yps + off) = l;
           }
         }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
   } else {
     // Head-major scatter (see gemm.hip): the wave's 64 columns are one (type t, head) block and
@@ -220,7 +269,7 @@ __global__ __launch_bounds__(NT) void gemm_h3_kernel(GemmH3Args g) {
     //   self  (EPI_QKV_ROT):   t0 -> q fp32 (rotary), t1 -> k planes (rotary), t2 -> v planes
     //   cross (EPI_CROSS_QKV): t0 -> qk fp32 * scale^0.5 and qk planes,        t1 -> v planes
     int* rowinfo = reinterpret_cast<int*>(smem);  // the k-loop ended with a barrier
-    for (int r = tid; r < TB; r += NT) {
+    for (int r = tid; r < BM; r += BM * 4) {
       int base = 0, stride = 0;
       if (m0 + r < g.R) head_row_base_h3(g.hl, m0 + r, base, stride);
       rowinfo[2 * r] = base;
@@ -273,22 +322,24 @@ __global__ __launch_bounds__(NT) void gemm_h3_kernel(GemmH3Args g) {
   if (g.ovf && __ballot(bad) != 0ull && lane == 0) atomicOr(g.ovf, 1);
 }
 
-#ifndef LG_GEMM_H3_PIPE
-// BK, stages (tools/kbench_gemm.hip)
-#define LG_GEMM_H3_PIPE 32, 2
-#endif
-
-template <int BK, int NSTAGE>
+template <int BM, int NSTAGE>
 hipError_t gemm_h3_launch(const GemmH3Args& a, int epi, hipStream_t st) {
-  const int blocks = ((a.R + TB - 1) / TB) * (a.Nout / TB);
+  const int blocks = ((a.R + BM - 1) / BM) * (a.Nout / TB);
+  const dim3 grid(blocks), block(BM * 4);
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_STORE, BK, NSTAGE>), dim3(blocks), dim3(NT), 0, st, a); break;
-    case EPI_QKV_ROT: hipLaunchKernelGGL((gemm_h3_kernel<EPI_QKV_ROT, BK, NSTAGE>), dim3(blocks), dim3(NT), 0, st, a); break;
-    case EPI_CROSS_QKV: hipLaunchKernelGGL((gemm_h3_kernel<EPI_CROSS_QKV, BK, NSTAGE>), dim3(blocks), dim3(NT), 0, st, a); break;
+    case EPI_STORE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_STORE, BM, NSTAGE>), grid, block, 0, st, a); break;
+    case EPI_QKV_ROT: hipLaunchKernelGGL((gemm_h3_kernel<EPI_QKV_ROT, BM, NSTAGE>), grid, block, 0, st, a); break;
+    case EPI_CROSS_QKV: hipLaunchKernelGGL((gemm_h3_kernel<EPI_CROSS_QKV, BM, NSTAGE>), grid, block, 0, st, a); break;
+    case EPI_PROBE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_PROBE, BM, NSTAGE>), grid, block, 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
+
+#ifndef LG_GEMM_H3_TILE
+// BM (rows per workgroup; 4*BM threads), LDS stages -- tools/kbench_gemm.hip
+#define LG_GEMM_H3_TILE 256, 2
+#endif
 
 hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
   if (a.R <= 0) return hipSuccess;
@@ -296,7 +347,7 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
       !a.W.p || a.A0.rows_pad < ((a.R + TB - 1) / TB) * TB || (a.K0 < a.K && a.A1.rows_pad < ((a.R + TB - 1) / TB) * TB) ||
       a.W.rows_pad != a.Nout || (a.Yp && a.yrows_pad < a.R))
     return hipErrorInvalidValue;
-  return gemm_h3_launch<LG_GEMM_H3_PIPE>(a, epi, st);
+  return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
 }
 
 // fp32 rows -> plane image; one thread per 8-element chunk

@@ -20,7 +20,7 @@ static _Float16* g_planes = nullptr;  // plane image of W * 2^sw
 static _Float16* g_aplanes = nullptr; // plane image of A
 static float g_unscale = 1.f;
 
-template <int BK = 32, int NS = 2, int EPI = EPI_STORE>
+template <int BM, int NS, int EPI = EPI_STORE>
 double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out, _Float16* Yp) {
   GemmH3Args a;
   memset(&a, 0, sizeof(a));
@@ -30,10 +30,10 @@ double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out,
   if (planes_out) { a.Yp = Yp; a.yps = (long long)s.R * s.N; a.yrows_pad = s.R; }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  CK((gemm_h3_launch<BK, NS>(a, EPI, 0)));
+  CK((gemm_h3_launch<BM, NS>(a, EPI, 0)));
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK((gemm_h3_launch<BK, NS>(a, EPI, 0)));
+  for (int i = 0; i < iters; ++i) CK((gemm_h3_launch<BM, NS>(a, EPI, 0)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -118,11 +118,9 @@ int main() {
     const int it = 20;
     double ms;
     ms = run<MODE_X6, 256, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x256x16 (16w)", ms, true);
-    ms = run_h3<32, 2>(s, bias, Y, it, false, Yp); rep("h3  planes bk32 x2", ms, true);
-    ms = run_h3<16, 4>(s, bias, Y, it, false, Yp); rep("h3  planes bk16 x4", ms, true);
-    ms = run_h3<16, 3>(s, bias, Y, it, false, Yp); rep("h3  planes bk16 x3", ms, true);
-    ms = run_h3<16, 2>(s, bias, Y, it, false, Yp); rep("h3  planes bk16 x2", ms, true);
-    ms = run_h3<32, 2>(s, bias, Y, it, true, Yp); rep("h3  bk32 x2 + plane-image out", ms, true);
+    ms = run_h3<256, 2>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2", ms, true);
+    ms = run_h3<256, 2>(s, bias, Y, it, true, Yp); rep("h3  256x256x32 x2 + planes out", ms, true);
+    ms = run_h3<256, 2, EPI_PROBE>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2, no epilogue", ms, false);
     CK(hipFree(Yp)); CK(hipFree(g_aplanes));
     CK(hipFree(g_planes));
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(bias)); CK(hipFree(Y)); CK(hipFree(Yr)); CK(hipFree(Sr));

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
     for (int u = 0; u < NSUB; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[u][r]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    tmax = max_xor32(tmax);
     const float m_new = fmaxf(m_run, tmax);
     const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2e);
     m_run = m_new;
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
     cur ^= 1;
   }
 
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = sum_xor32(l_run);
   const float inv = 1.f / l_tot;
   const int q = q_blk + wave * 32 + l32;
   if (q < Nq) {
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
 //  * Tree reductions for the tile max / sum; per-lane LDS offsets hoisted out of the loop.
 //  * The context is written straight into the plane image that ffn.0 consumes (common.h).
 // DIAG (tools/kbench_attn.hip only, never instantiated by the library): 1 = no softmax VALU,
-// 2 = no MFMAs -- to split the loop's time between the two pipes.
+// 2 = no MFMAs, 3 = MFMAs alone (no LDS, staging or barriers) -- to split the loop's time.
 // ----------------------------------------------------------------------------------------
 __device__ __forceinline__ f16x4 tr_read_h(const _Float16* p) {
   const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void attention_h3_kernel(AttnSet s
 #pragma unroll
       for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[s][0][e]), fabsf(x[s][1][e])));
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_xor32(mx);
     int ex = 0;
     if (mx > 0.f && mx <= 3.0e38f) {
       int E;
@@ -362,28 +362,66 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void attention_h3_kernel(AttnSet s
   int cur = 0;
   for (int t = 0; t < ntiles; ++t) {
     const int t0 = t * KT;
-    if (t + 1 < ntiles) gload(t0 + KT);
     const _Float16* Kc = Ks + cur * 2 * KPL + koff;
     const _Float16* Vc = Vs + cur * 2 * VPL;
 
-    // ---- S^T = K Q^T (x 2^(11+e))
+    // ---- S^T = K Q^T (x 2^(11+e)).  All K fragments of the tile are read up front (64 VGPRs),
+    // so the MFMAs wait on the first read only instead of one LDS round trip per k-step.
+    f16x8 kf[NSUB][4][2];
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int off = u * 32 * KLD + 16 * s;
+        if constexpr (DIAG == 3) {
+          kf[u][s][0] = qh[s];
+          kf[u][s][0][u] = (_Float16)(float)t;  // keep the MFMAs inside the loop
+          kf[u][s][1] = ql[s];
+        } else {
+          kf[u][s][0] = *reinterpret_cast<const f16x8*>(Kc + off);
+          kf[u][s][1] = *reinterpret_cast<const f16x8*>(Kc + KPL + off);
+        }
+      }
+    asm volatile("" ::: "memory");
+    if (DIAG != 3 && t + 1 < ntiles) gload(t0 + KT);
     f32x16 sc[NSUB];
 #pragma unroll
     for (int u = 0; u < NSUB; ++u) {
       sc[u] = f32x16{0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int off = u * 32 * KLD + 16 * s;
-        const f16x8 k0 = *reinterpret_cast<const f16x8*>(Kc + off);
-        const f16x8 k1 = *reinterpret_cast<const f16x8*>(Kc + KPL + off);
         if constexpr (DIAG == 2) {
-          sc[u][s] += (float)k0[0] + (float)k1[1];
+          sc[u][s] += (float)kf[u][s][0][0] + (float)kf[u][s][1][1];
         } else {
-          sc[u] = mfma_h3(k0, k1, qhs[s], ql[s], qh[s], sc[u]);
+          sc[u] = mfma_h3(kf[u][s][0], kf[u][s][1], qhs[s], ql[s], qh[s], sc[u]);
         }
       }
     }
-    if constexpr (DIAG != 1) {
+    // ---- V^T fragments of the tile (transposed reads), issued before the softmax so their
+    // latency hides behind it: key rows ka + tq (+8), ka = u*32 + 16s + 4*half
+    f16x8 vf[NSUB][2][2][2];  // [u][s][dim tile][plane]
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int vr = (u * 32 + 16 * s) * kHeadDim;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          if constexpr (DIAG == 3) {
+            vf[u][s][0][p] = qhs[s];
+            vf[u][s][1][p] = ql[s + 2 * p];
+            continue;
+          }
+          const f16x4 a0 = tr_read_h(Vc + p * VPL + vr + voff0);
+          const f16x4 a1 = tr_read_h(Vc + p * VPL + vr + 8 * kHeadDim + voff0);
+          const f16x4 b0 = tr_read_h(Vc + p * VPL + vr + voff1);
+          const f16x4 b1 = tr_read_h(Vc + p * VPL + vr + 8 * kHeadDim + voff1);
+          vf[u][s][0][p] = f16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          vf[u][s][1][p] = f16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        }
+      }
+    asm volatile("" ::: "memory");
+    if constexpr (DIAG != 1 && DIAG != 3) {
       if (t0 + KT > Nk) {  // mask keys past the end (last tile only)
 #pragma unroll
         for (int u = 0; u < NSUB; ++u)
@@ -404,7 +442,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void attention_h3_kernel(AttnSet s
       for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
         for (int r = 0; r < w; ++r) mr[r] = fmaxf(mr[r], mr[r + w]);
-      const float tmax = fmaxf(mr[0], __shfl_xor(mr[0], 32, 64));
+      const float tmax = max_xor32(mr[0]);
       const bool need = (tmax - m_use) * c_lane > 3.f;
       if (__ballot(need) != 0ull) {
         const float m_new = need ? tmax : m_use;
@@ -435,7 +473,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void attention_h3_kernel(AttnSet s
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         f16x8 ph, phs, pl;
-        if constexpr (DIAG == 1) {
+        if constexpr (DIAG == 1 || DIAG == 3) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) ph[j] = phs[j] = pl[j] = (_Float16)sc[u][8 * s + j];
         } else {
@@ -450,17 +488,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void attention_h3_kernel(AttnSet s
           }
         }
         // keys of element j: ka + j (j < 4), ka + 8 + (j - 4) (j >= 4), ka = u*32 + 16s + 4*half
-        const int vr = (u * 32 + 16 * s) * kHeadDim;
-        f16x8 v[2][2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const f16x4 a0 = tr_read_h(Vc + p * VPL + vr + voff0);
-          const f16x4 a1 = tr_read_h(Vc + p * VPL + vr + 8 * kHeadDim + voff0);
-          const f16x4 b0 = tr_read_h(Vc + p * VPL + vr + voff1);
-          const f16x4 b1 = tr_read_h(Vc + p * VPL + vr + 8 * kHeadDim + voff1);
-          v[0][p] = f16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-          v[1][p] = f16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-        }
+        const auto& v = vf[u][s];
         if constexpr (DIAG == 2) {
           o0[s] += (float)v[0][0][1] + (float)v[0][1][2] + (float)ph[3] + (float)pl[4] + (float)phs[5];
           o1[s] += (float)v[1][0][1] + (float)v[1][1][2];
@@ -470,12 +498,14 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void attention_h3_kernel(AttnSet s
         }
       }
 
-    if (t + 1 < ntiles) sstore(cur ^ 1);
-    __syncthreads();
+    if constexpr (DIAG != 3) {
+      if (t + 1 < ntiles) sstore(cur ^ 1);
+      __syncthreads();
+    }
     cur ^= 1;
   }
 
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = sum_xor32(l_run);
   const float inv = ldexpf(1.f / l_tot, -11);  // 2^-11 exact: same rounding as (o 2^-11) / l
   const int q = q_blk + wave * 32 + l32;
   if (q < Nq) {
@@ -513,6 +543,7 @@ static hipError_t attention_h3_launch(const AttnSet& s0, const AttnSet& s1, int 
                      nqb, scale * 1.4426950408889634f);
   return hipGetLastError();
 }
+
 
 template <int WAVES, int KT>
 static hipError_t attention_x6_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {

@@ -27,6 +27,17 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// op(v, v of lane ^ 32) for a commutative op, through v_permlane32_swap (no LDS round trip:
+// a ds_bpermute would queue behind the other waves' LDS reads).  Both halves get bitwise the
+// same result (same operands, same order).
+__device__ __forceinline__ float max_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -111,6 +122,20 @@ __device__ __forceinline__ int plane_swz(int row) { return (row >> 2) & 3; }
 // element offset of (row, k) inside one plane of an image with `rows_pad` rows
 __device__ __forceinline__ size_t plane_off(int row, int k, int rows_pad) {
   return ((size_t)(k >> 5) * rows_pad + row) * kKB + ((((k >> 3) & 3) ^ plane_swz(row)) << 3) + (k & 7);
+}
+
+// ---- LDS-DMA ------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) char lds_char;
+// one global_load_lds_dwordx4: lane i copies the 16 bytes at base + voff (base wave-uniform,
+// in SGPRs; voff per lane) to LDS byte address lds + 16 i (lds wave-uniform).  Inline asm: the
+// compiler neither counts it nor orders LDS reads behind it -- callers wait for it with an
+// explicit vmcnt + barrier.
+__device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(base), "s"(lds)
+               : "memory");
 }
 
 __device__ __forceinline__ float log_sigmoid(float x) {

@@ -34,24 +34,10 @@ namespace lg {
 namespace {
 constexpr int TB = 256;  // column tile; rows_pad granule
 
-typedef __attribute__((address_space(3))) char lds_char;
-
 __device__ __forceinline__ int xcd_remap_h3(int id, int n) {
   const int xcd = id & 7, local = id >> 3;
   const int base = n >> 3, extra = n & 7;
   return xcd * base + (xcd < extra ? xcd : extra) + local;
-}
-
-// one global_load_lds_dwordx4: lane i copies the 16 bytes at base + voff (base wave-uniform,
-// in SGPRs; voff per lane) to LDS byte address lds + 16 i (lds wave-uniform).  Inline asm: the
-// compiler neither counts it nor orders LDS reads behind it -- the k-loop waits for it with an
-// explicit vmcnt + barrier.
-__device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(base), "s"(lds)
-               : "memory");
 }
 
 __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, int& base, int& stride) {

@@ -5,9 +5,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
-#include "../cs566-project-lightglue_amd/csrc/attention.hip"
+#include "attn_experiments.hip"
 
 using namespace lg;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
@@ -38,6 +39,15 @@ __global__ void planes_h3(const float* x, _Float16* p, size_t n) {
   }
 }
 
+// plane image (K = 256) -> fp32 rows (h + l * 2^-11)
+__global__ void planes_to_rows(const _Float16* p, long long ps, int rows_pad, float* o, int rows) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= (size_t)rows * 256) return;
+  const int r = (int)(i / 256), c = (int)(i % 256);
+  const size_t off = plane_off(r, c, rows_pad);
+  o[i] = (float)p[off] + (float)p[ps + off] * (1.f / 2048.f);
+}
+
 // naive reference: one thread per (bh, query), double accumulation
 __global__ void ref_attn(const float* Q, const float* K, const float* V, float* O, int BH, int H, int N, float scale) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -62,11 +72,18 @@ __global__ void ref_attn(const float* Q, const float* K, const float* V, float* 
   for (int d = 0; d < 64; ++d) O[((size_t)b * N + q) * 256 + h * 64 + d] = (float)(o[d] / l);
 }
 
+static const char* g_only = nullptr;  // KB_ONLY=<substring>: run only the matching variants
+
 template <class F>
 void run(const char* name, F launch, int B, int H, const AttnSet& a0, const AttnSet& a1, float* Oref, float* O, size_t on) {
+  if (g_only && !strstr(name, g_only)) return;
   CK(hipMemset(O, 0, on * 4));
   CK(launch());
   CK(hipDeviceSynchronize());
+  if (a0.op) {
+    planes_to_rows<<<(on + 255) / 256, 256>>>(a0.op, a0.ops, a0.o_rows_pad, O, (int)(on / 256));
+    CK(hipDeviceSynchronize());
+  }
   std::vector<float> x(on), y(on);
   CK(hipMemcpy(x.data(), O, on * 4, hipMemcpyDeviceToHost));
   CK(hipMemcpy(y.data(), Oref, on * 4, hipMemcpyDeviceToHost));
@@ -88,6 +105,7 @@ void run(const char* name, F launch, int B, int H, const AttnSet& a0, const Attn
 
 int main(int argc, char** argv) {
   const int B = 32, H = 4, N = argc > 1 ? atoi(argv[1]) : 2048;
+  g_only = getenv("KB_ONLY");
   const size_t n = (size_t)B * H * N * 64;
   float *Q, *K, *V, *O, *Oref;
   void *KP, *VP, *KH, *VH;
@@ -107,14 +125,69 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   const long long ps = 2 * (long long)n;
   AttnSet x0{Q, KP, VP, ps, O, N, N}, x1{Q + n, (__bf16*)KP + n, (__bf16*)VP + n, ps, O + (size_t)B * N * 256, N, N};
-  AttnSet h0{Q, KH, VH, ps, O, N, N}, h1{Q + n, (_Float16*)KH + n, (_Float16*)VH + n, ps, O + (size_t)B * N * 256, N, N};
+  const int rp = (2 * B * N + 255) / 256 * 256;
+  _Float16* OP;
+  CK(hipMalloc(&OP, (size_t)2 * rp * 256 * 2));
+  AttnSet h0{Q, KH, VH, ps, O, N, N, OP, (long long)rp * 256, rp, 0};
+  AttnSet h1{Q + n, (_Float16*)KH + n, (_Float16*)VH + n, ps, O + (size_t)B * N * 256, N, N, OP, (long long)rp * 256, rp, B * N};
   const size_t on = (size_t)B * N * 256;  // compare set 0
   run("x6   w8 kt64", [&] { return attention_x6_launch<8, 64>(x0, x1, B, H, scale, 0); }, B, H, x0, x1, Oref, O, on);
-  run("h3   w8 kt64", [&] { return attention_h3_launch<8, 64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
-  run("h3v2 w8 kt64 occ2", [&] { return attention_h3v2_launch<8, 64, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
-  run("h3v2 DIAG1 no softmax", [&] { return attention_h3v2_launch<8, 64, 2, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
-  run("h3v2 DIAG1 occ4", [&] { return attention_h3v2_launch<8, 64, 4, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
-  run("h3v2 DIAG1 w4 occ4", [&] { return attention_h3v2_launch<4, 64, 4, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
-  run("h3v2 DIAG1 w8 kt32 occ4", [&] { return attention_h3v2_launch<8, 32, 4, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3 w8 kt64 occ2", [&] { return attention_h3_launch<8, 64, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3 DIAG1 no softmax", [&] { return attention_h3_launch<8, 64, 2, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3 DIAG2 no mfma", [&] { return attention_h3_launch<8, 64, 2, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3 DIAG3 mfma only", [&] { return attention_h3_launch<8, 64, 2, 3>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3 DIAG3 occ4", [&] { return attention_h3_launch<8, 64, 4, 3>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3pp kt64 (ping-pong)", [&] { return attention_h3pp_launch<64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3pp prio on M phase", [&] { return attention_h3pp_launch<64, 1, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3pp no prio", [&] { return attention_h3pp_launch<64, 1, 0>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3pp lag0 (lock-step)", [&] { return attention_h3pp_launch<64, 0, 0>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3pp no reads/copies/barriers", [&] { return attention_h3pp_launch<64, 1, 1, 64 + 8 + 4>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3pp no softmax", [&] { return attention_h3pp_launch<64, 1, 1, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3pp no mfma", [&] { return attention_h3pp_launch<64, 1, 1, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3pp no LDS reads/copies", [&] { return attention_h3pp_launch<64, 1, 1, 12>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  if (!g_only) {  // per-phase timelines (s_memtime) of waves 0 (group 0) and 4 (group 1) of workgroup 0
+    std::vector<unsigned long long> ts(8 * 4096);
+    auto show = [&](const char* name, auto launch) {
+      CK(hipMemset(O, 0, 8 * 4096 * 8));
+      CK(launch());
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(ts.data(), O, ts.size() * 8, hipMemcpyDeviceToHost));
+      const int nt = N / 64;
+      printf("%s\n", name);
+      for (int g = 0; g < 8; ++g) {
+        double m = 0, bm = 0, v = 0, bv = 0;
+        int cnt = 0;
+        for (int j = 2; j < nt - 2 && 4 * j + 4 < 160; ++j, ++cnt) {
+          const unsigned long long* t = &ts[g * 4096 + 4 * j];
+          m += (double)(t[1] - t[0]); bm += (double)(t[2] - t[1]); v += (double)(t[3] - t[2]); bv += (double)(t[4] - t[3]);
+        }
+        printf("  wave %d (ticks, mean of %d tiles): M %.0f  M-wait %.0f  V %.0f  V-wait %.0f\n", g, cnt, m / cnt, bm / cnt,
+               v / cnt, bv / cnt);
+      }
+    };
+    AttnSet t0 = h0;
+    t0.o = O;
+    show("stamps: full", [&] { return attention_h3pp_launch<64, 1, 1, 16>(t0, h1, B, H, scale, 0); });
+    {  // raw timeline of tile 10: each wave's stamps relative to wave 0's first stamp of the tile
+      const int j = 10;
+      const unsigned long long base = ts[0 * 4096 + 4 * j];
+      for (int w = 0; w < 8; ++w) {
+        printf("  raw w%d:", w);
+        for (int k = 0; k < 9; ++k) printf(" %7lld", (long long)(ts[w * 4096 + 4 * j + k] - base));
+        printf("\n");
+      }
+    }
+    show("stamps: no copies", [&] { return attention_h3pp_launch<64, 1, 1, 16 + 8>(t0, h1, B, H, scale, 0); });
+    show("stamps: no LDS reads", [&] { return attention_h3pp_launch<64, 1, 1, 16 + 4>(t0, h1, B, H, scale, 0); });
+    show("stamps: no reads/copies", [&] { return attention_h3pp_launch<64, 1, 1, 16 + 8 + 4>(t0, h1, B, H, scale, 0); });
+    show("stamps: MFMA only", [&] { return attention_h3pp_launch<64, 1, 1, 16 + 32 + 8 + 4>(t0, h1, B, H, scale, 0); });
+    show("stamps: no reads/copies, empty V", [&] { return attention_h3pp_launch<64, 1, 1, 16 + 32 + 8 + 4>(t0, h1, B, H, scale, 0); });
+    show("stamps: no reads/copies/barriers", [&] { return attention_h3pp_launch<64, 1, 1, 64 + 16 + 8 + 4>(t0, h1, B, H, scale, 0); });
+    show("stamps: no reads/copies, lock-step", [&] { return attention_h3pp_launch<64, 0, 1, 16 + 8 + 4>(t0, h1, B, H, scale, 0); });
+    show("stamps: full, empty V", [&] { return attention_h3pp_launch<64, 1, 1, 16 + 32>(t0, h1, B, H, scale, 0); });
+  }
+  run("h3p w8 kt64 occ2", [&] { return attention_h3p_launch<8, 64, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3p w4 kt64 occ2", [&] { return attention_h3p_launch<4, 64, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3 w4 kt64 occ2", [&] { return attention_h3_launch<4, 64, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   return 0;
 }

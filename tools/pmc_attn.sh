@@ -1,10 +1,14 @@
 #!/bin/bash
-# VALU / MFMA / LDS instruction counters for the attention micro-benchmark.
+# LDS / issue counters for the attention kbench variants (one rocprofv3 pass per counter group).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp
-OUT=gpurun_out/pmc_attn; mkdir -p $OUT
-hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/kbench_attn.hip -o /tmp/ka 2>/dev/null || exit 1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/a -o run -- /tmp/ka > $OUT/a.log 2>&1 || { tail -5 $OUT/a.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --output-format csv -d $OUT/b -o run -- /tmp/ka > $OUT/b.log 2>&1 || { tail -5 $OUT/b.log; exit 1; }
+mkdir -p gpurun_out/pmc_attn
+cd /tmp && export TMPDIR=/tmp
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+export KB_ONLY="${KB_ONLY:-ping-pong}"
+i=0
+for ctr in "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVE_CYCLES" "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_attn/p$i" -- "$R/tools/kbench_attn" > "$R/gpurun_out/pmc_attn/p$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
+done
 echo done

@@ -71,6 +71,7 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
   constexpr int PPW = PIECES / NW;
   static_assert(PIECES % NW == 0, "pieces per wave");
   __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE_BYTES];
+  __shared__ int rowinfo[2 * BM];  // QKV epilogues: head-major base / stride per tile row
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -250,19 +251,21 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
   } else {
-    // Head-major scatter (see gemm.hip): the wave's 64 columns are one (type t, head) block and
-    // lane l32 holds dims 2*l32 (tile 0) and 2*l32+1 (tile 1) -- the rotary partners.
+    // Head-major scatter through the same LDS transpose as EPI_STORE.  The wave's 64 columns are
+    // one (type t, head) block; GEMM column c holds dim 2c (c < 32) or 2(c - 32) + 1 (c >= 32) (the
+    // load-time Wqkv row order puts rotary partners in one lane of the MFMA tile).  Written into
+    // LDS at their natural dim, each lane then owns 8 consecutive dims (4 rotary pairs) of one row:
+    // 16-byte bias / cos / sin loads and 16-byte q and plane stores.
     //   self  (EPI_QKV_ROT):   t0 -> q fp32 (rotary), t1 -> k planes (rotary), t2 -> v planes
     //   cross (EPI_CROSS_QKV): t0 -> qk fp32 * scale^0.5 and qk planes,        t1 -> v planes
-    int* rowinfo = reinterpret_cast<int*>(smem);  // the k-loop ended with a barrier
+    const HeadLayout& hl = g.hl;
     for (int r = tid; r < BM; r += BM * 4) {
       int base = 0, stride = 0;
-      if (m0 + r < g.R) head_row_base_h3(g.hl, m0 + r, base, stride);
+      if (m0 + r < g.R) head_row_base_h3(hl, m0 + r, base, stride);
       rowinfo[2 * r] = base;
       rowinfo[2 * r + 1] = stride;
     }
     __syncthreads();
-    const HeadLayout& hl = g.hl;
     const int cbase = n0 + wn0;
     const int t = cbase / kDim, head = (cbase % kDim) / kHeadDim;
     const bool rot = EPI == EPI_QKV_ROT && t < 2;
@@ -270,40 +273,68 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
     const bool to_kp = EPI == EPI_QKV_ROT ? t == 1 : t == 0;
     const bool to_vp = EPI == EPI_QKV_ROT ? t == 2 : t == 1;
     const float sc = (EPI == EPI_CROSS_QKV && t == 0) ? hl.qk_scale : 1.f;
-    const float be = g.bias[cbase + l32], bo = g.bias[cbase + 32 + l32];
+    float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
+    const int d0 = (lane & 7) * 8;  // the lane's first dim
+    float bd[8];                    // bias in dim order: dim d <- GEMM column (d & 1) * 32 + d / 2
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int e = 0; e < 8; ++e) bd[e] = g.bias[cbase + ((d0 + e) & 1) * 32 + ((d0 + e) >> 1)];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int lr = wm0 + i * 32 + row32(r, half);
-        const int row = m0 + lr;
-        if (row >= g.R) continue;
-        const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + 2 * l32;
-        float xe = fmaf(acc[i][0][r], g.acc_scale, be);  // dim 2*l32   (even)
-        float xo = fmaf(acc[i][1][r], g.acc_scale, bo);  // dim 2*l32+1 (odd)
-        if (rot) {
-          // t*cos + rotate_half(t)*sin, rotate_half(x)[2i] = -x[2i+1], [2i+1] = x[2i]
-          const float c = hl.cosb[(size_t)row * kFreq + l32];
-          const float s = hl.sinb[(size_t)row * kFreq + l32];
-          const float e2 = add_rn(mul_rn(xe, c), mul_rn(-xo, s));
-          const float o2 = add_rn(mul_rn(xo, c), mul_rn(xe, s));
-          xe = e2;
-          xo = o2;
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = row32(r, half), dim = 2 * l32 + j;
+          ep[rr * 64 + (dim ^ ((rr & 1) << 2))] = acc[i][j][r];
         }
-        xe *= sc;
-        xo *= sc;
-        if (to_q) *reinterpret_cast<float2*>(hl.q + off) = make_float2(xe, xo);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int rr = (lane >> 3) + 8 * k;
+        const int lr = wm0 + i * 32 + rr;
+        const int row = m0 + lr;
+        const int sw = (rr & 1) << 2;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (d0 ^ sw));
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((d0 + 4) ^ sw));
+        if (row >= g.R) continue;
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = fmaf(e < 4 ? v0[e] : v1[e - 4], g.acc_scale, bd[e]);
+        if (rot) {
+          // t*cos + rotate_half(t)*sin, rotate_half(x)[2p] = -x[2p+1], [2p+1] = x[2p]; freq p = dim / 2
+          const f32x4 c4 = *reinterpret_cast<const f32x4*>(hl.cosb + (size_t)row * kFreq + d0 / 2);
+          const f32x4 s4 = *reinterpret_cast<const f32x4*>(hl.sinb + (size_t)row * kFreq + d0 / 2);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const float xe = x[2 * p], xo = x[2 * p + 1];
+            x[2 * p] = add_rn(mul_rn(xe, c4[p]), mul_rn(-xo, s4[p]));
+            x[2 * p + 1] = add_rn(mul_rn(xo, c4[p]), mul_rn(xe, s4[p]));
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] *= sc;
+        const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + d0;
+        if (to_q) {
+          *reinterpret_cast<f32x4*>(hl.q + off) = f32x4{x[0], x[1], x[2], x[3]};
+          *reinterpret_cast<f32x4*>(hl.q + off + 4) = f32x4{x[4], x[5], x[6], x[7]};
+        }
         if (to_kp || to_vp) {
           _Float16* base = static_cast<_Float16*>(to_kp ? hl.kp : hl.vp);
-          bad |= !(fabsf(xe) <= kF16Max) || !(fabsf(xo) <= kF16Max);
-          _Float16 eh, el, oh, ol;
-          split2h(xe, eh, el);
-          split2h(xo, oh, ol);
-          typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-          *reinterpret_cast<f16x2*>(base + off) = f16x2{eh, oh};
-          *reinterpret_cast<f16x2*>(base + hl.pstride + off) = f16x2{el, ol};
+          f16x8 h, l;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            bad |= !(fabsf(x[e]) <= kF16Max);
+            _Float16 a, c;
+            split2h(x[e], a, c);
+            h[e] = a;
+            l[e] = c;
+          }
+          *reinterpret_cast<f16x8*>(base + off) = h;
+          *reinterpret_cast<f16x8*>(base + hl.pstride + off) = l;
         }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
+    }
   }
   if (g.ovf && __ballot(bad) != 0ull && lane == 0) atomicOr(g.ovf, 1);
 }

@@ -59,10 +59,12 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int EPI, int BM, int NSTAGE>
-__global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
-  constexpr int BN = TB;                     // column tile
-  constexpr int NW = BM / 16;                // waves: (BM/64) x 4 of 64 x 64
+// BN x BM tile of (BM/64) x (BN/WN) waves, each 64 x WN (2 x WN/32 MFMA tiles of 32 x 32).
+template <int EPI, int BM, int NSTAGE, int BN = TB, int WN = 64>
+__global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(GemmH3Args g) {
+  constexpr int WGN = BN / WN;               // waves along N
+  constexpr int NW = (BM / 64) * WGN;
+  constexpr int NJ = WN / 32;                // 32-column MFMA tiles per wave
   constexpr int BK = kKB;                    // k-tile = one k-block of the plane images (32)
   constexpr int APT = BM * BK * 2;           // one A plane tile (bytes)
   constexpr int WPT = BN * BK * 2;           // one W plane tile
@@ -71,13 +73,14 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
   constexpr int PPW = PIECES / NW;
   static_assert(PIECES % NW == 0, "pieces per wave");
   __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE_BYTES];
-  __shared__ int rowinfo[2 * BM];  // QKV epilogues: head-major base / stride per tile row
+  constexpr bool kQkv = EPI == EPI_QKV_ROT || EPI == EPI_CROSS_QKV;
+  __shared__ int rowinfo[kQkv ? 2 * BM : 1];  // QKV epilogues: head-major base / stride per tile row
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, half = lane >> 5;
-  const int wm0 = (wave >> 2) * 64, wn0 = (wave & 3) * 64;
+  const int wm0 = (wave / WGN) * 64, wn0 = (wave % WGN) * WN;
 
   const int num_m = (g.R + BM - 1) / BM, num_n = g.Nout / BN;
   const int tile = xcd_remap_h3(blockIdx.x, num_m * num_n);
@@ -111,11 +114,11 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{0.f};
 
   // fragment (row r, 16-byte k-chunk c) of the plane tile at byte offset t0 of a stage
   auto frag = [&](const char* st, int t0, int r, int c) {
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       const int c = 2 * s + half;
-      f16x8 ah[2], al[2], wh[2], wl[2], whs[2];
+      f16x8 ah[2], al[2], wh[NJ], wl[NJ], whs[NJ];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int r = wm0 + i * 32 + l32;
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
         al[i] = frag(st, APT, r, c);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int r = wn0 + j * 32 + l32;
         wh[j] = frag(st, 2 * APT, r, c);
         wl[j] = frag(st, 2 * APT + WPT, r, c);
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_h3(ah[i], al[i], whs[j], wl[j], wh[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_h3(ah[i], al[i], whs[j], wl[j], wh[j], acc[i][j]);
     }
   };
 
@@ -176,11 +179,111 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) t += acc[i][j][r];
     if (t == 1234.5678f) g.Y[tid] = t;
+  } else if constexpr (EPI == EPI_LN_GELU) {
+    // ffn.0 + ffn.1 LayerNorm(512, eps 1e-5) + ffn.2 GELU(erf) (lightglue.py:171-176), fused: the
+    // workgroup holds complete rows (BN = 512), so the row statistics are reduced in LDS (free
+    // after the k-loop) and the activations leave only as the plane image ffn.3 consumes.
+    static_assert(BN == 512 && WN == 128 && BM == 128, "LN epilogue tile");
+    constexpr int RS = WGN * 32 + 4;  // row stride of the partial-sum table (floats)
+    float* red = reinterpret_cast<float*>(smem);           // [BM][RS] per-lane partials
+    float* mean_s = red + BM * RS;                         // [BM]
+    float* rstd_s = mean_s + BM;                           // [BM]
+    float* ep = rstd_s + BM + wave * (32 * 64);            // per-wave transpose buffer
+    static_assert((BM * RS + 2 * BM + NW * 32 * 64) * 4 <= NSTAGE * STAGE_BYTES, "epilogue scratch");
+    float gj[NJ], bj[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + l32;
+      const float bias = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = fmaf(acc[i][j][r], g.acc_scale, bias);
+      gj[j] = g.ln_g[col];
+      bj[j] = g.ln_b[col];
+    }
+    // row sum of f(v) over the 512 columns: lane partials over its NJ columns -> table ->
+    // 4 threads per row (32 partials each) -> shuffle
+    auto row_total = [&](auto f, float* out) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lr = wm0 + i * 32 + row32(r, half);
+          float p = 0.f;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) p += f(acc[i][j][r], lr);
+          red[lr * RS + (wave % WGN) * 32 + l32] = p;
+        }
+      __syncthreads();
+      const int row = tid >> 2, part = tid & 3;
+      const f32x4* src = reinterpret_cast<const f32x4*>(red + row * RS + part * 32);
+      float s4 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const f32x4 v = src[q];
+        s4 += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+      s4 += __shfl_xor(s4, 1, 64);
+      s4 += __shfl_xor(s4, 2, 64);
+      if (part == 0) out[row] = s4;
+      __syncthreads();
+    };
+    row_total([](float v, int) { return v; }, mean_s);
+    if (tid < BM) mean_s[tid] *= (1.f / 512.f);
+    __syncthreads();
+    row_total([&](float v, int lr) { const float d = v - mean_s[lr]; return d * d; }, rstd_s);
+    if (tid < BM) rstd_s[tid] = 1.f / sqrtf(rstd_s[tid] * (1.f / 512.f) + 1e-5f);
+    __syncthreads();
+    // normalise + GELU, then 16-byte plane-image stores through the per-wave transpose buffer
+    const int cq = (lane & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jh = 0; jh < NJ / 2; ++jh) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int j = 2 * jh + jj;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rr = row32(r, half), lr = wm0 + i * 32 + rr;
+            const float y = (acc[i][j][r] - mean_s[lr]) * rstd_s[lr] * gj[j] + bj[j];
+            const int c = jj * 32 + l32;
+            ep[rr * 64 + (c ^ ((rr & 1) << 2))] = 0.5f * y * (1.f + erff(y * 0.70710678118654752f));
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int rr = (lane >> 3) + 8 * k;
+          const int row = m0 + wm0 + i * 32 + rr;
+          const int sw = (rr & 1) << 2;
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
+          const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
+          if (row < g.R) {
+            f16x8 h, l;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float v = e < 4 ? v0[e] : v1[e - 4];
+              bad |= !(fabsf(v) <= kF16Max);
+              _Float16 a, c;
+              split2h(v, a, c);
+              h[e] = a;
+              l[e] = c;
+            }
+            const size_t off = plane_off(row, n0 + wn0 + jh * 64 + cq, g.yrows_pad);
+            *reinterpret_cast<f16x8*>(g.Yp + off) = h;
+            *reinterpret_cast<f16x8*>(g.Yp + g.yps + off) = l;
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
+      }
   } else if constexpr (EPI == EPI_STORE) {
+    static_assert(WN == 64, "EPI_STORE tile");
     // Transposed through LDS (free after the k-loop; 8 KiB per wave per 32-row pass) so that every
     // lane owns 8 consecutive columns of a row: fp32 stores, residual loads and plane-image
     // stores are then 16 bytes per lane.  LDS element (r, c) of a pass at r*64 + (c ^ 4*(r&1))
@@ -251,6 +354,7 @@ __global__ __launch_bounds__(BM * 4) void gemm_h3_kernel(GemmH3Args g) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
   } else {
+    static_assert(WN == 64, "QKV epilogue tile");
     // Head-major scatter through the same LDS transpose as EPI_STORE.  The wave's 64 columns are
     // one (type t, head) block; GEMM column c holds dim 2c (c < 32) or 2(c - 32) + 1 (c >= 32) (the
     // load-time Wqkv row order puts rotary partners in one lane of the MFMA tile).  Written into
@@ -353,6 +457,13 @@ hipError_t gemm_h3_launch(const GemmH3Args& a, int epi, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ffn.0 + LayerNorm + GELU (EPI_LN_GELU): 128 x 512 tiles, 8 waves of 64 x 128, two 80 KiB stages
+hipError_t gemm_h3_ln_launch(const GemmH3Args& a, hipStream_t st) {
+  const dim3 grid((a.R + 127) / 128), block(512);
+  hipLaunchKernelGGL((gemm_h3_kernel<EPI_LN_GELU, 128, 2, 512, 128>), grid, block, 0, st, a);
+  return hipGetLastError();
+}
+
 #ifndef LG_GEMM_H3_TILE
 // BM (rows per workgroup; 4*BM threads), LDS stages -- tools/kbench_gemm.hip
 #define LG_GEMM_H3_TILE 256, 2
@@ -364,6 +475,10 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
       !a.W.p || a.A0.rows_pad < ((a.R + TB - 1) / TB) * TB || (a.K0 < a.K && a.A1.rows_pad < ((a.R + TB - 1) / TB) * TB) ||
       a.W.rows_pad != a.Nout || (a.Yp && a.yrows_pad < a.R))
     return hipErrorInvalidValue;
+  if (epi == EPI_LN_GELU) {
+    if (a.Nout != 512 || !a.Yp || !a.ln_g || !a.ln_b || a.yrows_pad < a.R) return hipErrorInvalidValue;
+    return gemm_h3_ln_launch(a, st);
+  }
   return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
 }
 

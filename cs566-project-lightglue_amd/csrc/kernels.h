@@ -5,7 +5,13 @@
 
 namespace lg {
 
-enum EpiKind { EPI_STORE = 0, EPI_QKV_ROT = 1, EPI_CROSS_QKV = 2, EPI_PROBE = 3 /* benchmarking only */ };
+enum EpiKind {
+  EPI_STORE = 0,
+  EPI_QKV_ROT = 1,
+  EPI_CROSS_QKV = 2,
+  EPI_PROBE = 3,    // benchmarking only
+  EPI_LN_GELU = 4,  // gemm_h3 only: Yp = plane image of GELU(LayerNorm(acc + bias)), Nout = 512
+};
 
 // Operand formats of the fp32-accurate matrix-core arithmetic (common.h):
 //   PREC_H3  fp16x3 -- 3 fp16 MFMAs per product; runtime operands must satisfy |x| <= 65504
@@ -75,6 +81,8 @@ struct GemmH3Args {
   long long yps;
   int yrows_pad;
   int* ovf;           // set to 1 when a value written into Yp / K, V planes leaves the fp16 range
+  const float* ln_g;  // EPI_LN_GELU: LayerNorm weight / bias [Nout]
+  const float* ln_b;
   HeadLayout hl;      // EPI_QKV_ROT / EPI_CROSS_QKV
 };
 hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st);

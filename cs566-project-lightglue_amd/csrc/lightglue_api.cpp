@@ -697,12 +697,13 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
           g.R = R; g.Nout = D; g.Yp = w.Mp; g.yps = (long long)RP * D; g.yrows_pad = RP;
           LG_HIP(gemmh(g, EPI_STORE));
         }
-        // FFN: Linear(cat[x, msg]) -> LN -> GELU -> Linear + residual (x also as plane image)
+        // FFN: Linear(cat[x, msg]) -> LN -> GELU (one kernel: the activations leave only as the
+        // plane image ffn.3 consumes) -> Linear + residual (x also as plane image)
         GemmH3Args g = gemm_h3_base();
         g.A0 = image(w.Xp, D); g.K0 = D; g.A1 = image(h->fold ? w.Cp : w.Mp, D); g.K = 2 * D;
-        wplanes(g, bw.W1); g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
-        LG_HIP(gemmh(g, EPI_STORE));
-        LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, w.Hp, RP, w.ovf, st));
+        wplanes(g, bw.W1); g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D;
+        g.Yp = w.Hp; g.yps = (long long)RP * 2 * D; g.yrows_pad = RP; g.ln_g = Wb + bw.g; g.ln_b = Wb + bw.be;
+        LG_HIP(gemmh(g, EPI_LN_GELU));
         g = gemm_h3_base();
         g.A0 = image(w.Hp, 2 * D); g.K0 = 2 * D; g.K = 2 * D; wplanes(g, bw.W2); g.bias = Wb + bw.b2;
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;

@@ -30,6 +30,8 @@ EXPORTED_SYMBOLS = [
     "lg_log_optimal_transport",
     "lg_profile_enable",
     "lg_profile_read",
+    "lg_attention_workspace_bytes",
+    "lg_attention",
 ]
 KERNEL_IDS = {"attention": 0, "gemm": 1, "assign": 2}
 # lg_config_t.precision (include/lightglue_mi355x.h): "auto" = fp16x3 with a guarded bf16x6 rerun
@@ -128,6 +130,11 @@ def load():
         "lg_sinkhorn_workspace_bytes": (ctypes.c_int, [i32, i32, i32, ctypes.POINTER(sz)]),
         "lg_log_optimal_transport": (ctypes.c_int, [_P, ctypes.c_float, i32, i32, i32, i32, _P, _P, sz, _P]),
         "lg_profile_enable": (ctypes.c_int, [_P, ctypes.c_int]),
+        "lg_attention_workspace_bytes": (ctypes.c_int, [i32, i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_attention": (
+            ctypes.c_int,
+            [_P, _P, _P, i32, i32, i32, i32, ctypes.c_float, i32, _P, _P, sz, _P],
+        ),
         "lg_profile_read": (
             ctypes.c_int,
             [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),

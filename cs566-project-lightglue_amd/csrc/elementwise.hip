@@ -411,4 +411,51 @@ hipError_t remap_matches(const int64_t* m0c, const int64_t* m1c, const float* s0
   return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------------------
+// Kernel-check helpers (lg_attention): fp32 -> operand planes, plane image -> fp32 rows.
+// ----------------------------------------------------------------------------------------
+__global__ void split_planes_kernel(const float* x, size_t n, void* planes, int prec, int* ovf) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (i < n) {
+    const float v = x[i];
+    if (prec == PREC_H3) {
+      _Float16 h, l;
+      split2h(v, h, l);
+      bad = !(fabsf(v) <= kF16Max);
+      static_cast<_Float16*>(planes)[i] = h;
+      static_cast<_Float16*>(planes)[n + i] = l;
+    } else {
+      __bf16 h, m, l;
+      split3(v, h, m, l);
+      static_cast<__bf16*>(planes)[i] = h;
+      static_cast<__bf16*>(planes)[n + i] = m;
+      static_cast<__bf16*>(planes)[2 * n + i] = l;
+    }
+  }
+  if (ovf && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+}
+
+hipError_t split_planes(const float* x, size_t n, void* planes, int prec, int* ovf, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, planes, prec, ovf);
+  return hipGetLastError();
+}
+
+__global__ void image_to_rows_kernel(const _Float16* p, long long ps, int rows_pad, int K, float* out, int rows) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)rows * K) return;
+  const int r = (int)(i / K), c = (int)(i % K);
+  const size_t off = plane_off(r, c, rows_pad);
+  out[i] = (float)p[off] + (float)p[ps + off] * (1.f / kLoScale);
+}
+
+hipError_t image_to_rows(const _Float16* planes, long long ps, int rows_pad, int K, float* out, int rows, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  const size_t n = (size_t)rows * K;
+  hipLaunchKernelGGL(image_to_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, planes, ps, rows_pad, K,
+                     out, rows);
+  return hipGetLastError();
+}
+
 }  // namespace lg

@@ -156,6 +156,11 @@ hipError_t fold_out_proj(float* W1, float* b1, const float* Wo, const float* bo,
 hipError_t absmax(const float* src, size_t n, float* out, hipStream_t st);
 hipError_t split_weight_h3(const float* src, int rows, int K, float scale, _Float16* planes, hipStream_t st);
 
+// lg_attention (kernel-level checks): fp32 [n] -> operand planes of `prec` (plane stride n; fp16
+// range guard into ovf for PREC_H3), and a plane image (K columns) -> fp32 rows.
+hipError_t split_planes(const float* x, size_t n, void* planes, int prec, int* ovf, hipStream_t st);
+hipError_t image_to_rows(const _Float16* planes, long long ps, int rows_pad, int K, float* out, int rows, hipStream_t st);
+
 // Weight repacking: dst[r,:] = src[idx[r],:] (row length `cols`).
 hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st);
 

@@ -904,4 +904,59 @@ int lg_log_optimal_transport(const float* scores, float alpha, int32_t B, int32_
   return LG_OK;
 }
 
+namespace {
+size_t attention_ws(int B, int H, int Nq, int Nk, size_t& kv_off, size_t& img_off, int& rp) {
+  const size_t n = (size_t)B * H * Nk * 64;
+  rp = (int)(((size_t)B * Nq + 255) / 256 * 256);
+  kv_off = 256;                              // [ovf flag | k planes (3 max) | v planes | ctx image]
+  img_off = kv_off + 2 * 3 * n * 2;
+  return img_off + (size_t)2 * rp * 256 * 2;
+}
+}  // namespace
+
+int lg_attention_workspace_bytes(int32_t B, int32_t H, int32_t Nq, int32_t Nk, size_t* bytes) {
+  if (!bytes || B < 0 || H <= 0 || Nq < 0 || Nk < 0) return fail(LG_E_INVALID, "bad argument");
+  size_t kv, img;
+  int rp;
+  *bytes = attention_ws(B, H, Nq, Nk, kv, img, rp);
+  return LG_OK;
+}
+
+int lg_attention(const float* q, const float* k, const float* v, int32_t B, int32_t H, int32_t Nq, int32_t Nk,
+                 float scale, int32_t precision, float* ctx, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!q || !k || !v || !ctx) return fail(LG_E_INVALID, "null argument");
+  if (H * 64 != 256 || B < 0 || Nq < 0 || Nk <= 0) return fail(LG_E_INVALID, "bad shape (H * 64 must be 256, Nk > 0)");
+  size_t kv_off, img_off;
+  int rp;
+  const size_t need = attention_ws(B, H, Nq, Nk, kv_off, img_off, rp);
+  if (!workspace || workspace_bytes < need) return fail(LG_E_WORKSPACE, "workspace too small");
+  if (B == 0 || Nq == 0) return LG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = static_cast<char*>(workspace);
+  int* ovf = reinterpret_cast<int*>(ws);
+  const size_t n = (size_t)B * H * Nk * 64;
+  const int prec = precision == LG_PREC_X6 ? lg::PREC_X6 : lg::PREC_H3;
+  const int np = prec == lg::PREC_X6 ? 3 : 2;
+  void* kp = ws + kv_off;
+  void* vp = ws + kv_off + np * n * 2;
+  _Float16* img = reinterpret_cast<_Float16*>(ws + img_off);
+  LG_HIP(hipMemsetAsync(ovf, 0, sizeof(int), st));
+  LG_HIP(lg::split_planes(k, n, kp, prec, ovf, st));
+  LG_HIP(lg::split_planes(v, n, vp, prec, ovf, st));
+  if (prec == lg::PREC_H3) {
+    int flag = 0;
+    LG_HIP(hipMemcpyAsync(&flag, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+    LG_HIP(hipStreamSynchronize(st));
+    if (flag) return fail(LG_E_INVALID, "k or v outside the fp16 range (use LG_PREC_X6)");
+  }
+  // one set; the second set is empty (Nq = 0: its workgroups exit at once)
+  const lg::AttnSet s0{q, kp, vp, (long long)n, ctx, Nq, Nk, img, (long long)rp * 256, rp, 0};
+  lg::AttnSet s1 = s0;
+  s1.Nq = 0;
+  LG_HIP(lg::attention_f32(s0, s1, B, H, scale, prec, st));
+  if (prec == lg::PREC_H3) LG_HIP(lg::image_to_rows(img, (long long)rp * 256, rp, 256, ctx, B * Nq, st));
+  LG_HIP(hipStreamSynchronize(st));
+  return LG_OK;
+}
+
 }  // extern "C"

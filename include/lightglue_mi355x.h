@@ -146,6 +146,17 @@ int lg_log_optimal_transport(const float* scores, float alpha, int32_t B, int32_
                              int32_t iters, float* Z, void* workspace, size_t workspace_bytes,
                              void* stream);
 
+/* Kernel-level entry (tests; the reference has no counterpart -- it is the SDPA call at
+ * lightglue.py:139-149 in isolation): one launch of the forward's attention kernel.
+ * q, k, v: fp32 head-major [B][H][Nq or Nk][64] device tensors, H * 64 == 256; ctx: fp32
+ * [B][Nq][256] (column h*64 + d), softmax(scale * q k^T) v.  precision LG_PREC_AUTO runs the fp16x3
+ * kernel (k and v must lie in the fp16 range, else LG_E_INVALID), LG_PREC_X6 the bf16x6 one.
+ * Synchronises the stream (reads the range flag).  Workspace: lg_attention_workspace_bytes. */
+int lg_attention_workspace_bytes(int32_t B, int32_t H, int32_t Nq, int32_t Nk, size_t* bytes);
+int lg_attention(const float* q, const float* k, const float* v, int32_t B, int32_t H, int32_t Nq,
+                 int32_t Nk, float scale, int32_t precision, float* ctx, void* workspace,
+                 size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

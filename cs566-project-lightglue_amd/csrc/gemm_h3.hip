@@ -187,13 +187,20 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     // ffn.0 + ffn.1 LayerNorm(512, eps 1e-5) + ffn.2 GELU(erf) (lightglue.py:171-176), fused: the
     // workgroup holds complete rows (BN = 512), so the row statistics are reduced in LDS (free
     // after the k-loop) and the activations leave only as the plane image ffn.3 consumes.
-    static_assert(BN == 512 && WN == 128 && BM == 128, "LN epilogue tile");
-    constexpr int RS = WGN * 32 + 4;  // row stride of the partial-sum table (floats)
+    static_assert(BN == 512 && BM == 128, "LN epilogue tile");
+    constexpr int NT = NW * 64;
+    constexpr int PARTS = NT / BM;            // threads per row in the table reduction
+    constexpr int RS = WGN * 32 + 4;          // row stride of the partial-sum table (floats)
+    constexpr int PW = WGN * 32 / PARTS;      // partials summed per thread
+    static_assert(PW % 4 == 0, "table reduction");
+    constexpr int SCRATCH = NSTAGE * STAGE_BYTES / 4;  // floats
+    // LDS (free after the k-loop): [partial table | ... | mean | rstd]; the per-wave transpose
+    // buffers of the final stage overlay the table once the statistics are done
     float* red = reinterpret_cast<float*>(smem);           // [BM][RS] per-lane partials
-    float* mean_s = red + BM * RS;                         // [BM]
+    float* mean_s = red + SCRATCH - 2 * BM;                // [BM]
     float* rstd_s = mean_s + BM;                           // [BM]
-    float* ep = rstd_s + BM + wave * (32 * 64);            // per-wave transpose buffer
-    static_assert((BM * RS + 2 * BM + NW * 32 * 64) * 4 <= NSTAGE * STAGE_BYTES, "epilogue scratch");
+    float* ep = red + wave * (32 * 64);                    // per-wave transpose buffer
+    static_assert(BM * RS + 2 * BM <= SCRATCH && NW * 32 * 64 + 2 * BM <= SCRATCH, "epilogue scratch");
     float gj[NJ], bj[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -220,16 +227,16 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
           red[lr * RS + (wave % WGN) * 32 + l32] = p;
         }
       __syncthreads();
-      const int row = tid >> 2, part = tid & 3;
-      const f32x4* src = reinterpret_cast<const f32x4*>(red + row * RS + part * 32);
+      const int row = tid / PARTS, part = tid % PARTS;
+      const f32x4* src = reinterpret_cast<const f32x4*>(red + row * RS + part * PW);
       float s4 = 0.f;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < PW / 4; ++q) {
         const f32x4 v = src[q];
         s4 += (v[0] + v[1]) + (v[2] + v[3]);
       }
-      s4 += __shfl_xor(s4, 1, 64);
-      s4 += __shfl_xor(s4, 2, 64);
+#pragma unroll
+      for (int o = 1; o < PARTS; o <<= 1) s4 += __shfl_xor(s4, o, 64);
       if (part == 0) out[row] = s4;
       __syncthreads();
     };
@@ -457,10 +464,14 @@ hipError_t gemm_h3_launch(const GemmH3Args& a, int epi, hipStream_t st) {
   return hipGetLastError();
 }
 
-// ffn.0 + LayerNorm + GELU (EPI_LN_GELU): 128 x 512 tiles, 8 waves of 64 x 128, two 80 KiB stages
+#ifndef LG_GEMM_LN_WN
+#define LG_GEMM_LN_WN 64  // wave tile width: 64 -> 16 waves of 64 x 64, 128 -> 8 waves of 64 x 128
+#endif
+// ffn.0 + LayerNorm + GELU (EPI_LN_GELU): 128 x 512 tiles, two 80 KiB stages
+template <int WN>
 hipError_t gemm_h3_ln_launch(const GemmH3Args& a, hipStream_t st) {
-  const dim3 grid((a.R + 127) / 128), block(512);
-  hipLaunchKernelGGL((gemm_h3_kernel<EPI_LN_GELU, 128, 2, 512, 128>), grid, block, 0, st, a);
+  const dim3 grid((a.R + 127) / 128), block(2 * (512 / WN) * 64);
+  hipLaunchKernelGGL((gemm_h3_kernel<EPI_LN_GELU, 128, 2, 512, WN>), grid, block, 0, st, a);
   return hipGetLastError();
 }
 
@@ -477,7 +488,7 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
     return hipErrorInvalidValue;
   if (epi == EPI_LN_GELU) {
     if (a.Nout != 512 || !a.Yp || !a.ln_g || !a.ln_b || a.yrows_pad < a.R) return hipErrorInvalidValue;
-    return gemm_h3_ln_launch(a, st);
+    return gemm_h3_ln_launch<LG_GEMM_LN_WN>(a, st);
   }
   return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
 }

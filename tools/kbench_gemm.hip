@@ -41,6 +41,27 @@ double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out,
   return ms / iters;
 }
 
+template <int WN>
+double run_ln(const Shape& s, float* bias, float* gam, float* bet, _Float16* Yp, int iters) {
+  GemmH3Args a;
+  memset(&a, 0, sizeof(a));
+  a.A0 = {g_aplanes, (long long)s.R * s.K, s.R}; a.K0 = s.K; a.K = s.K;
+  a.W = {g_planes, (long long)s.N * s.K, s.N}; a.R = s.R; a.Nout = s.N;
+  a.acc_scale = g_unscale; a.out_scale = 1.f; a.bias = bias; a.ln_g = gam; a.ln_b = bet;
+  a.Yp = Yp; a.yps = (long long)s.R * s.N; a.yrows_pad = s.R;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(gemm_h3_ln_launch<WN>(a, 0));
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK(gemm_h3_ln_launch<WN>(a, 0));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
 template <int MODE, int BM, int BN, int BK, int WM, int WN, int EPI = EPI_STORE>
 double run(const Shape& s, float* A, float* W, float* bias, float* Y, int iters) {
   GemmArgs a;
@@ -121,6 +142,15 @@ int main() {
     ms = run_h3<256, 2>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2", ms, true);
     ms = run_h3<256, 2>(s, bias, Y, it, true, Yp); rep("h3  256x256x32 x2 + planes out", ms, true);
     ms = run_h3<256, 2, EPI_PROBE>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2, no epilogue", ms, false);
+    if (s.N == 512) {
+      float *gam, *bet;
+      CK(hipMalloc(&gam, s.N * 4)); CK(hipMalloc(&bet, s.N * 4));
+      fill<<<(s.N + 255) / 256, 256>>>(gam, s.N, 4);
+      fill<<<(s.N + 255) / 256, 256>>>(bet, s.N, 5);
+      ms = run_ln<64>(s, bias, gam, bet, Yp, it); rep("h3  LN+GELU 128x512, 16w 64x64", ms, false);
+      ms = run_ln<128>(s, bias, gam, bet, Yp, it); rep("h3  LN+GELU 128x512, 8w 64x128", ms, false);
+      CK(hipFree(gam)); CK(hipFree(bet));
+    }
     CK(hipFree(Yp)); CK(hipFree(g_aplanes));
     CK(hipFree(g_planes));
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(bias)); CK(hipFree(Y)); CK(hipFree(Yr)); CK(hipFree(Sr));

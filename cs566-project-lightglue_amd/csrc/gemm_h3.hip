@@ -54,6 +54,10 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 }
 }  // namespace
 
+#ifndef LG_GEMM_SETPRIO
+#define LG_GEMM_SETPRIO 0
+#endif
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -165,7 +169,13 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+#if LG_GEMM_SETPRIO
+    __builtin_amdgcn_s_setprio(1);  // keeps the MFMA cluster between the barriers (guide T5)
+#endif
     compute(kt % NSTAGE);
+#if LG_GEMM_SETPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -450,15 +460,17 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   if (g.ovf && __ballot(bad) != 0ull && lane == 0) atomicOr(g.ovf, 1);
 }
 
-template <int BM, int NSTAGE>
+template <int BM, int NSTAGE, int BN = TB, int WN = 64>
 hipError_t gemm_h3_launch(const GemmH3Args& a, int epi, hipStream_t st) {
-  const int blocks = ((a.R + BM - 1) / BM) * (a.Nout / TB);
-  const dim3 grid(blocks), block(BM * 4);
+  const int blocks = ((a.R + BM - 1) / BM) * (a.Nout / BN);
+  const dim3 grid(blocks), block((BM / 64) * (BN / WN) * 64);
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_STORE, BM, NSTAGE>), grid, block, 0, st, a); break;
-    case EPI_QKV_ROT: hipLaunchKernelGGL((gemm_h3_kernel<EPI_QKV_ROT, BM, NSTAGE>), grid, block, 0, st, a); break;
-    case EPI_CROSS_QKV: hipLaunchKernelGGL((gemm_h3_kernel<EPI_CROSS_QKV, BM, NSTAGE>), grid, block, 0, st, a); break;
-    case EPI_PROBE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_PROBE, BM, NSTAGE>), grid, block, 0, st, a); break;
+    case EPI_STORE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_STORE, BM, NSTAGE, BN, WN>), grid, block, 0, st, a); break;
+    case EPI_QKV_ROT: hipLaunchKernelGGL((gemm_h3_kernel<EPI_QKV_ROT, BM, NSTAGE, BN, WN>), grid, block, 0, st, a); break;
+    case EPI_CROSS_QKV:
+      hipLaunchKernelGGL((gemm_h3_kernel<EPI_CROSS_QKV, BM, NSTAGE, BN, WN>), grid, block, 0, st, a);
+      break;
+    case EPI_PROBE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_PROBE, BM, NSTAGE, BN, WN>), grid, block, 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -20,7 +20,7 @@ static _Float16* g_planes = nullptr;  // plane image of W * 2^sw
 static _Float16* g_aplanes = nullptr; // plane image of A
 static float g_unscale = 1.f;
 
-template <int BM, int NS, int EPI = EPI_STORE>
+template <int BM, int NS, int EPI = EPI_STORE, int BN = 256, int WN = 64>
 double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out, _Float16* Yp) {
   GemmH3Args a;
   memset(&a, 0, sizeof(a));
@@ -30,10 +30,10 @@ double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out,
   if (planes_out) { a.Yp = Yp; a.yps = (long long)s.R * s.N; a.yrows_pad = s.R; }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  CK((gemm_h3_launch<BM, NS>(a, EPI, 0)));
+  CK((gemm_h3_launch<BM, NS, BN, WN>(a, EPI, 0)));
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK((gemm_h3_launch<BM, NS>(a, EPI, 0)));
+  for (int i = 0; i < iters; ++i) CK((gemm_h3_launch<BM, NS, BN, WN>(a, EPI, 0)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -142,6 +142,10 @@ int main() {
     ms = run_h3<256, 2>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2", ms, true);
     ms = run_h3<256, 2>(s, bias, Y, it, true, Yp); rep("h3  256x256x32 x2 + planes out", ms, true);
     ms = run_h3<256, 2, EPI_PROBE>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2, no epilogue", ms, false);
+    ms = run_h3<128, 2, EPI_STORE, 128>(s, bias, Y, it, true, Yp); rep("h3  128x128 x2 + planes out", ms, true);
+    ms = run_h3<128, 2, EPI_PROBE, 128>(s, bias, Y, it, false, Yp); rep("h3  128x128 x2, no epilogue", ms, false);
+    ms = run_h3<128, 2, EPI_STORE, 256>(s, bias, Y, it, true, Yp); rep("h3  128x256 x2 + planes out", ms, true);
+    ms = run_h3<128, 3, EPI_STORE, 128>(s, bias, Y, it, true, Yp); rep("h3  128x128 x3 + planes out", ms, true);
     if (s.N == 512) {
       float *gam, *bet;
       CK(hipMalloc(&gam, s.N * 4)); CK(hipMalloc(&bet, s.N * 4));

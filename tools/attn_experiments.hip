@@ -701,4 +701,273 @@ static hipError_t attention_h3pp_launch(const AttnSet& s0, const AttnSet& s1, in
   return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------------------
+// fp16x3 attention, staggered groups (PREC_H3): same operands, numerics and LDS layout as
+// attention_h3_kernel, one workgroup barrier per 64-key tile.  Waves 0-3 run each tile as
+// [QK(t) MFMAs][softmax(t) VALU][PV(t) MFMAs]; waves 4-7 (their SIMD partners) defer the PV by
+// one tile: [PV(t-1) MFMAs][QK(t) MFMAs][softmax(t) VALU].  Between the barriers the partners'
+// MFMA and VALU blocks then line up against each other for two thirds of the tile (the softmax
+// of one beside the MFMAs of the other) instead of running in lock-step.  The late group keeps
+// P(t-1) in its score registers across the barrier and reads V(t-1) while V(t+1) is being
+// staged, hence three V slots.
+// ----------------------------------------------------------------------------------------
+template <int KT>
+__global__ __launch_bounds__(512, 2) void attention_h3s_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+                                                                float scale_log2e) {
+  constexpr int WAVES = 8, NT = 64 * WAVES, QB = 32 * WAVES;
+  constexpr int NSUB = KT / 32;
+  constexpr int KLD = kHeadDim + 8;       // K plane row stride (fp16)
+  constexpr int CH = 2 * KT * 8;          // 16-byte chunks per tile per tensor
+  constexpr int LDC = CH / NT;            // chunks per thread per tensor
+  constexpr int KPL = KT * KLD, VPL = KT * kHeadDim;
+  static_assert(CH % NT == 0, "tile/threads mismatch");
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[2 * 2 * KPL];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[3 * 2 * VPL];
+
+  const int item = xcd_chunk(blockIdx.x, gridDim.x);
+  const int qb = item % nqb;
+  const int sbh = item / nqb;
+  const int set = sbh / (B * H), bh = sbh - set * (B * H);
+  const AttnSet& S = set == 0 ? s0 : s1;
+  const int q_blk = qb * QB;
+  if (q_blk >= S.Nq) return;
+  const int Nq = S.Nq, Nk = S.Nk;
+  const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
+  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
+  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
+  const long long ps = S.pstride;
+  const int head = bh % H;
+  const int b = bh / H;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool late = wave >= 4;
+  const int l32 = lane & 31, half = lane >> 5;
+
+  const int qrow = min(q_blk + wave * 32 + l32, Nq - 1);
+  f16x8 qh[4], ql[4];  // q_h * 2^11 is re-formed per tile (the wave is at the VGPR limit)
+  float c_lane;
+  {
+    const float* qr = Q + (size_t)qrow * kHeadDim + half * 8;
+    f32x4 x[4][2];
+    float mx = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      x[s][0] = *reinterpret_cast<const f32x4*>(qr + 16 * s);
+      x[s][1] = *reinterpret_cast<const f32x4*>(qr + 16 * s + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[s][0][e]), fabsf(x[s][1][e])));
+    }
+    mx = max_xor32(mx);
+    int ex = 0;
+    if (mx > 0.f && mx <= 3.0e38f) {
+      int E;
+      (void)frexpf(mx, &E);
+      ex = min(max(4 - E, -100), 100);
+    }
+    c_lane = ldexpf(scale_log2e, -(11 + ex));
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 h, l;
+        split2h(ldexpf(x[s][e >> 2][e & 3], ex), h, l);
+        qh[s][e] = h;
+        ql[s][e] = l;
+      }
+  }
+
+  f32x4 rk[LDC], rv[LDC];
+  auto gload = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < LDC; ++i) {
+      const int c = tid + i * NT;
+      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
+      const size_t src = (size_t)p * ps + (size_t)min(t0 + r, Nk - 1) * kHeadDim + cb * 8;
+      rk[i] = *reinterpret_cast<const f32x4*>(Kp + src);
+      rv[i] = *reinterpret_cast<const f32x4*>(Vp + src);
+    }
+  };
+  auto sstore = [&](int kbuf, int vbuf) {
+#pragma unroll
+    for (int i = 0; i < LDC; ++i) {
+      const int c = tid + i * NT;
+      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
+      *reinterpret_cast<f32x4*>(&Ks[(kbuf * 2 + p) * KPL + r * KLD + cb * 8]) = rk[i];
+      *reinterpret_cast<f32x4*>(&Vs[(vbuf * 2 + p) * VPL + r * kHeadDim + ((cb ^ (((r >> 1) & 1) << 2)) * 8)]) = rv[i];
+    }
+  };
+
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tdim = ((lane >> 4) & 1) * 16 + 4 * tp;
+  const int sw = ((tq >> 1) & 1) << 5;
+  const int koff = l32 * KLD + 8 * half;
+  const int voff0 = (4 * half + tq) * kHeadDim + (tdim ^ sw);
+  const int voff1 = (4 * half + tq) * kHeadDim + ((32 + tdim) ^ sw);
+
+  f32x16 o0 = f32x16{0.f}, o1 = f32x16{0.f};
+  float m_use = -INFINITY;
+  float l_run = 0.f;
+  f32x16 sc[NSUB];  // S(t), then P(t) in place (the late group carries P(t-1) across the barrier)
+
+  // S^T = K Q^T (x 2^(11+e)) for the K tile in slot kbuf
+  auto qk = [&](int kbuf) {
+    const _Float16* Kc = Ks + kbuf * 2 * KPL + koff;
+    f16x8 kf[NSUB][4][2];
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int off = u * 32 * KLD + 16 * s;
+        kf[u][s][0] = *reinterpret_cast<const f16x8*>(Kc + off);
+        kf[u][s][1] = *reinterpret_cast<const f16x8*>(Kc + KPL + off);
+      }
+    _Float16 two11 = (_Float16)kLoScale;
+    asm volatile("" : "+v"(two11));  // keeps q_h * 2^11 from being hoisted out of the loop
+    f16x8 qhs[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qhs[s] = qh[s] * two11;
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) {
+      sc[u] = f32x16{0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sc[u] = mfma_h3(kf[u][s][0], kf[u][s][1], qhs[s], ql[s], qh[s], sc[u]);
+    }
+  };
+  // mask / tile max / lazy reference raise / exp / sum: S(t) -> P(t) in sc
+  auto softmax = [&](int t0) {
+    if (t0 + KT > Nk) {
+#pragma unroll
+      for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (t0 + u * 32 + row32(r, half) >= Nk) sc[u][r] = -INFINITY;
+    }
+    float mr[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float m = sc[0][r];
+#pragma unroll
+      for (int u = 1; u < NSUB; ++u) m = fmaxf(m, sc[u][r]);
+      mr[r] = m;
+    }
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+      for (int r = 0; r < w; ++r) mr[r] = fmaxf(mr[r], mr[r + w]);
+    const float tmax = max_xor32(mr[0]);
+    const bool need = (tmax - m_use) * c_lane > 3.f;
+    if (__ballot(need) != 0ull) {
+      // O holds every tile before t here (both groups): the rescale covers all of it
+      const float m_new = need ? tmax : m_use;
+      const float alpha = __builtin_amdgcn_exp2f((m_use - m_new) * c_lane);
+      m_use = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+    const float mb = m_use * c_lane;
+    float ps8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ps8[i] = 0.f;
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c_lane, -mb));
+        sc[u][r] = p;
+        ps8[(u * 16 + r) & 7] += p;
+      }
+    l_run += ((ps8[0] + ps8[1]) + (ps8[2] + ps8[3])) + ((ps8[4] + ps8[5]) + (ps8[6] + ps8[7]));
+  };
+  // O^T += V^T P^T (x 2^11) for the V tile in slot vbuf, P in sc
+  auto pv = [&](int vbuf) {
+    const _Float16* Vc = Vs + vbuf * 2 * VPL;
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int vr = (u * 32 + 16 * s) * kHeadDim;
+        f16x8 v[2][2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const f16x4 a0 = tr_read_h(Vc + p * VPL + vr + voff0);
+          const f16x4 a1 = tr_read_h(Vc + p * VPL + vr + 8 * kHeadDim + voff0);
+          const f16x4 b0 = tr_read_h(Vc + p * VPL + vr + voff1);
+          const f16x4 b1 = tr_read_h(Vc + p * VPL + vr + 8 * kHeadDim + voff1);
+          v[0][p] = f16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          v[1][p] = f16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        }
+        f16x8 ph, phs, pl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = sc[u][8 * s + j];
+          const _Float16 h = (_Float16)p;
+          const _Float16 hs = h * (_Float16)kLoScale;
+          ph[j] = h;
+          phs[j] = hs;
+          pl[j] = (_Float16)fmaf(p, kLoScale, -(float)hs);
+        }
+        o0 = mfma_h3(v[0][0], v[0][1], phs, pl, ph, o0);
+        o1 = mfma_h3(v[1][0], v[1][1], phs, pl, ph, o1);
+      }
+  };
+
+  const int ntiles = (Nk + KT - 1) / KT;
+  gload(0);
+  sstore(0, 0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int t0 = t * KT;
+    if (t + 1 < ntiles) gload(t0 + KT);
+    if (!late) {
+      qk(t & 1);
+      softmax(t0);
+      pv(t % 3);
+    } else {
+      if (t > 0) pv((t + 2) % 3);  // PV(t-1): V(t-1) in slot (t-1) % 3
+      qk(t & 1);
+      softmax(t0);
+    }
+    if (t + 1 < ntiles) sstore((t + 1) & 1, (t + 1) % 3);
+    __syncthreads();
+  }
+  if (late) pv((ntiles + 2) % 3);
+
+  const float l_tot = sum_xor32(l_run);
+  const float inv = ldexpf(1.f / l_tot, -11);  // 2^-11 exact: same rounding as (o 2^-11) / l
+  const int q = q_blk + wave * 32 + l32;
+  if (q < Nq) {
+    const int orow = S.o_row0 + b * Nq + q;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          _Float16 a, c;
+          split2h((hf ? o1 : o0)[4 * g + e] * inv, a, c);
+          h[e] = a;
+          l[e] = c;
+        }
+        const size_t off = plane_off(orow, head * kHeadDim + hf * 32 + 8 * g + 4 * half, S.o_rows_pad);
+        *reinterpret_cast<f16x4*>(S.op + off) = h;
+        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+      }
+  }
+}
+
+template <int KT>
+static hipError_t attention_h3s_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+  constexpr int QB = 256;
+  const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
+  if (nq == 0 || B == 0) return hipSuccess;
+  if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
+  const int nqb = (nq + QB - 1) / QB;
+  const int items = nqb * B * H * 2;
+  hipLaunchKernelGGL((attention_h3s_kernel<KT>), dim3(items), dim3(512), 0, st, s0, s1, B, H, nqb,
+                     scale * 1.4426950408889634f);
+  return hipGetLastError();
+}
+
 }  // namespace lg

@@ -100,6 +100,17 @@ __device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, f32x16 
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// the same with v_mfma_f32_16x16x32_f16: lane l supplies A[l & 15][8 (l >> 4) + j] and
+// B[8 (l >> 4) + j][l & 15]; accumulator register r of lane l holds C[4 (l >> 4) + r][l & 15]
+typedef float f32x4_ __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4_ mfma_h3_16(const f16x8& xh, const f16x8& xl, const f16x8& yhs, const f16x8& yl,
+                                             const f16x8& yh, f32x4_ c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, yh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, yl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, yhs, c, 0, 0, 0);
+  return c;
+}
+
 // acc += 2^11 * (x . y), x = (xh, xl), y = (yhs = yh * 2^11, yl, yh); smallest terms first
 __device__ __forceinline__ f32x16 mfma_h3(const f16x8& xh, const f16x8& xl, const f16x8& yhs, const f16x8& yl,
                                           const f16x8& yh, f32x16 c) {
@@ -115,10 +126,12 @@ __device__ __forceinline__ f32x16 mfma_h3(const f16x8& xh, const f16x8& xl, cons
 // tile is one contiguous block per plane and the GEMM stages it with plain LDS-DMA copies:
 //   [plane 0 (h) | plane 1 (l * 2^11)][K / 32 kblocks][rows_pad][32]
 // i.e. 64-byte rows of four 16-byte chunks; chunk c (k = 8c..8c+7 of the kblock) of row r is
-// stored at chunk c ^ plane_swz(r) (the swizzle that makes the GEMM's ds_read_b128 fragment
-// groups {0-3,12-15,20-27} conflict-free).  rows_pad is a multiple of 256 (the GEMM row tile).
+// stored at chunk c ^ plane_swz(r): the swizzle under which the GEMM's 16x16x32 fragment reads
+// (lane l: row l & 15 of a 16-row block, chunk l >> 4) hit all 16 slots of a 256-byte bank line
+// in every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...): with
+// k = (r >> 2) & 3, plane_swz = sigma(k), sigma = (0, 2, 3, 1).  rows_pad is a multiple of 256.
 constexpr int kKB = 32;  // k-block (columns per plane row)
-__device__ __forceinline__ int plane_swz(int row) { return (row >> 2) & 3; }
+__device__ __forceinline__ int plane_swz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 // element offset of (row, k) inside one plane of an image with `rows_pad` rows
 __device__ __forceinline__ size_t plane_off(int row, int k, int rows_pad) {
   return ((size_t)(k >> 5) * rows_pad + row) * kKB + ((((k >> 3) & 3) ^ plane_swz(row)) << 3) + (k & 7);

@@ -26,6 +26,8 @@
 // 256 x 256 x 32 beat 128 x 256 at two workgroups per CU and every k-tile of 16 with 2-4
 // stages).  blockIdx -> tile through a bijective XCD remap so the column tiles of one row panel
 // share an XCD's L2.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -56,6 +58,12 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 
 #ifndef LG_GEMM_SETPRIO
 #define LG_GEMM_SETPRIO 0
+#endif
+#ifndef LG_GEMM_MF16
+// MFMA shape: 1 = v_mfma_f32_16x16x32_f16 (one instruction per 32-k tile; on random operands the
+// chip sustains ~1.2x the flop rate of the 32x32x16 shape, tools/probe_mfma_shape.hip),
+// 0 = v_mfma_f32_32x32x16_f16
+#define LG_GEMM_MF16 1
 #endif
 
 template <int N>
@@ -118,11 +126,33 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     }
   };
 
-  f32x16 acc[2][NJ];
+  // wave tile 64 x WN as TI x TJ MFMA tiles of TR accumulator registers
+  constexpr bool kMF16 = LG_GEMM_MF16 != 0;
+  constexpr int TI = kMF16 ? 4 : 2, TJ = kMF16 ? WN / 16 : NJ, TR = kMF16 ? 4 : 16;
+  using AccT = typename std::conditional<kMF16, f32x4, f32x16>::type;
+  AccT acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{0.f};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = AccT{0.f};
+  // visit(i, fn): every accumulator element of the wave tile's row pass i (rows 32i .. 32i+31),
+  // as acc = fn(local row rr in [0,32), local column c in [0,WN), acc)
+  auto visit = [&](int i, auto fn) {
+    if constexpr (kMF16) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc[2 * i + a][j][r] = fn(a * 16 + (lane >> 4) * 4 + r, j * 16 + (lane & 15), acc[2 * i + a][j][r]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = fn(row32(r, half), j * 32 + l32, acc[i][j][r]);
+    }
+  };
 
   // fragment (row r, 16-byte k-chunk c) of the plane tile at byte offset t0 of a stage
   auto frag = [&](const char* st, int t0, int r, int c) {
@@ -130,6 +160,27 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   };
   auto compute = [&](int stage) {
     const char* st = smem + stage * STAGE_BYTES;
+    if constexpr (kMF16) {
+      // lane: row (lane & 15) of each 16-row block, k chunk lane >> 4 (k = 8c .. 8c+7)
+      const int c = lane >> 4, r16 = lane & 15;
+      f16x8 ah[TI], al[TI];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wm0 + i * 16 + r16;
+        ah[i] = frag(st, 0, r, c);
+        al[i] = frag(st, APT, r, c);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn0 + j * 16 + r16;
+        const f16x8 wh = frag(st, 2 * APT, r, c);
+        const f16x8 wl = frag(st, 2 * APT + WPT, r, c);
+        const f16x8 whs = wh * (_Float16)kLoScale;  // exact: |W_h| < 16
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[i][j] = mfma_h3_16(ah[i], al[i], whs, wl, wh, acc[i][j]);
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       const int c = 2 * s + half;
@@ -150,7 +201,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_h3(ah[i], al[i], whs[j], wl[j], wh[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j)
+          if constexpr (!kMF16) acc[i][j] = mfma_h3(ah[i], al[i], whs[j], wl[j], wh[j], acc[i][j]);
     }
   };
 
@@ -187,21 +239,22 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     // timing probe (tools/kbench_gemm.hip): keeps the accumulators live, stores nothing
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
+      for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        for (int r = 0; r < TR; ++r) t += acc[i][j][r];
     if (t == 1234.5678f) g.Y[tid] = t;
   } else if constexpr (EPI == EPI_LN_GELU) {
     // ffn.0 + ffn.1 LayerNorm(512, eps 1e-5) + ffn.2 GELU(erf) (lightglue.py:171-176), fused: the
     // workgroup holds complete rows (BN = 512), so the row statistics are reduced in LDS (free
     // after the k-loop) and the activations leave only as the plane image ffn.3 consumes.
-    static_assert(BN == 512 && BM == 128, "LN epilogue tile");
+    static_assert(BN == 512 && BM == 128 && WN == 64, "LN epilogue tile");
     constexpr int NT = NW * 64;
     constexpr int PARTS = NT / BM;            // threads per row in the table reduction
-    constexpr int RS = WGN * 32 + 4;          // row stride of the partial-sum table (floats)
-    constexpr int PW = WGN * 32 / PARTS;      // partials summed per thread
+    constexpr int LC = kMF16 ? 16 : 32;       // lanes sharing a row within a wave
+    constexpr int RS = WGN * LC + 4;          // row stride of the partial-sum table (floats)
+    constexpr int PW = WGN * LC / PARTS;      // partials summed per thread
     static_assert(PW % 4 == 0, "table reduction");
     constexpr int SCRATCH = NSTAGE * STAGE_BYTES / 4;  // floats
     // LDS (free after the k-loop): [partial table | ... | mean | rstd]; the per-wave transpose
@@ -211,30 +264,31 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     float* rstd_s = mean_s + BM;                           // [BM]
     float* ep = red + wave * (32 * 64);                    // per-wave transpose buffer
     static_assert(BM * RS + 2 * BM <= SCRATCH && NW * 32 * 64 + 2 * BM <= SCRATCH, "epilogue scratch");
-    float gj[NJ], bj[NJ];
+    // per-lane columns: j * LC + (lane % LC) of the wave tile
+    const int lcol = kMF16 ? (lane & 15) : l32;
+    float bj_[TJ], gj[TJ], bj[TJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int col = n0 + wn0 + j * 32 + l32;
-      const float bias = g.bias ? g.bias[col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = fmaf(acc[i][j][r], g.acc_scale, bias);
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * LC + lcol;
+      bj_[j] = g.bias ? g.bias[col] : 0.f;
       gj[j] = g.ln_g[col];
       bj[j] = g.ln_b[col];
     }
-    // row sum of f(v) over the 512 columns: lane partials over its NJ columns -> table ->
-    // 4 threads per row (32 partials each) -> shuffle
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      visit(i, [&](int, int c, float v) { return fmaf(v, g.acc_scale, bj_[c / LC]); });
+    // row sum of f(v) over the 512 columns: lane partials over its TJ columns -> table ->
+    // PARTS threads per row -> shuffle
     auto row_total = [&](auto f, float* out) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int lr = wm0 + i * 32 + row32(r, half);
+        for (int r = 0; r < TR; ++r) {
+          const int lr = wm0 + (kMF16 ? i * 16 + (lane >> 4) * 4 + r : i * 32 + row32(r, half));
           float p = 0.f;
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) p += f(acc[i][j][r], lr);
-          red[lr * RS + (wave % WGN) * 32 + l32] = p;
+          for (int j = 0; j < TJ; ++j) p += f(acc[i][j][r], lr);
+          red[lr * RS + (wave % WGN) * LC + lcol] = p;
         }
       __syncthreads();
       const int row = tid / PARTS, part = tid % PARTS;
@@ -259,20 +313,15 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     // normalise + GELU, then 16-byte plane-image stores through the per-wave transpose buffer
     const int cq = (lane & 7) * 8;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int jh = 0; jh < NJ / 2; ++jh) {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const int j = 2 * jh + jj;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rr = row32(r, half), lr = wm0 + i * 32 + rr;
-            const float y = (acc[i][j][r] - mean_s[lr]) * rstd_s[lr] * gj[j] + bj[j];
-            const int c = jj * 32 + l32;
-            ep[rr * 64 + (c ^ ((rr & 1) << 2))] = 0.5f * y * (1.f + erff(y * 0.70710678118654752f));
-          }
-        }
+    for (int i = 0; i < 2; ++i) {
+      constexpr int jh = 0;  // WN == 64: one 64-column pass per row pass
+      visit(i, [&](int rr, int c, float v) {
+        const int lr = wm0 + i * 32 + rr;
+        const float y = (v - mean_s[lr]) * rstd_s[lr] * gj[c / LC] + bj[c / LC];
+        ep[rr * 64 + (c ^ ((rr & 1) << 2))] = 0.5f * y * (1.f + erff(y * 0.70710678118654752f));
+        return v;
+      });
+      {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -299,6 +348,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
       }
+    }
   } else if constexpr (EPI == EPI_STORE) {
     static_assert(WN == 64, "EPI_STORE tile");
     // Transposed through LDS (free after the k-loop; 8 KiB per wave per 32-row pass) so that every
@@ -316,13 +366,10 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rr = row32(r, half), c = j * 32 + l32;
-          ep[rr * 64 + (c ^ ((rr & 1) << 2))] = acc[i][j][r];
-        }
+      visit(i, [&](int rr, int c, float v) {
+        ep[rr * 64 + (c ^ ((rr & 1) << 2))] = v;
+        return v;
+      });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -401,13 +448,11 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     for (int e = 0; e < 8; ++e) bd[e] = g.bias[cbase + ((d0 + e) & 1) * 32 + ((d0 + e) >> 1)];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rr = row32(r, half), dim = 2 * l32 + j;
-          ep[rr * 64 + (dim ^ ((rr & 1) << 2))] = acc[i][j][r];
-        }
+      visit(i, [&](int rr, int c, float v) {
+        const int dim = c < 32 ? 2 * c : 2 * (c - 32) + 1;
+        ep[rr * 64 + (dim ^ ((rr & 1) << 2))] = v;
+        return v;
+      });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int k = 0; k < 4; ++k) {

@@ -152,7 +152,7 @@ int main() {
       fill<<<(s.N + 255) / 256, 256>>>(gam, s.N, 4);
       fill<<<(s.N + 255) / 256, 256>>>(bet, s.N, 5);
       ms = run_ln<64>(s, bias, gam, bet, Yp, it); rep("h3  LN+GELU 128x512, 16w 64x64", ms, false);
-      ms = run_ln<128>(s, bias, gam, bet, Yp, it); rep("h3  LN+GELU 128x512, 8w 64x128", ms, false);
+
       CK(hipFree(gam)); CK(hipFree(bet));
     }
     CK(hipFree(Yp)); CK(hipFree(g_aplanes));

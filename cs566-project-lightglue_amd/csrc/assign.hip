@@ -6,9 +6,9 @@
 //   filter_matches              lightglue.py:321-337 (== superglue.py:288-298)
 //
 // All passes stream the [B,M,N] similarity (HBM/Infinity-Cache bound, no MFMA):
-//   row stats   one wave per row (max, then sum of exp(x - max))
-//   col stats   256 columns x a 64-row chunk per workgroup -> per-chunk partials, combined in
-//               chunk order (max pass, then sum pass)
+//   row stats   one wave per row (max, then sum of exp(x - max); 16-byte loads)
+//   col stats   256 columns x a 64-row chunk per workgroup, one read: running (max, sum) per
+//               column -> per-chunk partials, combined in chunk order
 //   row pass    one wave per row: the la value, written once, and the row argmax
 //   col argmax  per-chunk partial (value, first index) -> combine
 //   filter      one thread per keypoint
@@ -49,45 +49,64 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const float* sim, int ro
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float* x = sim + (size_t)row * N;
-  float m = -INFINITY;
-  for (int j = lane; j < N; j += 64) m = fmaxf(m, x[j]);
-  m = wave_max(m);
-  float s = 0.f;
-  for (int j = lane; j < N; j += 64) s += expf(x[j] - m);
+  float m = -INFINITY, s = 0.f;
+  if ((N & 3) == 0) {  // 16-byte loads (the second pass re-reads the 8 KiB row from cache)
+    for (int j = 4 * lane; j < N; j += 256) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + j);
+      m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    }
+    m = wave_max(m);
+    for (int j = 4 * lane; j < N; j += 256) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + j);
+      s += (expf(v[0] - m) + expf(v[1] - m)) + (expf(v[2] - m) + expf(v[3] - m));
+    }
+  } else {
+    for (int j = lane; j < N; j += 64) m = fmaxf(m, x[j]);
+    m = wave_max(m);
+    for (int j = lane; j < N; j += 64) s += expf(x[j] - m);
+  }
   s = wave_sum(s);
   if (lane == 0) { rmax[row] = m; rlog[row] = logf(s); }
 }
 
-// pass 0: per-chunk column max; pass 1: per-chunk sum of exp(x - cmax)
-template <int PASS>
-__global__ __launch_bounds__(256) void col_partial_kernel(const float* sim, int M, int N, const float* cmax, float* part) {
+// Column statistics of one 64-row chunk in a single read: running (max, sum of exp(x - max))
+// per column, rescaled when the max rises (rare after the first rows).
+__global__ __launch_bounds__(256) void col_stats_partial_kernel(const float* sim, int M, int N, float* pmax,
+                                                                float* psum) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int ch = blockIdx.y, b = blockIdx.z;
   const int nch = gridDim.y;
   if (j >= N) return;
   const int i0 = ch * CCH, i1 = min(M, i0 + CCH);
   const float* x = sim + (size_t)b * M * N + j;
-  float acc;
-  if (PASS == 0) {
-    acc = -INFINITY;
-    for (int i = i0; i < i1; ++i) acc = fmaxf(acc, x[(size_t)i * N]);
-  } else {
-    const float m = cmax[b * N + j];
-    acc = 0.f;
-    for (int i = i0; i < i1; ++i) acc += expf(x[(size_t)i * N] - m);
+  float m = -INFINITY, acc = 0.f;
+  for (int i = i0; i < i1; ++i) {
+    const float v = x[(size_t)i * N];
+    if (v > m) {
+      acc = acc * expf(m - v) + 1.f;
+      m = v;
+    } else {
+      acc += expf(v - m);
+    }
   }
-  part[((size_t)b * nch + ch) * N + j] = acc;
+  pmax[((size_t)b * nch + ch) * N + j] = m;
+  psum[((size_t)b * nch + ch) * N + j] = acc;
 }
 
-template <int PASS>
-__global__ void col_combine_kernel(const float* part, int nch, int N, int BN, float* out) {
+// combine the chunk partials in chunk order: cmax = max_c m_c, clog = log(sum_c s_c exp(m_c - cmax))
+__global__ void col_stats_combine_kernel(const float* pmax, const float* psum, int nch, int N, int BN, float* cmax,
+                                         float* clog) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= BN) return;
   const int b = t / N, j = t - b * N;
-  const float* p = part + (size_t)b * nch * N + j;
-  float acc = PASS == 0 ? -INFINITY : 0.f;
-  for (int c = 0; c < nch; ++c) acc = PASS == 0 ? fmaxf(acc, p[(size_t)c * N]) : acc + p[(size_t)c * N];
-  out[t] = PASS == 0 ? acc : logf(acc);
+  const float* pm = pmax + (size_t)b * nch * N + j;
+  const float* pv = psum + (size_t)b * nch * N + j;
+  float m = -INFINITY;
+  for (int c = 0; c < nch; ++c) m = fmaxf(m, pm[(size_t)c * N]);
+  float s = 0.f;
+  for (int c = 0; c < nch; ++c) s += pv[(size_t)c * N] * expf(pm[(size_t)c * N] - m);
+  cmax[t] = m;
+  clog[t] = logf(s);
 }
 
 __global__ void logsig_kernel(const float* z, float* ls, int n) {
@@ -224,10 +243,10 @@ hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st) {
   const int nch = (M + CCH - 1) / CCH;
   hipLaunchKernelGGL(row_stats_kernel, dim3((B * M + 3) / 4), dim3(256), 0, st, a.sim, B * M, N, s.rmax, s.rlog);
   const dim3 cg((N + 255) / 256, nch, B);
-  hipLaunchKernelGGL(col_partial_kernel<0>, cg, dim3(256), 0, st, a.sim, M, N, nullptr, s.pv);
-  hipLaunchKernelGGL(col_combine_kernel<0>, dim3((B * N + 255) / 256), dim3(256), 0, st, s.pv, nch, N, B * N, s.cmax);
-  hipLaunchKernelGGL(col_partial_kernel<1>, cg, dim3(256), 0, st, a.sim, M, N, s.cmax, s.pv);
-  hipLaunchKernelGGL(col_combine_kernel<1>, dim3((B * N + 255) / 256), dim3(256), 0, st, s.pv, nch, N, B * N, s.clog);
+  float* psum = reinterpret_cast<float*>(s.pi);  // the argmax index partials are not live yet
+  hipLaunchKernelGGL(col_stats_partial_kernel, cg, dim3(256), 0, st, a.sim, M, N, s.pv, psum);
+  hipLaunchKernelGGL(col_stats_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s.pv, psum, nch, N, B * N,
+                     s.cmax, s.clog);
   hipLaunchKernelGGL(logsig_kernel, dim3((B * M + 255) / 256), dim3(256), 0, st, a.z0, s.ls0, B * M);
   hipLaunchKernelGGL(logsig_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, a.z1, s.ls1, B * N);
   if (a.la) hipLaunchKernelGGL(la_last_row_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, a.z1, a.la, B, M, N);

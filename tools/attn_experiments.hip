@@ -970,4 +970,287 @@ static hipError_t attention_h3s_launch(const AttnSet& s0, const AttnSet& s1, int
   return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------------------
+// attention_h3m_kernel -- measured, superseded by attention_h3f_kernel (same MFMA data flow,
+// leaner softmax).  fp16x3 attention on v_mfma_f32_16x16x32_f16: the schedule of attention_h3_kernel
+// (8 waves x 32 queries, 64-key tiles double-buffered in LDS, one barrier per tile, lazy softmax
+// reference, context straight into ffn.0's plane image) with 16 x 16 MFMA tiles, which the chip
+// runs at a higher sustained rate than 32 x 32 tiles on random data (tools/probe_mfma_shape.hip).
+//   S^T[key][query] = K Q^T:  A = K tile (16 keys x 32 dims, lane: key l&15, dims 8(l>>4)..),
+//                             B = Q^T (lane: query l&15, dims 8(l>>4)..), two k-steps per head.
+//     Accumulator: lane l holds query l&15, keys 4(l>>4) + r (r < 4) of each 16-key tile.
+//   O^T[dim][query] += V^T P^T over 32-key steps p: B = P^T with k index 8g+j <-> key
+//     32p + 16(j>>2) + 4g + (j&3) (g = l>>4) -- exactly the S^T registers the lane already holds;
+//     A = V^T, lane: dim l&15 of a 16-dim tile, the same 8 keys, two ds_read_b64_tr_b16 (4 keys
+//     x 16 dims each per 16-lane group).
+//   Per-query reductions (max, sum, q range) run over the 4 lanes sharing l&15 (xor 16, xor 32).
+// LDS: rows of 64 halves (128 B); K 16-byte chunk c of row r at c ^ ((r >> 1) & 7), V chunk c at
+// c ^ 2((r >> 1) & 3) -- conflict-free for the b128 fragment reads and the transposed reads.
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ float max_xor16_32(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return max_xor32(v);
+}
+__device__ __forceinline__ float sum_xor16_32(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return sum_xor32(v);
+}
+
+template <int KT>
+__global__ __launch_bounds__(512, 2) void attention_h3m_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+                                                                float scale_log2e) {
+  constexpr int WAVES = 8, NT = 64 * WAVES, QB = 32 * WAVES;
+  constexpr int NKT = KT / 16;             // 16-key tiles per tile
+  constexpr int CH = 2 * KT * 8;           // 16-byte chunks per tile per tensor
+  constexpr int LDC = CH / NT;
+  constexpr int PL = KT * kHeadDim;        // one plane of a tile (elements)
+  static_assert(CH % NT == 0 && KT % 32 == 0, "tile/threads mismatch");
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[2 * 2 * PL];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[2 * 2 * PL];
+
+  const int item = xcd_chunk(blockIdx.x, gridDim.x);
+  const int qb = item % nqb;
+  const int sbh = item / nqb;
+  const int set = sbh / (B * H), bh = sbh - set * (B * H);
+  const AttnSet& S = set == 0 ? s0 : s1;
+  const int q_blk = qb * QB;
+  if (q_blk >= S.Nq) return;
+  const int Nq = S.Nq, Nk = S.Nk;
+  const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
+  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
+  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
+  const long long ps = S.pstride;
+  const int head = bh % H;
+  const int b = bh / H;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+
+  // Q^T B operand: query qt*16 + r16 of the wave, k-step ks: dims 32 ks + 8 g + j, scaled per
+  // query by 2^ex (row max over the 4 lanes sharing the query in [8, 16))
+  f16x8 qh[2][2], qhs[2][2], ql[2][2];
+  float c_lane[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qrow = min(q_blk + wave * 32 + qt * 16 + r16, Nq - 1);
+    const float* qr = Q + (size_t)qrow * kHeadDim + 8 * g;
+    f32x4 x[2][2];
+    float mx = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      x[ks][0] = *reinterpret_cast<const f32x4*>(qr + 32 * ks);
+      x[ks][1] = *reinterpret_cast<const f32x4*>(qr + 32 * ks + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[ks][0][e]), fabsf(x[ks][1][e])));
+    }
+    mx = max_xor16_32(mx);
+    int ex = 0;
+    if (mx > 0.f && mx <= 3.0e38f) {
+      int E;
+      (void)frexpf(mx, &E);
+      ex = min(max(4 - E, -100), 100);
+    }
+    c_lane[qt] = ldexpf(scale_log2e, -(11 + ex));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 h, l;
+        split2h(ldexpf(x[ks][e >> 2][e & 3], ex), h, l);
+        qh[qt][ks][e] = h;
+        ql[qt][ks][e] = l;
+        qhs[qt][ks][e] = h * (_Float16)kLoScale;
+      }
+  }
+
+  // tile staging through registers: chunk c -> plane c / (KT*8), row (c / 8) % KT, chunk c % 8
+  f32x4 rk[LDC], rv[LDC];
+  auto gload = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < LDC; ++i) {
+      const int c = tid + i * NT;
+      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
+      const size_t src = (size_t)p * ps + (size_t)min(t0 + r, Nk - 1) * kHeadDim + cb * 8;
+      rk[i] = *reinterpret_cast<const f32x4*>(Kp + src);
+      rv[i] = *reinterpret_cast<const f32x4*>(Vp + src);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LDC; ++i) {
+      const int c = tid + i * NT;
+      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
+      *reinterpret_cast<f32x4*>(&Ks[(buf * 2 + p) * PL + r * kHeadDim + ((cb ^ ((r >> 1) & 7)) * 8)]) = rk[i];
+      *reinterpret_cast<f32x4*>(&Vs[(buf * 2 + p) * PL + r * kHeadDim + ((cb ^ (((r >> 1) & 3) << 1)) * 8)]) = rv[i];
+    }
+  };
+
+  // per-lane LDS offsets (elements).  K fragment (key kt*16 + r16, chunk 4 ks + g), swizzle of row
+  // r16 (kt*16 does not change (r >> 1) & 7).  V transposed read: the 16-lane group g reads rows
+  // (keys) 32p + 16h + 4g + q (q = (lane & 15) >> 2) at dims 16 dt + 4 (lane & 3); row bits (r>>1)&3
+  // = (2g + (q >> 1)) & 3.
+  const int kswz = (r16 >> 1) & 7;
+  const int koff = r16 * kHeadDim;
+  const int vq = (lane & 15) >> 2, vp4 = lane & 3;
+  const int vrow = 4 * g + vq;
+  const int vswz = ((vrow >> 1) & 3) << 1;
+
+  f32x4 o[4][2];  // O^T tiles (x 2^11): [dim tile dt][query tile qt]
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt][0] = o[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_use[2] = {-INFINITY, -INFINITY};
+  float l_run[2] = {0.f, 0.f};
+
+  const int ntiles = (Nk + KT - 1) / KT;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const int t0 = t * KT;
+    const _Float16* Kc = Ks + cur * 2 * PL;
+    const _Float16* Vc = Vs + cur * 2 * PL;
+
+    // ---- S^T = K Q^T
+    f16x8 kf[NKT][2][2];  // [key tile][k-step][plane]
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int off = kt * 16 * kHeadDim + koff + (((4 * ks + g) ^ kswz) << 3);
+        kf[kt][ks][0] = *reinterpret_cast<const f16x8*>(Kc + off);
+        kf[kt][ks][1] = *reinterpret_cast<const f16x8*>(Kc + PL + off);
+      }
+    asm volatile("" ::: "memory");
+    if (t + 1 < ntiles) gload(t0 + KT);
+    f32x4 sc[NKT][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) a = mfma_h3_16(kf[kt][ks][0], kf[kt][ks][1], qhs[qt][ks], ql[qt][ks], qh[qt][ks], a);
+        sc[kt][qt] = a;
+      }
+    // ---- V^T fragments of the tile: [32-key step p][dim tile dt][plane] (8 keys per lane)
+    f16x8 vf[NKT / 2][4][2];
+#pragma unroll
+    for (int p = 0; p < NKT / 2; ++p)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          // rows 32p + vrow and 32p + 16 + vrow; dims 16 dt + 4 vp4 -> chunk 2dt + (vp4 >> 1), 8-byte half vp4 & 1
+          const int col = ((((2 * dt + (vp4 >> 1)) ^ vswz) << 3) + 4 * (vp4 & 1));
+          const f16x4 lo = tr_read_h(Vc + pl * PL + (32 * p + vrow) * kHeadDim + col);
+          const f16x4 hi = tr_read_h(Vc + pl * PL + (32 * p + 16 + vrow) * kHeadDim + col);
+          vf[p][dt][pl] = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+    asm volatile("" ::: "memory");
+    // ---- softmax per query tile: keys t0 + 16 kt + 4 g + r
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      if (t0 + KT > Nk) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t0 + 16 * kt + 4 * g + r >= Nk) sc[kt][qt][r] = -INFINITY;
+      }
+      float mr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float m = sc[0][qt][r];
+#pragma unroll
+        for (int kt = 1; kt < NKT; ++kt) m = fmaxf(m, sc[kt][qt][r]);
+        mr[r] = m;
+      }
+      const float tmax = max_xor16_32(fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3])));
+      const bool need = (tmax - m_use[qt]) * c_lane[qt] > 3.f;
+      if (__ballot(need) != 0ull) {
+        const float m_new = need ? tmax : m_use[qt];
+        const float alpha = __builtin_amdgcn_exp2f((m_use[qt] - m_new) * c_lane[qt]);
+        m_use[qt] = m_new;
+        l_run[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[dt][qt][r] *= alpha;
+      }
+      const float mb = m_use[qt] * c_lane[qt];
+      float ps4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kt][qt][r], c_lane[qt], -mb));
+          sc[kt][qt][r] = pv;
+          ps4[r] += pv;
+        }
+      l_run[qt] += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
+    }
+    // ---- O^T += V^T P^T (x 2^11), 32 keys per step
+#pragma unroll
+    for (int p = 0; p < NKT / 2; ++p)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f16x8 ph, phs, pl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float pv = sc[2 * p + (j >> 2)][qt][j & 3];
+          const _Float16 h = (_Float16)pv;
+          const _Float16 hs = h * (_Float16)kLoScale;
+          ph[j] = h;
+          phs[j] = hs;
+          pl[j] = (_Float16)fmaf(pv, kLoScale, -(float)hs);
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt][qt] = mfma_h3_16(vf[p][dt][0], vf[p][dt][1], phs, pl, ph, o[dt][qt]);
+      }
+
+    if (t + 1 < ntiles) sstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // context rows into the plane image (K = 256): lane holds dims 16 dt + 4 g + r of query qt*16+r16
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float l_tot = sum_xor16_32(l_run[qt]);
+    const float inv = ldexpf(1.f / l_tot, -11);
+    const int q = q_blk + wave * 32 + qt * 16 + r16;
+    if (q < Nq) {
+      const int orow = S.o_row0 + b * Nq + q;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          _Float16 a, c;
+          split2h(o[dt][qt][e] * inv, a, c);
+          h[e] = a;
+          l[e] = c;
+        }
+        const size_t off = plane_off(orow, head * kHeadDim + 16 * dt + 4 * g, S.o_rows_pad);
+        *reinterpret_cast<f16x4*>(S.op + off) = h;
+        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+      }
+    }
+  }
+}
+
+template <int KT>
+static hipError_t attention_h3m_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+  constexpr int QB = 256;
+  const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
+  if (nq == 0 || B == 0) return hipSuccess;
+  if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
+  const int nqb = (nq + QB - 1) / QB;
+  const int items = nqb * B * H * 2;
+  hipLaunchKernelGGL((attention_h3m_kernel<KT>), dim3(items), dim3(512), 0, st, s0, s1, B, H, nqb,
+                     scale * 1.4426950408889634f);
+  return hipGetLastError();
+}
+
 }  // namespace lg

@@ -138,6 +138,7 @@ struct lg_handle {
     double flops, bytes;
   };
   bool prof_on = false;
+  unsigned prof_mask = 0;  // bit k: kernel family k is timed
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
   hipEvent_t ev() {
@@ -151,7 +152,7 @@ struct lg_handle {
     return e;
   }
   int prof_begin(int kind, hipStream_t st) {
-    if (!prof_on) return -1;
+    if (!prof_on || !(prof_mask & (1u << kind))) return -1;
     Rec r{ev(), ev(), kind, 0.0, 0.0};
     (void)hipEventRecord(r.a, st);
     recs.push_back(r);
@@ -848,6 +849,8 @@ int lg_profile_enable(lg_handle_t* h, int enable) {
   }
   h->recs.clear();
   h->prof_on = enable != 0;
+  // 1 = every family; otherwise bit (k + 1) selects family k (LG_PROFILE_ONLY(k))
+  h->prof_mask = enable == 1 ? ~0u : ((unsigned)enable >> 1);
   return LG_OK;
 }
 

@@ -307,10 +307,16 @@ class LightGlue(nn.Module):
         }
 
     # ------------------------------------------------------------ profiling (bench.py)
-    def profile_enable(self, enable=True):
+    def profile_enable(self, enable=True, only=None):
+        """Start timing the hot kernel families (all, or only the names in `only`)."""
         if self._handle is None:
             raise RuntimeError("run one forward first (the native handle is created lazily)")
-        _lib.check(_lib.load().lg_profile_enable(self._handle, int(enable)), "lg_profile_enable")
+        code = int(bool(enable))
+        if enable and only:
+            code = 0
+            for k in only:
+                code |= 1 << (_lib.KERNEL_IDS[k] + 1)
+        _lib.check(_lib.load().lg_profile_enable(self._handle, code), "lg_profile_enable")
 
     def profile_read(self, kernel):
         """(total_ms, launches, algorithmic_flops, algorithmic_bytes) since profile_enable()."""

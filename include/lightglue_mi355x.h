@@ -128,6 +128,9 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
  * the ALGORITHMIC flops / bytes of each launch.  lg_profile_read synchronises on the recorded
  * events and returns totals since the last lg_profile_enable(h, 1). */
 enum { LG_KERNEL_ATTENTION = 0, LG_KERNEL_GEMM = 1, LG_KERNEL_ASSIGN = 2, LG_KERNEL_COUNT = 3 };
+/* enable: 0 = off, 1 = every family, or an OR of LG_PROFILE_ONLY(k) to time only those families
+ * (fewer events inside a timed region). */
+#define LG_PROFILE_ONLY(k) (1 << ((k) + 1))
 int lg_profile_enable(lg_handle_t* h, int enable);
 int lg_profile_read(lg_handle_t* h, int kernel, double* total_ms, int64_t* launches, double* flops,
                     double* bytes);

@@ -198,3 +198,25 @@ def test_filter_matches_matches_oracle():
         # exp() of the same fp32 value: GPU expf vs torch-CPU differ by <= 1 ulp
         np.testing.assert_allclose(got[2].cpu().numpy(), ref[2].numpy(), rtol=3e-7, atol=0)
         np.testing.assert_allclose(got[3].cpu().numpy(), ref[3].numpy(), rtol=3e-7, atol=0)
+
+
+def test_profile_family_mask():
+    """lg_profile_enable: 1 times every family; LG_PROFILE_ONLY(k) masks time only family k."""
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1}
+    m = _model(conf, synthetic_state_dict(conf, seed=0))
+    d = _gpu_data(synthetic_pair(B=1, M=128, N=96, seed=3))
+    with torch.no_grad():
+        m(d)
+        m.profile_enable(True, only=("attention",))
+        m(d)
+        att = m.profile_read("attention")
+        gem = m.profile_read("gemm")
+        m.profile_enable(True)
+        m(d)
+        gem_all = m.profile_read("gemm")
+        m.profile_enable(False)
+    assert att[1] == 2 * 9 and att[0] > 0  # self + cross per layer
+    assert gem[1] == 0
+    assert gem_all[1] > 0 and gem_all[2] > 0

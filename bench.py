@@ -36,7 +36,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
 # or six bf16 ones (bf16x6, the guarded fallback), so their fp32-equivalent matrix
 # peak is the fp16/bf16 dense peak / 3 (or / 6).
 PEAKS = {
-    "fp16x3": (BF16_MFMA_PEAK_TFLOPS / 3.0, "lg::attention_h3f_kernel",
+    "fp16x3": (BF16_MFMA_PEAK_TFLOPS / 3.0, "lg::attention_h3g_kernel",
                "fp32-equivalent: fp16 dense 2500 TF/s / 3 fp16 products per fp32 product (fp32 MFMA peak is 157.3)"),
     "bf16x6": (BF16_MFMA_PEAK_TFLOPS / 6.0, "lg::attention_x6_kernel",
                "fp32-equivalent: bf16 dense 2500 TF/s / 6 bf16 products per fp32 product (fp32 MFMA peak is 157.3)"),

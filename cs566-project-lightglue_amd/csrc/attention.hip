@@ -548,8 +548,8 @@ static hipError_t attention_h3_launch(const AttnSet& s0, const AttnSet& s1, int 
 
 
 // ----------------------------------------------------------------------------------------
-// attention_h3f_kernel (PREC_H3, the production fp16x3 attention): 8 waves x 32 queries, 64-key
-// K/V tiles double-buffered in LDS (one barrier per tile), lazy softmax reference, context
+// fp16x3 attention (PREC_H3; attention_h3f/h3g kernels): 8 waves x 32 queries, 64-key
+// K/V softmax steps, tiles double-buffered in LDS, lazy softmax reference, context
 // straight into ffn.0's plane image, all products on v_mfma_f32_16x16x32_f16 (16 x 16 tiles run
 // at ~1.15x the rate of 32 x 32 tiles on random data, tools/probe_mfma_shape.hip):
 //   S^T[key][query] = K Q^T:  A = K tile (16 keys x 32 dims, lane: key l&15, dims 8(l>>4)..),
@@ -594,15 +594,24 @@ __device__ __forceinline__ float sum_x16_32(float v) {
   return sum_xor32(__uint_as_float(r[0]) + __uint_as_float(r[1]));
 }
 
-template <int KT>
-__global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+
+// attention_h3g_kernel: the production kernel of the design above.  K/V tiles are staged by
+// LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write; the swizzle is applied by
+// the per-lane source offsets), SUBS 64-key softmax steps per LDS tile, i.e. per barrier
+// (SUBS = 2: 2 x 64 KiB of LDS), and PRIO raises the second-dispatched half of the waves to
+// s_setprio 1 once.  tools/kbench_attn.hip: 862 us vs 907-918 us for the register-staged
+// attention_h3f_kernel (tools/attn_experiments.hip) at the bench shape.
+template <int SUBS, int PRIO>
+__global__ __launch_bounds__(512, 2) void attention_h3g_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
                                                                 float scale_log2e) {
-  constexpr int WAVES = 8, NT = 64 * WAVES, QB = 32 * WAVES;
+  constexpr int WAVES = 8, QB = 32 * WAVES;
+  constexpr int KT = 64;                   // keys per sub-tile (one softmax step)
+  constexpr int LT = KT * SUBS;            // keys per LDS tile (one barrier)
   constexpr int NKT = KT / 16;
-  constexpr int CH = 2 * KT * 8;
-  constexpr int LDC = CH / NT;
-  constexpr int PL = KT * kHeadDim;
-  static_assert(CH % NT == 0 && KT == 64, "tile/threads mismatch");
+  constexpr int PL = LT * kHeadDim;        // one plane of an LDS tile (elements)
+  constexpr int PIECES = 4 * LT / 8;       // 1 KiB LDS-DMA pieces per tile (K h/l, V h/l; 8 rows each)
+  constexpr int PPW = PIECES / WAVES;
+  static_assert(PIECES % WAVES == 0, "pieces per wave");
   __shared__ __attribute__((aligned(16))) _Float16 Ks[2 * 2 * PL];
   __shared__ __attribute__((aligned(16))) _Float16 Vs[2 * 2 * PL];
 
@@ -621,7 +630,7 @@ __global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnS
   const int head = bh % H;
   const int b = bh / H;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
 
   f16x8 qh[2][2], qhs[2][2], ql[2][2];
@@ -659,24 +668,23 @@ __global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnS
       }
   }
 
-  f32x4 rk[LDC], rv[LDC];
-  auto gload = [&](int t0) {
+  // LDS-DMA staging of one LDS tile (keys t0 .. t0+LT-1) into buffer buf: piece q (wave-uniform)
+  // = 8 rows of one plane of K (q < PIECES/2) or V; lane i fills LDS slot (row i>>3, chunk i&7)
+  // with the source chunk that the swizzle puts there (rows past Nk repeat row Nk-1)
+  const uint32_t ks_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)Ks);
+  const uint32_t vs_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)Vs);
+  auto issue = [&](int t0, int buf) {
 #pragma unroll
-    for (int i = 0; i < LDC; ++i) {
-      const int c = tid + i * NT;
-      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
-      const size_t src = (size_t)p * ps + (size_t)min(t0 + r, Nk - 1) * kHeadDim + cb * 8;
-      rk[i] = *reinterpret_cast<const f32x4*>(Kp + src);
-      rv[i] = *reinterpret_cast<const f32x4*>(Vp + src);
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < LDC; ++i) {
-      const int c = tid + i * NT;
-      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
-      *reinterpret_cast<f32x4*>(&Ks[(buf * 2 + p) * PL + r * kHeadDim + ((cb ^ ((r >> 1) & 7)) * 8)]) = rk[i];
-      *reinterpret_cast<f32x4*>(&Vs[(buf * 2 + p) * PL + r * kHeadDim + ((cb ^ (((r >> 1) & 3) << 1)) * 8)]) = rv[i];
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;
+      const bool isv = q >= PIECES / 2;
+      const int qq = isv ? q - PIECES / 2 : q;
+      const int pl = qq / (LT / 8), r = (qq % (LT / 8)) * 8 + (lane >> 3), cs = lane & 7;
+      const int c = isv ? cs ^ (((r >> 1) & 3) << 1) : cs ^ ((r >> 1) & 7);
+      const _Float16* base = (isv ? Vp : Kp) + (size_t)pl * ps + (size_t)t0 * kHeadDim;
+      const uint32_t voff = (uint32_t)((min(t0 + r, Nk - 1) - t0) * kHeadDim + c * 8) * 2u;
+      const uint32_t dst = (isv ? vs_lds : ks_lds) + (uint32_t)(((buf * 2 + pl) * PL + (qq % (LT / 8)) * 8 * kHeadDim) * 2);
+      dma16(base, voff, dst);
     }
   };
 
@@ -684,9 +692,6 @@ __global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnS
   const int vq = (lane & 15) >> 2, vp4 = lane & 3;
   const int vrow = 4 * g + vq;
   const int vswz = ((vrow >> 1) & 3) << 1;
-  // per-lane LDS bases; everything else in a tile's reads is a compile-time offset
-  const _Float16* kbase = Ks + r16 * kHeadDim;
-  const _Float16* vbase = Vs + vrow * kHeadDim + 4 * (vp4 & 1);
   int kcol[2], vcol[4];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) kcol[ks] = ((4 * ks + g) ^ kswz) << 3;
@@ -698,14 +703,15 @@ __global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnS
   for (int dt = 0; dt < 4; ++dt) o[dt][0] = o[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_use[2] = {-INFINITY, -INFINITY};
   float l_run[2] = {0.f, 0.f};
-  const int ntiles = (Nk + KT - 1) / KT;
 
-  auto body = [&](auto BUFc, auto MASKc, int t) {
-    constexpr int buf = decltype(BUFc)::value;
+  // one 64-key softmax step over LDS rows off .. off+63 of the current buffer (off: element
+  // offset buf*2*PL + sub*KT*kHeadDim, a compile-time constant in the main loop)
+  auto body = [&](auto OFFc, auto MASKc, int t0) {
+    const int off = OFFc;
     constexpr bool MASK = decltype(MASKc)::value;
-    const int t0 = t * KT;
-    const _Float16* Kc = kbase + buf * 2 * PL;
-    const _Float16* Vc = vbase + buf * 2 * PL;
+    // from the __shared__ arrays themselves (not captured pointers), so the reads stay ds_read
+    const _Float16* Kc = Ks + r16 * kHeadDim + off;
+    const _Float16* Vc = Vs + vrow * kHeadDim + 4 * (vp4 & 1) + off;
 
     f16x8 kf[NKT][2][2];
 #pragma unroll
@@ -717,7 +723,6 @@ __global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnS
         kf[kt][ks][1] = *reinterpret_cast<const f16x8*>(Kc + PL + off);
       }
     asm volatile("" ::: "memory");
-    if (t + 1 < ntiles) gload(t0 + KT);
     f32x4 sc[NKT][2];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
@@ -801,29 +806,44 @@ __global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnS
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[dt][qt] = mfma_h3_16(vf[p][dt][0], vf[p][dt][1], phs, pl, ph, o[dt][qt]);
       }
-
-    if (t + 1 < ntiles) sstore(buf ^ 1);
-    __syncthreads();
   };
 
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  using B0 = std::integral_constant<int, 0>;
-  using B1 = std::integral_constant<int, 1>;
   using NoMask = std::integral_constant<bool, false>;
   using Mask = std::integral_constant<bool, true>;
-  const int nfull = Nk / KT;
+  const int nlt = (Nk + LT - 1) / LT;
+  const int nfull = Nk / LT;  // LDS tiles without a ragged end
+  using IC0 = std::integral_constant<int, 0>;
+  using IC1 = std::integral_constant<int, KT * kHeadDim>;
+  using IC2 = std::integral_constant<int, 2 * PL>;
+  using IC3 = std::integral_constant<int, 2 * PL + KT * kHeadDim>;
+  static_assert(SUBS == 1 || SUBS == 2, "sub-tiles per LDS tile");
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   int t = 0;
   for (; t + 2 <= nfull; t += 2) {
-    body(B0{}, NoMask{}, t);
-    body(B1{}, NoMask{}, t + 1);
+    if (t + 1 < nlt) issue((t + 1) * LT, 1);  // buffer 1 was released by the last barrier
+    body(IC0{}, NoMask{}, t * LT);
+    if constexpr (SUBS == 2) body(IC1{}, NoMask{}, t * LT + KT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 2 < nlt) issue((t + 2) * LT, 0);
+    body(IC2{}, NoMask{}, (t + 1) * LT);
+    if constexpr (SUBS == 2) body(IC3{}, NoMask{}, (t + 1) * LT + KT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  if (t < nfull) {
-    body(B0{}, NoMask{}, t);
-    if (t + 1 < ntiles) body(B1{}, Mask{}, t + 1);
-  } else if (t < ntiles) {
-    body(B0{}, Mask{}, t);
+  for (; t < nlt; ++t) {  // at most two LDS tiles: masked steps, runtime buffer
+    const int buf = t & 1;
+    if (t + 1 < nlt) issue((t + 1) * LT, buf ^ 1);
+    for (int sub = 0; sub < SUBS; ++sub) {
+      const int s0 = t * LT + sub * KT;
+      if (s0 < Nk) body(buf * 2 * PL + sub * KT * kHeadDim, Mask{}, s0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 
   // context rows into the plane image: o = 2^11 sum(v p) (the MFMA scale), l_run = 2^11 sum(p),
@@ -853,15 +873,15 @@ __global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnS
   }
 }
 
-template <int KT>
-static hipError_t attention_h3f_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+template <int SUBS, int PRIO = 0>
+static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
   constexpr int QB = 256;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
   if (nq == 0 || B == 0) return hipSuccess;
   if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
   const int nqb = (nq + QB - 1) / QB;
   const int items = nqb * B * H * 2;
-  hipLaunchKernelGGL((attention_h3f_kernel<KT>), dim3(items), dim3(512), 0, st, s0, s1, B, H, nqb,
+  hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO>), dim3(items), dim3(512), 0, st, s0, s1, B, H, nqb,
                      scale * 1.4426950408889634f);
   return hipGetLastError();
 }
@@ -894,7 +914,7 @@ hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, flo
 #ifdef LG_ATTN_H3_LEGACY
     return attention_h3_launch<LG_ATTN_H3_CONFIG>(s0, s1, B, H, scale, st);
 #else
-    return attention_h3f_launch<64>(s0, s1, B, H, scale, st);
+    return attention_h3g_launch<2, 1>(s0, s1, B, H, scale, st);
 #endif
   }
   return attention_x6_launch<LG_ATTN_CONFIG>(s0, s1, B, H, scale, st);

@@ -1253,4 +1253,278 @@ static hipError_t attention_h3m_launch(const AttnSet& s0, const AttnSet& s1, int
   return hipGetLastError();
 }
 
+// attention_h3f_kernel -- measured, superseded by attention_h3g_kernel: the same math with K/V
+// staged through registers (global_load -> ds_write) and one 64-key tile per barrier.
+template <int KT>
+__global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+                                                                float scale_log2e) {
+  constexpr int WAVES = 8, NT = 64 * WAVES, QB = 32 * WAVES;
+  constexpr int NKT = KT / 16;
+  constexpr int CH = 2 * KT * 8;
+  constexpr int LDC = CH / NT;
+  constexpr int PL = KT * kHeadDim;
+  static_assert(CH % NT == 0 && KT == 64, "tile/threads mismatch");
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[2 * 2 * PL];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[2 * 2 * PL];
+
+  const int item = xcd_chunk(blockIdx.x, gridDim.x);
+  const int qb = item % nqb;
+  const int sbh = item / nqb;
+  const int set = sbh / (B * H), bh = sbh - set * (B * H);
+  const AttnSet& S = set == 0 ? s0 : s1;
+  const int q_blk = qb * QB;
+  if (q_blk >= S.Nq) return;
+  const int Nq = S.Nq, Nk = S.Nk;
+  const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
+  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
+  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
+  const long long ps = S.pstride;
+  const int head = bh % H;
+  const int b = bh / H;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+
+  f16x8 qh[2][2], qhs[2][2], ql[2][2];
+  float c_lane[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qrow = min(q_blk + wave * 32 + qt * 16 + r16, Nq - 1);
+    const float* qr = Q + (size_t)qrow * kHeadDim + 8 * g;
+    f32x4 x[2][2];
+    float mx = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      x[ks][0] = *reinterpret_cast<const f32x4*>(qr + 32 * ks);
+      x[ks][1] = *reinterpret_cast<const f32x4*>(qr + 32 * ks + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[ks][0][e]), fabsf(x[ks][1][e])));
+    }
+    mx = max_x16_32(mx);
+    int ex = 0;
+    if (mx > 0.f && mx <= 3.0e38f) {
+      int E;
+      (void)frexpf(mx, &E);
+      ex = min(max(4 - E, -100), 100);
+    }
+    c_lane[qt] = ldexpf(scale_log2e, -(11 + ex));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 h, l;
+        split2h(ldexpf(x[ks][e >> 2][e & 3], ex), h, l);
+        qh[qt][ks][e] = h;
+        ql[qt][ks][e] = l;
+        qhs[qt][ks][e] = h * (_Float16)kLoScale;
+      }
+  }
+
+  f32x4 rk[LDC], rv[LDC];
+  auto gload = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < LDC; ++i) {
+      const int c = tid + i * NT;
+      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
+      const size_t src = (size_t)p * ps + (size_t)min(t0 + r, Nk - 1) * kHeadDim + cb * 8;
+      rk[i] = *reinterpret_cast<const f32x4*>(Kp + src);
+      rv[i] = *reinterpret_cast<const f32x4*>(Vp + src);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LDC; ++i) {
+      const int c = tid + i * NT;
+      const int p = c / (KT * 8), r = (c / 8) % KT, cb = c % 8;
+      *reinterpret_cast<f32x4*>(&Ks[(buf * 2 + p) * PL + r * kHeadDim + ((cb ^ ((r >> 1) & 7)) * 8)]) = rk[i];
+      *reinterpret_cast<f32x4*>(&Vs[(buf * 2 + p) * PL + r * kHeadDim + ((cb ^ (((r >> 1) & 3) << 1)) * 8)]) = rv[i];
+    }
+  };
+
+  const int kswz = (r16 >> 1) & 7;
+  const int vq = (lane & 15) >> 2, vp4 = lane & 3;
+  const int vrow = 4 * g + vq;
+  const int vswz = ((vrow >> 1) & 3) << 1;
+  // per-lane LDS bases; everything else in a tile's reads is a compile-time offset
+  const _Float16* kbase = Ks + r16 * kHeadDim;
+  const _Float16* vbase = Vs + vrow * kHeadDim + 4 * (vp4 & 1);
+  int kcol[2], vcol[4];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) kcol[ks] = ((4 * ks + g) ^ kswz) << 3;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) vcol[dt] = ((2 * dt + (vp4 >> 1)) ^ vswz) << 3;
+
+  f32x4 o[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt][0] = o[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_use[2] = {-INFINITY, -INFINITY};
+  float l_run[2] = {0.f, 0.f};
+  const int ntiles = (Nk + KT - 1) / KT;
+
+  auto body = [&](auto BUFc, auto MASKc, int t) {
+    constexpr int buf = decltype(BUFc)::value;
+    constexpr bool MASK = decltype(MASKc)::value;
+    const int t0 = t * KT;
+    const _Float16* Kc = kbase + buf * 2 * PL;
+    const _Float16* Vc = vbase + buf * 2 * PL;
+
+    f16x8 kf[NKT][2][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int off = kt * 16 * kHeadDim + kcol[ks];
+        kf[kt][ks][0] = *reinterpret_cast<const f16x8*>(Kc + off);
+        kf[kt][ks][1] = *reinterpret_cast<const f16x8*>(Kc + PL + off);
+      }
+    asm volatile("" ::: "memory");
+    if (t + 1 < ntiles) gload(t0 + KT);
+    f32x4 sc[NKT][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) a = mfma_h3_16(kf[kt][ks][0], kf[kt][ks][1], qhs[qt][ks], ql[qt][ks], qh[qt][ks], a);
+        sc[kt][qt] = a;
+      }
+    f16x8 vf[NKT / 2][4][2];
+#pragma unroll
+    for (int p = 0; p < NKT / 2; ++p)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          const f16x4 lo = tr_read_h(Vc + pl * PL + (32 * p) * kHeadDim + vcol[dt]);
+          const f16x4 hi = tr_read_h(Vc + pl * PL + (32 * p + 16) * kHeadDim + vcol[dt]);
+          vf[p][dt][pl] = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      if constexpr (MASK) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t0 + 16 * kt + 4 * g + r >= Nk) sc[kt][qt][r] = -INFINITY;
+      }
+      const float m0 = max3f(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
+      const float m1 = max3f(sc[0][qt][3], sc[1][qt][0], sc[1][qt][1]);
+      const float m2 = max3f(sc[1][qt][2], sc[1][qt][3], sc[2][qt][0]);
+      const float m3 = max3f(sc[2][qt][1], sc[2][qt][2], sc[2][qt][3]);
+      const float m4 = max3f(sc[3][qt][0], sc[3][qt][1], sc[3][qt][2]);
+      const float lmax = fmaxf(max3f(m0, m1, m2), max3f(m3, m4, sc[3][qt][3]));
+      // the lane-local max decides whether any query can need a raise; only then are the four
+      // lanes of each query reduced (the raise itself is per query, exactly as in h3/h3m)
+      if (__ballot((lmax - m_use[qt]) * c_lane[qt] > 3.f) != 0ull) {
+        const float tmax = max_x16_32(lmax);
+        const bool need = (tmax - m_use[qt]) * c_lane[qt] > 3.f;
+        const float m_new = need ? tmax : m_use[qt];
+        const float alpha = __builtin_amdgcn_exp2f((m_use[qt] - m_new) * c_lane[qt]);
+        m_use[qt] = m_new;
+        l_run[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[dt][qt][r] *= alpha;
+      }
+      // e = p 2^11
+      const float mb = fmaf(m_use[qt], c_lane[qt], -11.f);
+      float ps4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][qt][r], c_lane[qt], -mb));
+          sc[kt][qt][r] = e;
+          ps4[r] += e;
+        }
+      l_run[qt] += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
+    }
+#pragma unroll
+    for (int p = 0; p < NKT / 2; ++p)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f16x8 ph, phs, pl;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const float e0 = sc[2 * p + (j >> 2)][qt][j & 3];
+          const float e1 = sc[2 * p + (j >> 2)][qt][(j & 3) + 1];
+          const f16x2 hs = {(_Float16)e0, (_Float16)e1};
+          const f16x2 h = hs * (f16x2){(_Float16)(1.f / kLoScale), (_Float16)(1.f / kLoScale)};
+          const f16x2 lo = lo_pair(e0, e1, hs);
+          phs[j] = hs[0]; phs[j + 1] = hs[1];
+          ph[j] = h[0]; ph[j + 1] = h[1];
+          pl[j] = lo[0]; pl[j + 1] = lo[1];
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt][qt] = mfma_h3_16(vf[p][dt][0], vf[p][dt][1], phs, pl, ph, o[dt][qt]);
+      }
+
+    if (t + 1 < ntiles) sstore(buf ^ 1);
+    __syncthreads();
+  };
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using NoMask = std::integral_constant<bool, false>;
+  using Mask = std::integral_constant<bool, true>;
+  const int nfull = Nk / KT;
+  int t = 0;
+  for (; t + 2 <= nfull; t += 2) {
+    body(B0{}, NoMask{}, t);
+    body(B1{}, NoMask{}, t + 1);
+  }
+  if (t < nfull) {
+    body(B0{}, NoMask{}, t);
+    if (t + 1 < ntiles) body(B1{}, Mask{}, t + 1);
+  } else if (t < ntiles) {
+    body(B0{}, Mask{}, t);
+  }
+
+  // context rows into the plane image: o = 2^11 sum(v p) (the MFMA scale), l_run = 2^11 sum(p),
+  // so 1 / l_run is the old 2^-11 / l exactly
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float l_tot = sum_x16_32(l_run[qt]);
+    const float inv = 1.f / l_tot;
+    const int q = q_blk + wave * 32 + qt * 16 + r16;
+    if (q < Nq) {
+      const int orow = S.o_row0 + b * Nq + q;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          _Float16 a, c;
+          split2h(o[dt][qt][e] * inv, a, c);
+          h[e] = a;
+          l[e] = c;
+        }
+        const size_t off = plane_off(orow, head * kHeadDim + 16 * dt + 4 * g, S.o_rows_pad);
+        *reinterpret_cast<f16x4*>(S.op + off) = h;
+        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+      }
+    }
+  }
+}
+
+template <int KT>
+static hipError_t attention_h3f_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+  constexpr int QB = 256;
+  const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
+  if (nq == 0 || B == 0) return hipSuccess;
+  if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
+  const int nqb = (nq + QB - 1) / QB;
+  const int items = nqb * B * H * 2;
+  hipLaunchKernelGGL((attention_h3f_kernel<KT>), dim3(items), dim3(512), 0, st, s0, s1, B, H, nqb,
+                     scale * 1.4426950408889634f);
+  return hipGetLastError();
+}
+
 }  // namespace lg

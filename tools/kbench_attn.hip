@@ -136,6 +136,10 @@ int main(int argc, char** argv) {
   run("h3s staggered", [&] { return attention_h3s_launch<64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3m 16x16x32", [&] { return attention_h3m_launch<64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3f lean softmax", [&] { return attention_h3f_launch<64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3g dma sub2", [&] { return attention_h3g_launch<2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3g dma sub1", [&] { return attention_h3g_launch<1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3g dma sub1 prio", [&] { return attention_h3g_launch<1, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3g dma sub2 prio", [&] { return attention_h3g_launch<2, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3 DIAG1 no softmax", [&] { return attention_h3_launch<8, 64, 2, 1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3 DIAG2 no mfma", [&] { return attention_h3_launch<8, 64, 2, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3 DIAG3 mfma only", [&] { return attention_h3_launch<8, 64, 2, 3>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);

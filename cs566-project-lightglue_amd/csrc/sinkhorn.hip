@@ -5,10 +5,19 @@
 //   iters x { u = log_mu - LSE_j(Zc + v);  v = log_nu - LSE_i(Zc + u) }
 //   out = Zc + u + v + log(M+N)
 //
-// Both half-steps are row reductions: the u-step walks rows of `scores`, the v-step walks rows
-// of a transposed copy made once (tiled LDS transpose), so every pass is a coalesced stream.
-// One wave per row; the two-pass max-then-sum LSE mirrors torch.logsumexp's formulation.
-// HBM/Infinity-Cache bound: per iteration 2 x B*M*N*4 bytes are read.
+// Fused path (N <= 4096, the configs[4] shape): ONE read of the scores per iteration.  A wave
+// holds a whole row in registers (lane: columns 256k + 4 lane + e), so the u-step's LSE_j is the
+// two-pass max-then-sum of torch.logsumexp without a second read; with u_i known, the same
+// registers feed the v-step's column statistics Z_ij + u_i as running (max, sum) pairs per
+// column.  The 8 waves of a workgroup (consecutive row runs of one pair) merge their column
+// pairs through LDS, one partial per workgroup goes to HBM, and sinkhorn_colmerge_kernel turns
+// the partials into v (LSE_i = M + log sum_p s_p e^(m_p - M)).  Order per iteration as in the
+// reference: u from the previous v, then v from the new u.
+// HBM bound: B*M*N*4 bytes read per iteration (+ partials, ~3%).
+// General path (N > 4096): the u-step walks rows of `scores`, the v-step walks rows of a
+// transposed copy made once (tiled LDS transpose); one wave per row, two-pass max-then-sum.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -73,26 +82,272 @@ __global__ void sinkhorn_out_kernel(const float* scores, const float* u, const f
   Z[t] = ((z + u[b * (M + 1) + i]) + v[b * (N + 1) + j]) - norm;
 }
 
+
+// ---------------------------------------------------------------- fused path (N <= 4096)
+namespace {
+constexpr int kSkMaxN = 4096;               // real columns held in registers (16 float4 per lane)
+constexpr int kSkTargetWG = 256;            // ~one workgroup per CU
+
+__host__ __device__ constexpr int sk_waves(int k4) { return k4 >= 16 ? 4 : 8; }  // waves per workgroup
+
+struct SkPlan {
+  int rw;  // rows per wave
+  int p;   // workgroups (partials) per pair
+};
+
+SkPlan sk_plan(int B, int M, int N) {
+  const int w = sk_waves((N + 255) / 256);
+  const int rows = M + 1;
+  int p = (kSkTargetWG + B - 1) / B;
+  p = std::max(1, std::min(p, (rows + w - 1) / w));
+  const int rb = (rows + p - 1) / p;
+  const int rw = (rb + w - 1) / w;
+  return {rw, (rows + w * rw - 1) / (w * rw)};
+}
+
+bool sk_fused_ok(int M, int N) { return M > 0 && N > 0 && N <= kSkMaxN; }
+
+// merge running (max, sum) pair b into a: sum of e^(x - max) over the union
+__device__ __forceinline__ void lse_merge(float& am, float& as, float bm, float bs) {
+  const float m = fmaxf(am, bm);
+  const float ea = am == m ? 1.f : __expf(am - m);
+  const float eb = bm == m ? 1.f : __expf(bm - m);
+  as = as * ea + bs * eb;
+  am = m;
+}
+}  // namespace
+
+// One iteration: u <- log_mu - LSE_j(Zc + v) for the workgroup's rows, then this workgroup's
+// column partials of Zc + u.  K4 = float4 column chunks per lane (columns 256k + 4 lane + e);
+// VEC: rows are 16-byte aligned (N % 4 == 0).
+template <int K4, bool VEC, int W, bool PF = false>
+__global__ __launch_bounds__(W * 64) void sinkhorn_fused_kernel(const float* __restrict__ scores,
+                                                                       const float* __restrict__ v, float* u,
+                                                                       float2* part, int M, int N, int rw, int P,
+                                                                       float alpha, float lm_in, float lm_bin) {
+  __shared__ float2 mbuf[W / 2][kSkMaxN + 1]; // wave-pair merge buffers
+  __shared__ float4 vs[kSkMaxN / 4 + 1];      // v of the real columns
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x / P, p = blockIdx.x - b * P;
+  const float* vb = v + (size_t)b * (N + 1);
+  for (int j = tid; j < 4 * (kSkMaxN / 4 + 1); j += W * 64)  // finite past N: masked columns stay -inf
+    reinterpret_cast<float*>(vs)[j] = j < N ? vb[j] : 0.f;
+  const float vbin = vb[N];
+  __syncthreads();
+
+  float cm[K4][4], cs[K4][4];
+#pragma unroll
+  for (int k = 0; k < K4; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cm[k][e] = -INFINITY, cs[k][e] = 0.f;
+  float bm = -INFINITY, bs = 0.f;  // bin column (same in every lane)
+
+  const int r0 = (p * W + wave) * rw;
+  const int r1 = min(r0 + rw, M + 1);
+  // row i -> registers (masked columns -inf; the dustbin row is alpha)
+  auto load_row = [&](int i, float (&x)[K4][4]) {
+    const bool bin_row = i == M;
+    const float* row = scores + ((size_t)b * M + i) * N;
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const int c = 256 * k + 4 * lane;
+      if (bin_row) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] = c + e < N ? alpha : -INFINITY;
+      } else if (VEC) {
+        const f32x4 t = c < N ? *reinterpret_cast<const f32x4*>(row + c) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] = t[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] = c + e < N ? row[c + e] : -INFINITY;
+      }
+    }
+  };
+  float x[K4][4];
+  if (r0 < r1) load_row(r0, x);
+  for (int i = r0; i < r1; ++i) {
+    // PF: next row in flight while this one is reduced (measured slower: 10.9 vs 9.3 ms at
+    // configs[4] -- the kernel is VALU-bound and the row copy costs 64 moves)
+    float xn[K4][4];
+    if (PF && i + 1 < r1) load_row(i + 1, xn);
+    const bool bin_row = i == M;
+    // u_i = log_mu_i - LSE_j(Zc_ij + v_j)   (superglue.py:178)
+    // (Zc + v recomputed in the sum pass from LDS rather than held: registers go to x and the
+    // column statistics)
+    auto yv = [&](int k) {
+      const float4 vv = vs[min(64 * k + lane, kSkMaxN / 4)];
+      return f32x4{x[k][0] + vv.x, x[k][1] + vv.y, x[k][2] + vv.z, x[k][3] + vv.w};
+    };
+    float m = alpha + vbin;
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const f32x4 y = yv(k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m = fmaxf(m, y[e]);
+    }
+    m = wave_max(m);
+    asm volatile("" ::: "memory");  // re-read v from LDS below instead of holding Zc + v live
+    float s = lane == 0 ? __expf((alpha + vbin) - m) : 0.f;
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const f32x4 y = yv(k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += __expf(y[e] - m);
+    }
+    s = wave_sum(s);
+    const float lse = m == -INFINITY ? m : m + __logf(s);
+    const float ui = (bin_row ? lm_bin : lm_in) - lse;
+    if (lane == 0) u[(size_t)b * (M + 1) + i] = ui;
+    // column statistics of Zc_ij + u_i (superglue.py:179), one running (max, sum) per column
+#pragma unroll
+    for (int k = 0; k < K4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float z = x[k][e] + ui;
+        const float d = z - cm[k][e];
+        const float t = __expf(-fabsf(d));
+        if (d > 0.f) {
+          cs[k][e] = fmaf(cs[k][e], t, 1.f);
+          cm[k][e] = z;
+        } else {
+          cs[k][e] += t;
+        }
+      }
+    const float zb = alpha + ui;
+    const float db = zb - bm, tb = __expf(-fabsf(db));
+    if (db > 0.f) {
+      bs = fmaf(bs, tb, 1.f);
+      bm = zb;
+    } else {
+      bs += tb;
+    }
+    if (i + 1 < r1) {
+      if constexpr (PF) {
+#pragma unroll
+        for (int k = 0; k < K4; ++k)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[k][e] = xn[k][e];
+      } else {
+        load_row(i + 1, x);
+      }
+    }
+  }
+
+  // merge the W waves pairwise (W/2 -> 0.., ..., 1 -> 0) through LDS
+#pragma unroll
+  for (int half = W / 2; half >= 1; half >>= 1) {
+    if (wave >= half && wave < 2 * half) {
+      float2* dst = mbuf[wave - half];
+#pragma unroll
+      for (int k = 0; k < K4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 256 * k + 4 * lane + e;
+          if (c < N) dst[c] = make_float2(cm[k][e], cs[k][e]);
+        }
+      if (lane == 0) dst[N] = make_float2(bm, bs);
+    }
+    __syncthreads();
+    if (wave < half) {
+      const float2* src = mbuf[wave];
+#pragma unroll
+      for (int k = 0; k < K4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 256 * k + 4 * lane + e;
+          if (c < N) {
+            const float2 o = src[c];
+            lse_merge(cm[k][e], cs[k][e], o.x, o.y);
+          }
+        }
+      const float2 o = src[N];
+      lse_merge(bm, bs, o.x, o.y);
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    float2* dst = part + ((size_t)b * P + p) * (N + 1);
+#pragma unroll
+    for (int k = 0; k < K4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 256 * k + 4 * lane + e;
+        if (c < N) dst[c] = make_float2(cm[k][e], cs[k][e]);
+      }
+    if (lane == 0) dst[N] = make_float2(bm, bs);
+  }
+}
+
+// v_j = log_nu_j - LSE_i(Zc_ij + u_i) from the P workgroup partials of column j
+__global__ void sinkhorn_colmerge_kernel(const float2* part, float* v, int B, int N, int P, float lm_in, float lm_bin) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * (N + 1)) return;
+  const int b = t / (N + 1), j = t - b * (N + 1);
+  const float2* q = part + (size_t)b * P * (N + 1) + j;
+  float m = -INFINITY, s = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const float2 o = q[(size_t)p * (N + 1)];
+    lse_merge(m, s, o.x, o.y);
+  }
+  const float lse = m == -INFINITY ? m : m + logf(s);
+  v[t] = (j == N ? lm_bin : lm_in) - lse;
+}
+
+template <int K4>
+static void launch_fused(const float* scores, const float* v, float* u, float2* part, int B, int M, int N,
+                         const SkPlan& pl, float alpha, float lm_in, float mu_bin, hipStream_t st) {
+  // 16 chunks per lane: a row (64) + column statistics (128) exceed the 256 registers of two
+  // waves per SIMD, so those run 4 waves per workgroup at one wave per SIMD
+  constexpr int W = sk_waves(K4);
+  const dim3 grid(B * pl.p), block(W * 64);
+  if (N % 4 == 0)
+    hipLaunchKernelGGL((sinkhorn_fused_kernel<K4, true, W>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw, pl.p,
+                       alpha, lm_in, mu_bin);
+  else
+    hipLaunchKernelGGL((sinkhorn_fused_kernel<K4, false, W>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw,
+                       pl.p, alpha, lm_in, mu_bin);
+}
+
 size_t sinkhorn_workspace_floats(int B, int M, int N) {
+  if (sk_fused_ok(M, N))  // [u | v | partials (max, sum) B x P x (N+1)]
+    return (size_t)B * (M + 1) + 64 + (size_t)B * (N + 1) + 64 + 2 * (size_t)B * sk_plan(B, M, N).p * (N + 1) + 256;
   return (size_t)B * M * N + (size_t)B * (M + 1) + (size_t)B * (N + 1) + 256;
 }
 
 hipError_t log_optimal_transport(const float* scores, float alpha, int B, int M, int N, int iters, float* Z, float* ws,
                                  hipStream_t st) {
   if (B == 0) return hipSuccess;
-  float* sT = ws;
-  float* u = sT + (size_t)B * M * N;
-  float* v = u + (size_t)B * (M + 1) + 64;
-  hipError_t e;
-  if ((e = hipMemsetAsync(u, 0, sizeof(float) * B * (M + 1), st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(v, 0, sizeof(float) * B * (N + 1), st)) != hipSuccess) return e;
-  if (M > 0 && N > 0)
-    hipLaunchKernelGGL(transpose_kernel, dim3((N + 63) / 64, (M + 63) / 64, B), dim3(256), 0, st, scores, sT, M, N);
   // log_mu / log_nu (superglue.py:194-197), computed in fp32 like the reference
   const float ms = (float)M, ns = (float)N;
   const float norm = -logf(ms + ns);
   const float mu_bin = logf(ns) + norm, nu_bin = logf(ms) + norm;
-  for (int it = 0; it < iters; ++it) {
+  const bool fused = sk_fused_ok(M, N);
+  float* sT = ws;
+  float* u = fused ? ws : sT + (size_t)B * M * N;
+  float* v = u + (size_t)B * (M + 1) + 64;
+  hipError_t e;
+  if ((e = hipMemsetAsync(u, 0, sizeof(float) * B * (M + 1), st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(v, 0, sizeof(float) * B * (N + 1), st)) != hipSuccess) return e;
+  if (fused) {
+    float2* part = reinterpret_cast<float2*>(v + (size_t)B * (N + 1) + 64);
+    const SkPlan pl = sk_plan(B, M, N);
+    const int k4 = (N + 255) / 256;
+    for (int it = 0; it < iters; ++it) {
+      if (k4 <= 1) launch_fused<1>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
+      else if (k4 <= 2) launch_fused<2>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
+      else if (k4 <= 4) launch_fused<4>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
+      else if (k4 <= 8) launch_fused<8>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
+      else launch_fused<16>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
+      hipLaunchKernelGGL(sinkhorn_colmerge_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, part, v, B, N,
+                         pl.p, norm, nu_bin);
+    }
+  } else {
+    if (M > 0 && N > 0)
+      hipLaunchKernelGGL(transpose_kernel, dim3((N + 63) / 64, (M + 63) / 64, B), dim3(256), 0, st, scores, sT, M, N);
+  }
+  for (int it = 0; !fused && it < iters; ++it) {
     hipLaunchKernelGGL(lse_step_kernel, dim3((B * (M + 1) + 3) / 4), dim3(256), 0, st, scores, v, u, B, M, N, alpha, norm,
                        mu_bin);
     hipLaunchKernelGGL(lse_step_kernel, dim3((B * (N + 1) + 3) / 4), dim3(256), 0, st, sT, u, v, B, N, M, alpha, norm,

@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""Per-GPU measurements of the BASELINE.json configs other than the headline one (bench.py).
+
+    python tools/bench_configs.py [--only 1,3,4] [--reps R]
+
+One JSON line per config:
+  configs[1]  N=1024, 9 layers, B=1 (latency-shaped: one pair per forward)
+  configs[3]  N=2048, width/depth pruning on (0.95 / 0.95), B=1 per forward (the reference's pruning
+              is B == 1 only, lightglue.py:528,533); MegaDepth-like 1600x1200 keypoints; the
+              per-GPU share of the 8-GPU work-queue run (parallel.match_dynamic pulls single pairs)
+  configs[4]  N=4096, 8 pairs per GPU (64 over 8 GPUs): the LightGlue forward at N=4096 and the
+              SuperGlue log-domain Sinkhorn (superglue.py:173-201, 50 iterations) on the
+              [8, 4096, 4096] similarity, each timed on its own; Sinkhorn against the HBM roofline
+              (algorithmic bytes = one read of the B*M*N fp32 scores per iteration + the Z write)
+Synthetic inputs and random-init weights as in bench.py; inputs resident in HBM.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import lgamd  # noqa: E402,F401
+from bench import HBM_PEAK_GBS, gpu_pairs  # noqa: E402
+from lightglue_amd import LightGlue, log_optimal_transport  # noqa: E402
+from lightglue_amd.weights import synthetic_state_dict  # noqa: E402
+
+
+def model_for(conf, device):
+    m = LightGlue(conf).eval().to(device)
+    sd = synthetic_state_dict({"filter_threshold": 0.1}, seed=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    return m
+
+
+def timed(fn, reps, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, out
+
+
+def cfg1(dev, reps):
+    m = model_for({"filter_threshold": 0.1}, dev)
+    data = gpu_pairs(1, 1024, 256, seed=1, device=dev)
+    with torch.no_grad():
+        s, pred = timed(lambda: m(data), reps)
+    return {"config": "configs[1]: synthetic N=1024 d=256, 9 layers, batch=1, 1 GPU", "value": round(1 / s, 2),
+            "unit": "image-pairs/s", "ms_per_pair": round(1e3 * s, 3),
+            "matches": int((pred["matches0"] > -1).sum())}
+
+
+def cfg3(dev, reps):
+    conf = {"filter_threshold": 0.1, "width_confidence": 0.95, "depth_confidence": 0.95}
+    m = model_for(conf, dev)
+    P = 16
+    data = gpu_pairs(P, 2048, 256, seed=3, device=dev, size=(1600.0, 1200.0))
+    pairs = [{k: (v[i:i + 1] if torch.is_tensor(v) else {"image_size": v["image_size"][i:i + 1]})
+              for k, v in data.items()} for i in range(P)]
+    layers = []
+
+    def run():
+        layers.clear()
+        for d in pairs:
+            with torch.no_grad():
+                p = m(d)
+            layers.append(int(p["stop_layer"]))
+        return p
+
+    s, _ = timed(run, max(1, reps // 4), warm=1)
+    return {"config": "configs[3]: N=2048 (1600x1200 keypoints), width+depth pruning 0.95, B=1 per forward, "
+                      "per-GPU share of the pair-sharded work queue",
+            "value": round(P / s, 2), "unit": "image-pairs/s per GPU", "ms_per_pair": round(1e3 * s / P, 3),
+            "pairs_in_sample": P, "layers_executed": layers}
+
+
+def cfg4(dev, reps):
+    B, N = 8, 4096
+    m = model_for({"filter_threshold": 0.1}, dev)
+    data = gpu_pairs(B, N, 256, seed=4, device=dev)
+    with torch.no_grad():
+        s_fwd, _ = timed(lambda: m(data), max(1, reps // 2), warm=1)
+    g = torch.Generator(device=dev).manual_seed(5)
+    scores = torch.randn((B, N, N), generator=g, device=dev) * 2.0
+    iters = 50
+    s_sk, Z = timed(lambda: log_optimal_transport(scores, 1.0, iters), reps)
+    # algorithmic bytes: one streamed read of the B*N*N fp32 scores per iteration (both half-steps
+    # from the same read) + the final Z write and its scores read
+    by = float(iters * B * N * N * 4 + B * (N + 1) * (N + 1) * 4 + B * N * N * 4)
+    gbs = by / s_sk / 1e9
+    return {"config": "configs[4]: N=4096 d=256, 8 pairs per GPU (batch 64 over 8 GPUs), Sinkhorn 50 iters",
+            "forward_pairs_per_s": round(B / s_fwd, 2), "forward_ms": round(1e3 * s_fwd, 3),
+            "sinkhorn_ms": round(1e3 * s_sk, 3), "sinkhorn_pairs_per_s": round(B / s_sk, 2),
+            "end_to_end_pairs_per_s": round(B / (s_fwd + s_sk), 2),
+            "sinkhorn_roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                  "algorithmic_bytes": by,
+                                  "note": "scores 537 MB > 256 MB Infinity Cache; >1 means cache reuse"},
+            "Z_finite": bool(torch.isfinite(Z).all())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="1,3,4")
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    fns = {"1": cfg1, "3": cfg3, "4": cfg4}
+    for k in a.only.split(","):
+        print(json.dumps(fns[k](dev, a.reps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

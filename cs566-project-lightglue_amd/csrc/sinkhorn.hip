@@ -70,16 +70,31 @@ __global__ __launch_bounds__(256) void lse_step_kernel(const float* src, const f
   }
 }
 
-__global__ void sinkhorn_out_kernel(const float* scores, const float* u, const float* v, float* Z, int B, int M, int N,
-                                    float alpha, float norm) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t per = (size_t)(M + 1) * (N + 1);
-  if (t >= (size_t)B * per) return;
-  const int b = (int)(t / per);
-  const int rem = (int)(t - (size_t)b * per);
-  const int i = rem / (N + 1), j = rem - i * (N + 1);
-  const float z = (i < M && j < N) ? scores[((size_t)b * M + i) * N + j] : alpha;
-  Z[t] = ((z + u[b * (M + 1) + i]) + v[b * (N + 1) + j]) - norm;
+// out = Zc + u_i + v_j - norm (superglue.py:199-201): one row per blockIdx.x, 4 consecutive
+// columns per thread (16-byte score loads when rows are aligned), no 64-bit index division
+__global__ __launch_bounds__(256) void sinkhorn_out_kernel(const float* scores, const float* u, const float* v,
+                                                           float* Z, int M, int N, float alpha, float norm) {
+  const int r = blockIdx.x;  // b * (M + 1) + i
+  const int b = r / (M + 1), i = r - b * (M + 1);
+  const int j0 = (blockIdx.y * 256 + threadIdx.x) * 4;
+  if (j0 > N) return;
+  const float ui = u[r];
+  const float* vb = v + (size_t)b * (N + 1);
+  float* zr = Z + (size_t)r * (N + 1);
+  float x[4];
+  if (i < M && j0 + 3 < N && (N & 3) == 0) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(scores + ((size_t)b * M + i) * N + j0);
+    x[0] = t[0], x[1] = t[1], x[2] = t[2], x[3] = t[3];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = j0 + e;
+      x[e] = (i < M && j < N) ? scores[((size_t)b * M + i) * N + j] : alpha;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (j0 + e <= N) zr[j0 + e] = ((x[e] + ui) + vb[j0 + e]) - norm;
 }
 
 
@@ -87,16 +102,22 @@ __global__ void sinkhorn_out_kernel(const float* scores, const float* u, const f
 namespace {
 constexpr int kSkMaxN = 4096;               // real columns held in registers (16 float4 per lane)
 constexpr int kSkTargetWG = 256;            // ~one workgroup per CU
+#ifndef LG_SINKHORN_SCALED
+#define LG_SINKHORN_SCALED 1
+#endif
+constexpr bool kSkScaled = LG_SINKHORN_SCALED != 0;  // sinkhorn_scaled_kernel first (exact rerun if flagged)
 
-__host__ __device__ constexpr int sk_waves(int k4) { return k4 >= 16 ? 4 : 8; }  // waves per workgroup
+// waves per workgroup: 8, except the exact kernel at 16 chunks per lane, whose row (64) and
+// running column pairs (128) do not fit the 256 registers of two waves per SIMD
+__host__ __device__ constexpr int sk_waves(int k4, bool exact) { return exact && k4 >= 16 ? 4 : 8; }
 
 struct SkPlan {
   int rw;  // rows per wave
   int p;   // workgroups (partials) per pair
 };
 
-SkPlan sk_plan(int B, int M, int N) {
-  const int w = sk_waves((N + 255) / 256);
+SkPlan sk_plan(int B, int M, int N, bool exact) {
+  const int w = sk_waves((N + 255) / 256, exact);
   const int rows = M + 1;
   int p = (kSkTargetWG + B - 1) / B;
   p = std::max(1, std::min(p, (rows + w - 1) / w));
@@ -167,6 +188,7 @@ __global__ __launch_bounds__(W * 64) void sinkhorn_fused_kernel(const float* __r
   };
   float x[K4][4];
   if (r0 < r1) load_row(r0, x);
+#pragma unroll 1
   for (int i = r0; i < r1; ++i) {
     // PF: next row in flight while this one is reduced (measured slower: 10.9 vs 9.3 ms at
     // configs[4] -- the kernel is VALU-bound and the row copy costs 64 moves)
@@ -295,12 +317,212 @@ __global__ void sinkhorn_colmerge_kernel(const float2* part, float* v, int B, in
   v[t] = (j == N ? lm_bin : lm_in) - lse;
 }
 
+
+// wave-wide max / sum without an LDS round trip: DPP within 16 lanes (quad xor 1, xor 2,
+// half-row mirror, row mirror), then v_permlane16_swap / v_permlane32_swap across rows; every
+// lane ends with bitwise the same value
+template <int C>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return max_xor32(fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return sum_xor32(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+}
+
+// Scaled variant (default): the column statistics reuse the row pass's exponentials.  With
+// e_ij = exp(Zc_ij + v_j - m_i) (m_i the row max, so e_ij <= 1) and a_i = exp(u_i + m_i)
+// = exp(log_mu_i) / s_i <= 1, e_ij * a_i = exp(Zc_ij + u_i + v_j): every row adds into the same
+// per-column frame e^(v_j), so the column statistic is a plain sum S_j = sum_i e_ij a_i (one FMA
+// per element, no second exponential, partials merge by addition) and
+// LSE_i(Zc_ij + u_i) = log S_j - v_j.  Terms below fp32's range are lost where the exact kernel
+// keeps them; the merge flags any column whose S_j falls under 2^-100 and
+// log_optimal_transport then reruns with sinkhorn_fused_kernel (running max per column).
+template <int K4, bool VEC, int W>
+__global__ __launch_bounds__(W * 64) void sinkhorn_scaled_kernel(const float* __restrict__ scores,
+                                                                 const float* __restrict__ v, float* u, float* part,
+                                                                 int M, int N, int rw, int P, float alpha, float lm_in,
+                                                                 float lm_bin) {
+  __shared__ float sbuf[W / 2][kSkMaxN + 1];  // wave-pair merge buffers
+  __shared__ float4 vs[kSkMaxN / 4 + 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x / P, p = blockIdx.x - b * P;
+  const float* vb = v + (size_t)b * (N + 1);
+  for (int j = tid; j < 4 * (kSkMaxN / 4 + 1); j += W * 64) reinterpret_cast<float*>(vs)[j] = j < N ? vb[j] : 0.f;
+  const float vbin = vb[N];
+  const float ybin = alpha + vbin;
+  __syncthreads();
+
+  float acc[K4][4];
+#pragma unroll
+  for (int k = 0; k < K4; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[k][e] = 0.f;
+  float accb = 0.f;
+
+  const int r0 = (p * W + wave) * rw;
+  const int r1 = min(r0 + rw, M + 1);
+  // y: Zc_i row (masked columns -inf) -> Zc + v -> e; accumulates e * a into the column sums
+  auto process = [&](float (&y)[K4][4], int i, bool bin_row) {
+    asm volatile("" ::: "memory");  // re-read v from LDS per row rather than pinning 4*K4 registers
+    float m = ybin;
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const float4 vv = vs[min(64 * k + lane, kSkMaxN / 4)];
+      y[k][0] += vv.x;
+      y[k][1] += vv.y;
+      y[k][2] += vv.z;
+      y[k][3] += vv.w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m = fmaxf(m, y[k][e]);
+    }
+    m = wave_max_dpp(m);
+    const float eb = __expf(ybin - m);
+    float s = lane == 0 ? eb : 0.f;
+#pragma unroll
+    for (int k = 0; k < K4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y[k][e] = __expf(y[k][e] - m);
+        s += y[k][e];
+      }
+    s = wave_sum_dpp(s);
+    const float lm = bin_row ? lm_bin : lm_in;
+    const float ls = __logf(s);
+    const float ui = lm - (m + ls);  // superglue.py:178
+    if (lane == 0) u[(size_t)b * (M + 1) + i] = ui;
+    const float a = __expf(lm - ls);
+#pragma unroll
+    for (int k = 0; k < K4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[k][e] = fmaf(y[k][e], a, acc[k][e]);
+    accb = fmaf(eb, a, accb);
+  };
+  const int rl = min(r1, M);  // real rows; the dustbin row M (all alpha) is handled after
+  auto load = [&](float (&y)[K4][4], int i) {
+    const char* row = reinterpret_cast<const char*>(scores + ((size_t)b * M + i) * N);
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const int c = 256 * k + 4 * lane;
+      if (VEC) {
+        f32x4 t = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        if (c < N) t = *reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[k][e] = t[e];
+      } else {
+        const float* rf = reinterpret_cast<const float*>(row);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[k][e] = c + e < N ? rf[c + e] : -INFINITY;
+      }
+    }
+  };
+  // two row buffers in ping-pong: the next row's loads are in flight while this one is reduced
+  float ya[K4][4], yb[K4][4];
+  if (r0 < rl) load(ya, r0);
+#pragma unroll 1
+  for (int i = r0; i < rl; i += 2) {
+    if (i + 1 < rl) load(yb, i + 1);
+    process(ya, i, false);
+    if (i + 1 >= rl) break;
+    if (i + 2 < rl) load(ya, i + 2);
+    process(yb, i + 1, false);
+  }
+  if (r0 <= M && M < r1) {
+    float y[K4][4];
+#pragma unroll
+    for (int k = 0; k < K4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[k][e] = 256 * k + 4 * lane + e < N ? alpha : -INFINITY;
+    process(y, M, true);
+  }
+
+#pragma unroll
+  for (int half = W / 2; half >= 1; half >>= 1) {
+    if (wave >= half && wave < 2 * half) {
+      float* dst = sbuf[wave - half];
+#pragma unroll
+      for (int k = 0; k < K4; ++k) {
+        const int c = 256 * k + 4 * lane;
+        if (VEC && c < N) {
+          *reinterpret_cast<f32x4*>(dst + c) = f32x4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
+        } else if (!VEC) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < N) dst[c + e] = acc[k][e];
+        }
+      }
+      if (lane == 0) dst[N] = accb;
+    }
+    __syncthreads();
+    if (wave < half) {
+      const float* src = sbuf[wave];
+#pragma unroll
+      for (int k = 0; k < K4; ++k) {
+        const int c = 256 * k + 4 * lane;
+        if (VEC && c < N) {
+          const f32x4 o = *reinterpret_cast<const f32x4*>(src + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[k][e] += o[e];
+        } else if (!VEC) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < N) acc[k][e] += src[c + e];
+        }
+      }
+      accb += src[N];
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    float* dst = part + ((size_t)b * P + p) * (N + 1);
+#pragma unroll
+    for (int k = 0; k < K4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 256 * k + 4 * lane + e;
+        if (c < N) dst[c] = acc[k][e];
+      }
+    if (lane == 0) dst[N] = accb;
+  }
+}
+
+// v_j <- log_nu_j - (log S_j - v_j), S_j = sum of the P partials; flags S_j < 2^-100
+__global__ void sinkhorn_scaled_merge_kernel(const float* part, float* v, int* flag, int B, int N, int P, float lm_in,
+                                             float lm_bin) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  bool low = false;
+  if (t < B * (N + 1)) {
+    const int b = t / (N + 1), j = t - b * (N + 1);
+    const float* q = part + (size_t)b * P * (N + 1) + j;
+    float S = 0.f;
+#pragma unroll 8
+    for (int p = 0; p < P; ++p) S += q[(size_t)p * (N + 1)];
+    low = !(S >= 0x1p-100f);
+    const float lse = logf(S) - v[t];
+    v[t] = (j == N ? lm_bin : lm_in) - lse;
+  }
+  if (__ballot(low) != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
 template <int K4>
 static void launch_fused(const float* scores, const float* v, float* u, float2* part, int B, int M, int N,
                          const SkPlan& pl, float alpha, float lm_in, float mu_bin, hipStream_t st) {
   // 16 chunks per lane: a row (64) + column statistics (128) exceed the 256 registers of two
   // waves per SIMD, so those run 4 waves per workgroup at one wave per SIMD
-  constexpr int W = sk_waves(K4);
+  constexpr int W = sk_waves(K4, true);
   const dim3 grid(B * pl.p), block(W * 64);
   if (N % 4 == 0)
     hipLaunchKernelGGL((sinkhorn_fused_kernel<K4, true, W>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw, pl.p,
@@ -310,9 +532,24 @@ static void launch_fused(const float* scores, const float* v, float* u, float2* 
                        pl.p, alpha, lm_in, mu_bin);
 }
 
+
+template <int K4>
+static void launch_scaled(const float* scores, const float* v, float* u, float* part, int B, int M, int N,
+                          const SkPlan& pl, float alpha, float lm_in, float mu_bin, hipStream_t st) {
+  constexpr int W = sk_waves(K4, false);
+  const dim3 grid(B * pl.p), block(W * 64);
+  if (N % 4 == 0)
+    hipLaunchKernelGGL((sinkhorn_scaled_kernel<K4, true, W>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw, pl.p,
+                       alpha, lm_in, mu_bin);
+  else
+    hipLaunchKernelGGL((sinkhorn_scaled_kernel<K4, false, W>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw,
+                       pl.p, alpha, lm_in, mu_bin);
+}
+
 size_t sinkhorn_workspace_floats(int B, int M, int N) {
   if (sk_fused_ok(M, N))  // [u | v | partials (max, sum) B x P x (N+1)]
-    return (size_t)B * (M + 1) + 64 + (size_t)B * (N + 1) + 64 + 2 * (size_t)B * sk_plan(B, M, N).p * (N + 1) + 256;
+    return (size_t)B * (M + 1) + 64 + (size_t)B * (N + 1) + 64 +
+           2 * (size_t)B * std::max(sk_plan(B, M, N, true).p, sk_plan(B, M, N, false).p) * (N + 1) + 256 + 64;
   return (size_t)B * M * N + (size_t)B * (M + 1) + (size_t)B * (N + 1) + 256;
 }
 
@@ -332,16 +569,38 @@ hipError_t log_optimal_transport(const float* scores, float alpha, int B, int M,
   if ((e = hipMemsetAsync(v, 0, sizeof(float) * B * (N + 1), st)) != hipSuccess) return e;
   if (fused) {
     float2* part = reinterpret_cast<float2*>(v + (size_t)B * (N + 1) + 64);
-    const SkPlan pl = sk_plan(B, M, N);
+    const SkPlan pl = sk_plan(B, M, N, false), ple = sk_plan(B, M, N, true);
+    int* flag = reinterpret_cast<int*>(part + (size_t)B * std::max(pl.p, ple.p) * (N + 1)) + 64;
     const int k4 = (N + 255) / 256;
-    for (int it = 0; it < iters; ++it) {
-      if (k4 <= 1) launch_fused<1>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
-      else if (k4 <= 2) launch_fused<2>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
-      else if (k4 <= 4) launch_fused<4>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
-      else if (k4 <= 8) launch_fused<8>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
-      else launch_fused<16>(scores, v, u, part, B, M, N, pl, alpha, norm, mu_bin, st);
+    int low = 0;
+    if (kSkScaled) {
+      if ((e = hipMemsetAsync(flag, 0, sizeof(int), st)) != hipSuccess) return e;
+      float* fp = reinterpret_cast<float*>(part);
+      for (int it = 0; it < iters; ++it) {
+        if (k4 <= 1) launch_scaled<1>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
+        else if (k4 <= 2) launch_scaled<2>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
+        else if (k4 <= 4) launch_scaled<4>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
+        else if (k4 <= 8) launch_scaled<8>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
+        else launch_scaled<16>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
+        hipLaunchKernelGGL(sinkhorn_scaled_merge_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, fp, v, flag,
+                           B, N, pl.p, norm, nu_bin);
+      }
+      // the flag decides whether the exact kernel reruns: one 4-byte read-back
+      if ((e = hipMemcpyAsync(&low, flag, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+      if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+      if (low) {
+        if ((e = hipMemsetAsync(u, 0, sizeof(float) * B * (M + 1), st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(v, 0, sizeof(float) * B * (N + 1), st)) != hipSuccess) return e;
+      }
+    }
+    for (int it = 0; (!kSkScaled || low) && it < iters; ++it) {
+      if (k4 <= 1) launch_fused<1>(scores, v, u, part, B, M, N, ple, alpha, norm, mu_bin, st);
+      else if (k4 <= 2) launch_fused<2>(scores, v, u, part, B, M, N, ple, alpha, norm, mu_bin, st);
+      else if (k4 <= 4) launch_fused<4>(scores, v, u, part, B, M, N, ple, alpha, norm, mu_bin, st);
+      else if (k4 <= 8) launch_fused<8>(scores, v, u, part, B, M, N, ple, alpha, norm, mu_bin, st);
+      else launch_fused<16>(scores, v, u, part, B, M, N, ple, alpha, norm, mu_bin, st);
       hipLaunchKernelGGL(sinkhorn_colmerge_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, part, v, B, N,
-                         pl.p, norm, nu_bin);
+                         ple.p, norm, nu_bin);
     }
   } else {
     if (M > 0 && N > 0)
@@ -353,9 +612,8 @@ hipError_t log_optimal_transport(const float* scores, float alpha, int B, int M,
     hipLaunchKernelGGL(lse_step_kernel, dim3((B * (N + 1) + 3) / 4), dim3(256), 0, st, sT, u, v, B, N, M, alpha, norm,
                        nu_bin);
   }
-  const size_t tot = (size_t)B * (M + 1) * (N + 1);
-  hipLaunchKernelGGL(sinkhorn_out_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, scores, u, v, Z, B, M, N,
-                     alpha, norm);
+  hipLaunchKernelGGL(sinkhorn_out_kernel, dim3(B * (M + 1), (N + 1 + 1023) / 1024), dim3(256), 0, st, scores, u, v, Z, M,
+                     N, alpha, norm);
   return hipGetLastError();
 }
 

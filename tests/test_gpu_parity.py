@@ -212,6 +212,24 @@ def test_sinkhorn_matches_oracle_shapes(B, M, N, alpha, iters):
     assert torch.equal(inner.max(2).indices[clear], rinner.max(2).indices[clear])
 
 
+@pytest.mark.parametrize("N", [72, 4096])
+def test_sinkhorn_underflow_column_takes_exact_path(N):
+    """A column ~300 below every row's maximum: its exponentials underflow in the scaled
+    one-FMA column statistics, the merge flags it and the exact running-max kernel reruns; the
+    result must still match the oracle."""
+    import oracle
+    from lightglue_amd import log_optimal_transport
+
+    g = torch.Generator().manual_seed(11)
+    scores = torch.randn((2, 50, N), generator=g) * 2.0
+    scores[:, :, 5] = -300.0
+    scores[1, 7, :] = -250.0
+    ref = oracle.log_optimal_transport(scores, 1.0, 20)
+    Z = log_optimal_transport(scores.cuda(), 1.0, 20).cpu()
+    assert torch.isfinite(ref).all()
+    np.testing.assert_allclose(Z.numpy(), ref.numpy(), atol=1e-4, rtol=1e-5)
+
+
 def test_filter_matches_matches_oracle():
     import oracle
     from lightglue_amd import filter_matches

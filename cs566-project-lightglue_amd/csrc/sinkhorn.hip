@@ -70,31 +70,28 @@ __global__ __launch_bounds__(256) void lse_step_kernel(const float* src, const f
   }
 }
 
-// out = Zc + u_i + v_j - norm (superglue.py:199-201): one row per blockIdx.x, 4 consecutive
-// columns per thread (16-byte score loads when rows are aligned), no 64-bit index division
+// out = Zc + u_i + v_j - norm (superglue.py:199-201): one row per blockIdx.x, 1024 columns per
+// blockIdx.y; each load / store instruction covers 256 consecutive columns (coalesced whatever
+// the alignment of the N+1-long output rows)
 __global__ __launch_bounds__(256) void sinkhorn_out_kernel(const float* scores, const float* u, const float* v,
                                                            float* Z, int M, int N, float alpha, float norm) {
   const int r = blockIdx.x;  // b * (M + 1) + i
   const int b = r / (M + 1), i = r - b * (M + 1);
-  const int j0 = (blockIdx.y * 256 + threadIdx.x) * 4;
-  if (j0 > N) return;
   const float ui = u[r];
   const float* vb = v + (size_t)b * (N + 1);
+  const float* sr = scores + ((size_t)b * M + min(i, M - 1)) * N;
   float* zr = Z + (size_t)r * (N + 1);
   float x[4];
-  if (i < M && j0 + 3 < N && (N & 3) == 0) {
-    const f32x4 t = *reinterpret_cast<const f32x4*>(scores + ((size_t)b * M + i) * N + j0);
-    x[0] = t[0], x[1] = t[1], x[2] = t[2], x[3] = t[3];
-  } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int j = j0 + e;
-      x[e] = (i < M && j < N) ? scores[((size_t)b * M + i) * N + j] : alpha;
-    }
+  for (int e = 0; e < 4; ++e) {
+    const int j = blockIdx.y * 1024 + e * 256 + threadIdx.x;
+    x[e] = (i < M && j < N) ? sr[j] : alpha;
   }
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
-    if (j0 + e <= N) zr[j0 + e] = ((x[e] + ui) + vb[j0 + e]) - norm;
+  for (int e = 0; e < 4; ++e) {
+    const int j = blockIdx.y * 1024 + e * 256 + threadIdx.x;
+    if (j <= N) zr[j] = ((x[e] + ui) + vb[j]) - norm;
+  }
 }
 
 

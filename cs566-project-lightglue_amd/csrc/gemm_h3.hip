@@ -26,6 +26,8 @@
 // 256 x 256 x 32 beat 128 x 256 at two workgroups per CU and every k-tile of 16 with 2-4
 // stages).  blockIdx -> tile through a bijective XCD remap so the column tiles of one row panel
 // share an XCD's L2.
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "common.h"
@@ -249,7 +251,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     // ffn.0 + ffn.1 LayerNorm(512, eps 1e-5) + ffn.2 GELU(erf) (lightglue.py:171-176), fused: the
     // workgroup holds complete rows (BN = 512), so the row statistics are reduced in LDS (free
     // after the k-loop) and the activations leave only as the plane image ffn.3 consumes.
-    static_assert(BN == 512 && BM == 128 && WN == 64, "LN epilogue tile");
+    static_assert(BN == 512 && (BM == 128 || BM == 64) && WN == 64, "LN epilogue tile");
     constexpr int NT = NW * 64;
     constexpr int PARTS = NT / BM;            // threads per row in the table reduction
     constexpr int LC = kMF16 ? 16 : 32;       // lanes sharing a row within a wave
@@ -524,12 +526,30 @@ hipError_t gemm_h3_launch(const GemmH3Args& a, int epi, hipStream_t st) {
 #ifndef LG_GEMM_LN_WN
 #define LG_GEMM_LN_WN 64  // wave tile width: 64 -> 16 waves of 64 x 64, 128 -> 8 waves of 64 x 128
 #endif
-// ffn.0 + LayerNorm + GELU (EPI_LN_GELU): 128 x 512 tiles, two 80 KiB stages
-template <int WN>
+// ffn.0 + LayerNorm + GELU (EPI_LN_GELU): 128 x 512 tiles, two 80 KiB stages (BM = 64: 64 x 512
+// tiles, two 72 KiB stages -- small row counts)
+template <int WN, int BM = 128>
 hipError_t gemm_h3_ln_launch(const GemmH3Args& a, hipStream_t st) {
-  const dim3 grid((a.R + 127) / 128), block(2 * (512 / WN) * 64);
-  hipLaunchKernelGGL((gemm_h3_kernel<EPI_LN_GELU, 128, 2, 512, WN>), grid, block, 0, st, a);
+  const dim3 grid((a.R + BM - 1) / BM), block((BM / 64) * (512 / WN) * 64);
+  hipLaunchKernelGGL((gemm_h3_kernel<EPI_LN_GELU, BM, 2, 512, WN>), grid, block, 0, st, a);
   return hipGetLastError();
+}
+
+// Tile choice.  The 256 x 256 (16-wave) tile is the throughput shape; when it would leave most
+// of the 256 CUs idle (fewer tiles than CUs: B = 1 forwards, pruned token sets) the 64 x 64
+// single-wave tile spreads the same work over 16x more workgroups.  LG_GEMM_TILE=big|small
+// overrides the choice (tests run both on the golden cases).
+enum { TILE_AUTO, TILE_BIG, TILE_SMALL };
+static int gemm_tile_override() {
+  const char* e = getenv("LG_GEMM_TILE");
+  if (!e) return TILE_AUTO;
+  if (!strcmp(e, "big")) return TILE_BIG;
+  if (!strcmp(e, "small")) return TILE_SMALL;
+  return TILE_AUTO;
+}
+static bool use_small_tiles(long long big_tiles) {
+  const int o = gemm_tile_override();
+  return o == TILE_SMALL || (o == TILE_AUTO && big_tiles < 256);
 }
 
 #ifndef LG_GEMM_H3_TILE
@@ -545,8 +565,10 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
     return hipErrorInvalidValue;
   if (epi == EPI_LN_GELU) {
     if (a.Nout != 512 || !a.Yp || !a.ln_g || !a.ln_b || a.yrows_pad < a.R) return hipErrorInvalidValue;
+    if (use_small_tiles((a.R + 127) / 128)) return gemm_h3_ln_launch<64, 64>(a, st);
     return gemm_h3_ln_launch<LG_GEMM_LN_WN>(a, st);
   }
+  if (use_small_tiles((long long)((a.R + TB - 1) / TB) * (a.Nout / TB))) return gemm_h3_launch<64, 2, 64, 64>(a, epi, st);
   return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
 }
 

@@ -84,6 +84,23 @@ def test_forward_matches_reference_golden(name, precision):
     check_against_golden(pred, g)
 
 
+@pytest.mark.parametrize("tile", ["big", "small"])
+@pytest.mark.parametrize("name", case_names())
+def test_forward_golden_both_gemm_tiles(name, tile, monkeypatch):
+    """The fp16x3 GEMM picks 256x256 tiles (throughput) or 64x64 tiles (fewer big tiles than CUs,
+    e.g. B = 1) by row count; LG_GEMM_TILE forces either so that both are checked against the
+    reference on every golden case."""
+    monkeypatch.setenv("LG_GEMM_TILE", tile)
+    g = load(name)
+    conf, sd, data = case_inputs(g["meta"])
+    model = _model(conf, sd, "auto")
+    with torch.no_grad():
+        pred = model(_gpu_data(data))
+    torch.cuda.synchronize()
+    assert model.last_precision_used == "fp16x3"
+    check_against_golden(pred, g)
+
+
 def test_fp16_range_guard_reruns_in_bf16x6():
     """Descriptors beyond the fp16 range (|x| > 65504) trip the guard: the forward is recomputed
     in bf16x6 and gives exactly the bf16x6 result."""

@@ -28,6 +28,8 @@
 // query blocks sharing one K/V run on the same XCD (L2).
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -601,10 +603,10 @@ __device__ __forceinline__ float sum_x16_32(float v) {
 // (SUBS = 2: 2 x 64 KiB of LDS), and PRIO raises the second-dispatched half of the waves to
 // s_setprio 1 once.  tools/kbench_attn.hip: 862 us vs 907-918 us for the register-staged
 // attention_h3f_kernel (tools/attn_experiments.hip) at the bench shape.
-template <int SUBS, int PRIO>
-__global__ __launch_bounds__(512, 2) void attention_h3g_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+template <int SUBS, int PRIO, int WAVES = 8>
+__global__ __launch_bounds__(64 * WAVES, 8 / WAVES + (WAVES == 8)) void attention_h3g_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
                                                                 float scale_log2e) {
-  constexpr int WAVES = 8, QB = 32 * WAVES;
+  constexpr int QB = 32 * WAVES;
   constexpr int KT = 64;                   // keys per sub-tile (one softmax step)
   constexpr int LT = KT * SUBS;            // keys per LDS tile (one barrier)
   constexpr int NKT = KT / 16;
@@ -818,7 +820,7 @@ __global__ __launch_bounds__(512, 2) void attention_h3g_kernel(AttnSet s0, AttnS
   using IC3 = std::integral_constant<int, 2 * PL + KT * kHeadDim>;
   static_assert(SUBS == 1 || SUBS == 2, "sub-tiles per LDS tile");
   // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (PRIO && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -873,17 +875,30 @@ __global__ __launch_bounds__(512, 2) void attention_h3g_kernel(AttnSet s0, AttnS
   }
 }
 
-template <int SUBS, int PRIO = 0>
+template <int SUBS, int PRIO = 0, int WAVES = 8>
 static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
-  constexpr int QB = 256;
+  constexpr int QB = 32 * WAVES;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
   if (nq == 0 || B == 0) return hipSuccess;
   if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
   const int nqb = (nq + QB - 1) / QB;
   const int items = nqb * B * H * 2;
-  hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO>), dim3(items), dim3(512), 0, st, s0, s1, B, H, nqb,
+  hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
                      scale * 1.4426950408889634f);
   return hipGetLastError();
+}
+
+// Query block size: 8 waves (256 queries) per workgroup is the throughput shape; when that gives
+// fewer work items than CUs (B = 1, pruned sets) 4 waves per workgroup spread the queries over
+// twice the CUs (each workgroup still streams all keys).  LG_ATTN_WAVES=8|4|2 forces one.
+static int attention_waves(int B, int H, int nq) {
+  if (const char* e = getenv("LG_ATTN_WAVES")) {
+    const int w = atoi(e);
+    if (w == 8 || w == 4 || w == 2) return w;
+  }
+  // 4 waves measured best below one item per CU (B = 1, N = 1024: 32.9 us vs 42.7 (8) / 38.1 (2));
+  // 2 is kept for LG_ATTN_WAVES only
+  return (long long)((nq + 255) / 256) * B * H * 2 >= 256 ? 8 : 4;
 }
 
 template <int WAVES, int KT>
@@ -914,7 +929,12 @@ hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, flo
 #ifdef LG_ATTN_H3_LEGACY
     return attention_h3_launch<LG_ATTN_H3_CONFIG>(s0, s1, B, H, scale, st);
 #else
-    return attention_h3g_launch<2, 1>(s0, s1, B, H, scale, st);
+    const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
+    switch (attention_waves(B, H, nq)) {
+      case 2: return attention_h3g_launch<2, 1, 2>(s0, s1, B, H, scale, st);
+      case 4: return attention_h3g_launch<2, 1, 4>(s0, s1, B, H, scale, st);
+      default: return attention_h3g_launch<2, 1, 8>(s0, s1, B, H, scale, st);
+    }
 #endif
   }
   return attention_x6_launch<LG_ATTN_CONFIG>(s0, s1, B, H, scale, st);

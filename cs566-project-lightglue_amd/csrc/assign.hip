@@ -13,6 +13,8 @@
 //   col argmax  per-chunk partial (value, first index) -> combine
 //   filter      one thread per keypoint
 // Ties resolve to the smallest index, as torch-CPU max(dim) does.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -204,6 +206,233 @@ __global__ void filter_kernel(Stats st, int B, int M, int N, float th, int64_t* 
   }
 }
 
+
+// ------------------------------------------------------------------ fused passes (N % 4 == 0,
+// N <= 2048: the main path).  A workgroup of 8 waves owns one 64-row chunk of one pair (wave w:
+// rows 8w .. 8w+7 of the chunk), so its column partials have exactly the [B][nch][N] layout the
+// combine kernels above read.
+//   stats pass: ONE read of sim for both softmax directions -- a wave holds a row in registers
+//     (row max, then sum of exp(x - max): row_stats_kernel's formula) and folds it into running
+//     (max, sum) column pairs; the 8 waves merge through LDS (col_stats_combine finishes)
+//   la pass:    ONE read of sim for the la write, the row argmax and the column argmax partials
+//     (running first-index best per column, merged across waves in row order)
+// The old path (row_stats + col_stats_partial, row_pass + col_arg_partial: four reads) serves
+// other N.
+namespace {
+constexpr int kAsW = 8;          // waves per workgroup (CCH / kAsW = 8 rows each)
+constexpr int kAsMaxN = 2048;
+
+__device__ __forceinline__ void lse_merge_pair(float& am, float& as, float bm, float bs) {
+  const float m = fmaxf(am, bm);
+  const float ea = am == m ? 1.f : expf(am - m);
+  const float eb = bm == m ? 1.f : expf(bm - m);
+  as = as * ea + bs * eb;
+  am = m;
+}
+}  // namespace
+
+template <int K4>
+__global__ __launch_bounds__(kAsW * 64) void stats_fused_kernel(const float* __restrict__ sim, int M, int N, float* rmax,
+                                                                float* rlog, float* pmax, float* psum) {
+  __shared__ float2 mb[kAsW / 2][kAsMaxN];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ch = blockIdx.x, b = blockIdx.y, nch = gridDim.x;
+  float cm[K4][4], cs[K4][4];
+#pragma unroll
+  for (int k = 0; k < K4; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cm[k][e] = -INFINITY, cs[k][e] = 0.f;
+  const int r0 = ch * CCH + wave * (CCH / kAsW);
+  const int r1 = min(M, r0 + CCH / kAsW);
+#pragma unroll 1
+  for (int i = r0; i < r1; ++i) {
+    const char* row = reinterpret_cast<const char*>(sim + ((size_t)b * M + i) * N);
+    f32x4 x[K4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const int c = 256 * k + 4 * lane;
+      x[k] = c < N ? *reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane))
+                   : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      m = fmaxf(m, fmaxf(fmaxf(x[k][0], x[k][1]), fmaxf(x[k][2], x[k][3])));
+    }
+    m = wave_max(m);
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < K4; ++k) sum += (expf(x[k][0] - m) + expf(x[k][1] - m)) + (expf(x[k][2] - m) + expf(x[k][3] - m));
+    sum = wave_sum(sum);
+    if (lane == 0) {
+      rmax[(size_t)b * M + i] = m;
+      rlog[(size_t)b * M + i] = logf(sum);
+    }
+#pragma unroll
+    for (int k = 0; k < K4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // col_stats_partial_kernel's running update
+        const float v = x[k][e];
+        if (v > cm[k][e]) {
+          cs[k][e] = cs[k][e] * expf(cm[k][e] - v) + 1.f;
+          cm[k][e] = v;
+        } else {
+          cs[k][e] += expf(v - cm[k][e]);
+        }
+      }
+  }
+#pragma unroll
+  for (int half = kAsW / 2; half >= 1; half >>= 1) {
+    if (wave >= half && wave < 2 * half) {
+#pragma unroll
+      for (int k = 0; k < K4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 256 * k + 4 * lane + e;
+          if (c < N) mb[wave - half][c] = make_float2(cm[k][e], cs[k][e]);
+        }
+    }
+    __syncthreads();
+    if (wave < half) {
+#pragma unroll
+      for (int k = 0; k < K4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 256 * k + 4 * lane + e;
+          if (c < N) {
+            const float2 o = mb[wave][c];
+            lse_merge_pair(cm[k][e], cs[k][e], o.x, o.y);
+          }
+        }
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < K4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 256 * k + 4 * lane + e;
+        if (c < N) {
+          pmax[((size_t)b * nch + ch) * N + c] = cm[k][e];
+          psum[((size_t)b * nch + ch) * N + c] = cs[k][e];
+        }
+      }
+  }
+}
+
+// la row write + row argmax + column argmax partials; lane columns j = 64 t + lane (coalesced
+// scalar loads and la stores, as row_pass_kernel)
+template <int T>
+__global__ __launch_bounds__(kAsW * 64) void la_fused_kernel(const float* __restrict__ sim, Stats st,
+                                                             const float* __restrict__ z0, float* la, int M, int N) {
+  __shared__ float cst[3][kAsMaxN];              // cmax, clog, ls1 of this pair
+  __shared__ float mbv[kAsW / 2][kAsMaxN];
+  __shared__ int mbi[kAsW / 2][kAsMaxN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ch = blockIdx.x, b = blockIdx.y, nch = gridDim.x;
+  for (int j = tid; j < N; j += kAsW * 64) {
+    cst[0][j] = st.cmax[(size_t)b * N + j];
+    cst[1][j] = st.clog[(size_t)b * N + j];
+    cst[2][j] = st.ls1[(size_t)b * N + j];
+  }
+  __syncthreads();
+  const int r0 = ch * CCH + wave * (CCH / kAsW);
+  const int r1 = min(M, r0 + CCH / kAsW);
+  float cb[T];  // col_arg_partial_kernel's scan: best = -inf, index = first row, strict >
+  int ci[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) cb[t] = -INFINITY, ci[t] = r0;
+#pragma unroll 1
+  for (int i = r0; i < r1; ++i) {
+    const int ri = b * M + i;
+    const float rm = st.rmax[ri], rl = st.rlog[ri], l0 = st.ls0[ri];
+    const float* x = sim + (size_t)ri * N;
+    float* lr = la ? la + ((size_t)b * (M + 1) + i) * (N + 1) : nullptr;
+    float xv[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int j = 64 * t + lane;
+      xv[t] = j < N ? x[j] : 0.f;
+    }
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int j = 64 * t + lane;
+      if (j < N) {
+        // score_at<false>: same operations in the same order
+        const float s0 = (xv[t] - rm) - rl;
+        const float s1 = (xv[t] - cst[0][j]) - cst[1][j];
+        const float v = (s0 + s1) + (l0 + cst[2][j]);
+        if (lr) lr[j] = v;
+        if (bi == 0x7fffffff || v > best) { best = v; bi = j; }
+        if (v > cb[t]) { cb[t] = v; ci[t] = i; }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (lane == 0) {
+      st.max0[ri] = best;
+      st.arg0[ri] = bi;
+      if (lr) lr[N] = log_sigmoid(-z0[ri]);
+    }
+  }
+  // merge waves (wave w + half holds later rows: it wins only with a strictly greater value)
+#pragma unroll
+  for (int half = kAsW / 2; half >= 1; half >>= 1) {
+    if (wave >= half && wave < 2 * half) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int j = 64 * t + lane;
+        if (j < N) {
+          mbv[wave - half][j] = cb[t];
+          mbi[wave - half][j] = ci[t];
+        }
+      }
+    }
+    __syncthreads();
+    if (wave < half) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int j = 64 * t + lane;
+        if (j < N) {
+          const float ov = mbv[wave][j];
+          const int oi = mbi[wave][j];
+          if (ov > cb[t]) { cb[t] = ov; ci[t] = oi; }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int j = 64 * t + lane;
+      if (j < N) {
+        st.pv[((size_t)b * nch + ch) * N + j] = cb[t];
+        st.pi[((size_t)b * nch + ch) * N + j] = ci[t];
+      }
+    }
+  }
+}
+
+template <int K4>
+static void launch_assign_fused(const AssignArgs& a, const Stats& s, int nch, float* psum, hipStream_t st) {
+  const dim3 grid(nch, a.B), block(kAsW * 64);
+  hipLaunchKernelGGL((stats_fused_kernel<K4>), grid, block, 0, st, a.sim, a.M, a.N, s.rmax, s.rlog, s.pv, psum);
+}
+template <int T>
+static void launch_la_fused(const AssignArgs& a, const Stats& s, int nch, hipStream_t st) {
+  const dim3 grid(nch, a.B), block(kAsW * 64);
+  hipLaunchKernelGGL((la_fused_kernel<T>), grid, block, 0, st, a.sim, s, a.z0, a.la, a.M, a.N);
+}
+
+#ifndef LG_ASSIGN_FUSED
+#define LG_ASSIGN_FUSED 1
+#endif
+
 static Stats carve(float* ws, int B, int M, int N) {
   const int nch = (M + CCH - 1) / CCH;
   Stats s;
@@ -241,15 +470,35 @@ hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st) {
   if (B * M == 0 || B * N == 0) return hipErrorInvalidValue;
   const Stats s = carve(a.ws, B, M, N);
   const int nch = (M + CCH - 1) / CCH;
-  hipLaunchKernelGGL(row_stats_kernel, dim3((B * M + 3) / 4), dim3(256), 0, st, a.sim, B * M, N, s.rmax, s.rlog);
-  const dim3 cg((N + 255) / 256, nch, B);
   float* psum = reinterpret_cast<float*>(s.pi);  // the argmax index partials are not live yet
-  hipLaunchKernelGGL(col_stats_partial_kernel, cg, dim3(256), 0, st, a.sim, M, N, s.pv, psum);
+  const bool fused = LG_ASSIGN_FUSED && N % 4 == 0 && N <= kAsMaxN && !getenv("LG_ASSIGN_UNFUSED");
+  if (fused) {
+    const int k4 = (N + 255) / 256;
+    if (k4 <= 1) launch_assign_fused<1>(a, s, nch, psum, st);
+    else if (k4 <= 2) launch_assign_fused<2>(a, s, nch, psum, st);
+    else if (k4 <= 4) launch_assign_fused<4>(a, s, nch, psum, st);
+    else launch_assign_fused<8>(a, s, nch, psum, st);
+  } else {
+    hipLaunchKernelGGL(row_stats_kernel, dim3((B * M + 3) / 4), dim3(256), 0, st, a.sim, B * M, N, s.rmax, s.rlog);
+    const dim3 cg((N + 255) / 256, nch, B);
+    hipLaunchKernelGGL(col_stats_partial_kernel, cg, dim3(256), 0, st, a.sim, M, N, s.pv, psum);
+  }
   hipLaunchKernelGGL(col_stats_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s.pv, psum, nch, N, B * N,
                      s.cmax, s.clog);
   hipLaunchKernelGGL(logsig_kernel, dim3((B * M + 255) / 256), dim3(256), 0, st, a.z0, s.ls0, B * M);
   hipLaunchKernelGGL(logsig_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, a.z1, s.ls1, B * N);
   if (a.la) hipLaunchKernelGGL(la_last_row_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, a.z1, a.la, B, M, N);
+  if (fused) {
+    const int t = (N + 63) / 64;
+    if (t <= 4) launch_la_fused<4>(a, s, nch, st);
+    else if (t <= 8) launch_la_fused<8>(a, s, nch, st);
+    else if (t <= 16) launch_la_fused<16>(a, s, nch, st);
+    else launch_la_fused<32>(a, s, nch, st);
+    hipLaunchKernelGGL(col_arg_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s, nch, N, B * N);
+    hipLaunchKernelGGL(filter_kernel, dim3((B * (M + N) + 255) / 256), dim3(256), 0, st, s, B, M, N, a.th, a.m0, a.m1,
+                       a.s0, a.s1);
+    return hipGetLastError();
+  }
   return argmax_and_filter<false>(a.sim, s, a.z0, a.la, B, M, N, a.th, a.m0, a.m1, a.s0, a.s1, st);
 }
 

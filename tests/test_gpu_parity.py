@@ -84,15 +84,18 @@ def test_forward_matches_reference_golden(name, precision):
     check_against_golden(pred, g)
 
 
-@pytest.mark.parametrize("tile,waves", [("big", "8"), ("small", "4"), ("small", "2")])
+@pytest.mark.parametrize("tile,waves,assign", [("big", "8", "fused"), ("small", "4", "fused"), ("small", "2", "unfused")])
 @pytest.mark.parametrize("name", case_names())
-def test_forward_golden_all_launch_shapes(name, tile, waves, monkeypatch):
+def test_forward_golden_all_launch_shapes(name, tile, waves, assign, monkeypatch):
     """The fp16x3 GEMM picks 256x256 tiles (throughput) or 64x64 tiles (fewer big tiles than CUs,
     e.g. B = 1) by row count, and the attention 8, 4 or 2 waves (256/128/64 queries) per
-    workgroup; LG_GEMM_TILE / LG_ATTN_WAVES force each so that every launch shape is checked
-    against the reference on every golden case."""
+    workgroup, and the assignment its two-read fused passes (N % 4 == 0, N <= 2048) or the
+    four-read ones; LG_GEMM_TILE / LG_ATTN_WAVES / LG_ASSIGN_UNFUSED force each so that every
+    launch shape is checked against the reference on every golden case."""
     monkeypatch.setenv("LG_GEMM_TILE", tile)
     monkeypatch.setenv("LG_ATTN_WAVES", waves)
+    if assign == "unfused":  # the four-read assignment path (N % 4 != 0 or N > 2048)
+        monkeypatch.setenv("LG_ASSIGN_UNFUSED", "1")
     g = load(name)
     conf, sd, data = case_inputs(g["meta"])
     model = _model(conf, sd, "auto")

@@ -143,7 +143,10 @@ int lg_filter_matches(const float* scores, int32_t B, int32_t M, int32_t N, doub
                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* log_optimal_transport (superglue.py:181-201): Z [B,M+1,N+1] = log-domain Sinkhorn of
- * `scores` [B,M,N] with a dustbin of score `alpha`, `iters` iterations, multiplied by M+N. */
+ * `scores` [B,M,N] with a dustbin of score `alpha`, `iters` iterations, multiplied by M+N.
+ * N <= 4096: one read of the scores per iteration with scaled column sums; synchronises the
+ * stream once (4-byte underflow flag) and reruns the exact running-max kernel if any column sum
+ * left the fp32 range.  N > 4096: two reads per iteration, fully asynchronous. */
 int lg_sinkhorn_workspace_bytes(int32_t B, int32_t M, int32_t N, size_t* bytes);
 int lg_log_optimal_transport(const float* scores, float alpha, int32_t B, int32_t M, int32_t N,
                              int32_t iters, float* Z, void* workspace, size_t workspace_bytes,

@@ -88,9 +88,12 @@ CASES = ["random_ragged", "increasing_scores", "decreasing_scores", "large_logit
          "one_key_in_last_tile"]
 
 
-@pytest.mark.parametrize("precision", ["auto", "bf16x6"])
+@pytest.mark.parametrize("precision,waves", [("auto", "8"), ("auto", "4"), ("auto", "2"), ("bf16x6", "8")])
 @pytest.mark.parametrize("name", CASES)
-def test_attention_matches_float64(name, precision):
+def test_attention_matches_float64(name, precision, waves, monkeypatch):
+    # fp16x3 kernel under every query-block shape (LG_ATTN_WAVES: 256 / 128 / 64 queries per
+    # workgroup); the small shapes here would otherwise always pick 4
+    monkeypatch.setenv("LG_ATTN_WAVES", waves)
     q, k, v, scale = case(name)
     got = run_attention(q, k, v, scale, precision)
     ref = reference(q, k, v, scale)

@@ -244,6 +244,7 @@ __global__ __launch_bounds__(kAsW * 64) void stats_fused_kernel(const float* __r
     for (int e = 0; e < 4; ++e) cm[k][e] = -INFINITY, cs[k][e] = 0.f;
   const int r0 = ch * CCH + wave * (CCH / kAsW);
   const int r1 = min(M, r0 + CCH / kAsW);
+  auto c_ok = [&](int k, int e) { return 256 * k + 4 * lane + e < N; };
 #pragma unroll 1
   for (int i = r0; i < r1; ++i) {
     const char* row = reinterpret_cast<const char*>(sim + ((size_t)b * M + i) * N);
@@ -268,13 +269,15 @@ __global__ __launch_bounds__(kAsW * 64) void stats_fused_kernel(const float* __r
 #pragma unroll
     for (int k = 0; k < K4; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {  // col_stats_partial_kernel's running update
+      for (int e = 0; e < 4; ++e) {  // running (max, sum) with one exponential: e^-|v - max|
         const float v = x[k][e];
-        if (v > cm[k][e]) {
-          cs[k][e] = cs[k][e] * expf(cm[k][e] - v) + 1.f;
+        const float d = v - cm[k][e];
+        const float t = expf(-fabsf(d));
+        if (d > 0.f) {
+          cs[k][e] = fmaf(cs[k][e], t, 1.f);
           cm[k][e] = v;
-        } else {
-          cs[k][e] += expf(v - cm[k][e]);
+        } else if (c_ok(k, e)) {
+          cs[k][e] += t;
         }
       }
   }
@@ -318,12 +321,12 @@ __global__ __launch_bounds__(kAsW * 64) void stats_fused_kernel(const float* __r
   }
 }
 
-// la row write + row argmax + column argmax partials; lane columns j = 64 t + lane (coalesced
-// scalar loads and la stores, as row_pass_kernel)
-template <int T>
+// la row write + row argmax + column argmax partials; lane columns 256 k + 4 lane + e (16-byte
+// sim loads and LDS column-stat reads; the la rows are N+1 long, so their stores stay scalar)
+template <int K4>
 __global__ __launch_bounds__(kAsW * 64) void la_fused_kernel(const float* __restrict__ sim, Stats st,
                                                              const float* __restrict__ z0, float* la, int M, int N) {
-  __shared__ float cst[3][kAsMaxN];              // cmax, clog, ls1 of this pair
+  __shared__ __attribute__((aligned(16))) float cst[3][kAsMaxN];  // cmax, clog, ls1 of this pair
   __shared__ float mbv[kAsW / 2][kAsMaxN];
   __shared__ int mbi[kAsW / 2][kAsMaxN];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -336,35 +339,43 @@ __global__ __launch_bounds__(kAsW * 64) void la_fused_kernel(const float* __rest
   __syncthreads();
   const int r0 = ch * CCH + wave * (CCH / kAsW);
   const int r1 = min(M, r0 + CCH / kAsW);
-  float cb[T];  // col_arg_partial_kernel's scan: best = -inf, index = first row, strict >
-  int ci[T];
+  float cb[K4][4];  // col_arg_partial_kernel's scan: best = -inf, index = first row, strict >
+  int ci[K4][4];
 #pragma unroll
-  for (int t = 0; t < T; ++t) cb[t] = -INFINITY, ci[t] = r0;
+  for (int k = 0; k < K4; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cb[k][e] = -INFINITY, ci[k][e] = r0;
 #pragma unroll 1
   for (int i = r0; i < r1; ++i) {
     const int ri = b * M + i;
     const float rm = st.rmax[ri], rl = st.rlog[ri], l0 = st.ls0[ri];
-    const float* x = sim + (size_t)ri * N;
+    const char* row = reinterpret_cast<const char*>(sim + (size_t)ri * N);
     float* lr = la ? la + ((size_t)b * (M + 1) + i) * (N + 1) : nullptr;
-    float xv[T];
+    f32x4 xv[K4];
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const int j = 64 * t + lane;
-      xv[t] = j < N ? x[j] : 0.f;
+    for (int k = 0; k < K4; ++k) {
+      const int c = 256 * k + 4 * lane;
+      xv[k] = c < N ? *reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane)) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     float best = -INFINITY;
     int bi = 0x7fffffff;
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const int j = 64 * t + lane;
-      if (j < N) {
-        // score_at<false>: same operations in the same order
-        const float s0 = (xv[t] - rm) - rl;
-        const float s1 = (xv[t] - cst[0][j]) - cst[1][j];
-        const float v = (s0 + s1) + (l0 + cst[2][j]);
-        if (lr) lr[j] = v;
-        if (bi == 0x7fffffff || v > best) { best = v; bi = j; }
-        if (v > cb[t]) { cb[t] = v; ci[t] = i; }
+    for (int k = 0; k < K4; ++k) {
+      const int c = 256 * k + 4 * lane;
+      if (c < N) {
+        const f32x4 cmx = *reinterpret_cast<const f32x4*>(&cst[0][c]);
+        const f32x4 clg = *reinterpret_cast<const f32x4*>(&cst[1][c]);
+        const f32x4 l1 = *reinterpret_cast<const f32x4*>(&cst[2][c]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          // score_at<false>: same operations in the same order
+          const float s0 = (xv[k][e] - rm) - rl;
+          const float s1 = (xv[k][e] - cmx[e]) - clg[e];
+          const float v = (s0 + s1) + (l0 + l1[e]);
+          if (lr) lr[c + e] = v;
+          if (bi == 0x7fffffff || v > best) { best = v; bi = c + e; }
+          if (v > cb[k][e]) { cb[k][e] = v; ci[k][e] = i; }
+        }
       }
     }
 #pragma unroll
@@ -384,23 +395,26 @@ __global__ __launch_bounds__(kAsW * 64) void la_fused_kernel(const float* __rest
   for (int half = kAsW / 2; half >= 1; half >>= 1) {
     if (wave >= half && wave < 2 * half) {
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const int j = 64 * t + lane;
-        if (j < N) {
-          mbv[wave - half][j] = cb[t];
-          mbi[wave - half][j] = ci[t];
+      for (int k = 0; k < K4; ++k) {
+        const int c = 256 * k + 4 * lane;
+        if (c < N) {
+          *reinterpret_cast<f32x4*>(&mbv[wave - half][c]) = f32x4{cb[k][0], cb[k][1], cb[k][2], cb[k][3]};
+          *reinterpret_cast<int4*>(&mbi[wave - half][c]) = make_int4(ci[k][0], ci[k][1], ci[k][2], ci[k][3]);
         }
       }
     }
     __syncthreads();
     if (wave < half) {
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const int j = 64 * t + lane;
-        if (j < N) {
-          const float ov = mbv[wave][j];
-          const int oi = mbi[wave][j];
-          if (ov > cb[t]) { cb[t] = ov; ci[t] = oi; }
+      for (int k = 0; k < K4; ++k) {
+        const int c = 256 * k + 4 * lane;
+        if (c < N) {
+          const f32x4 ov = *reinterpret_cast<const f32x4*>(&mbv[wave][c]);
+          const int4 oi = *reinterpret_cast<const int4*>(&mbi[wave][c]);
+          const int oa[4] = {oi.x, oi.y, oi.z, oi.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (ov[e] > cb[k][e]) { cb[k][e] = ov[e]; ci[k][e] = oa[e]; }
         }
       }
     }
@@ -408,11 +422,11 @@ __global__ __launch_bounds__(kAsW * 64) void la_fused_kernel(const float* __rest
   }
   if (wave == 0) {
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const int j = 64 * t + lane;
-      if (j < N) {
-        st.pv[((size_t)b * nch + ch) * N + j] = cb[t];
-        st.pi[((size_t)b * nch + ch) * N + j] = ci[t];
+    for (int k = 0; k < K4; ++k) {
+      const int c = 256 * k + 4 * lane;
+      if (c < N) {
+        *reinterpret_cast<f32x4*>(st.pv + ((size_t)b * nch + ch) * N + c) = f32x4{cb[k][0], cb[k][1], cb[k][2], cb[k][3]};
+        *reinterpret_cast<int4*>(st.pi + ((size_t)b * nch + ch) * N + c) = make_int4(ci[k][0], ci[k][1], ci[k][2], ci[k][3]);
       }
     }
   }
@@ -489,11 +503,11 @@ hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(logsig_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, a.z1, s.ls1, B * N);
   if (a.la) hipLaunchKernelGGL(la_last_row_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, a.z1, a.la, B, M, N);
   if (fused) {
-    const int t = (N + 63) / 64;
-    if (t <= 4) launch_la_fused<4>(a, s, nch, st);
-    else if (t <= 8) launch_la_fused<8>(a, s, nch, st);
-    else if (t <= 16) launch_la_fused<16>(a, s, nch, st);
-    else launch_la_fused<32>(a, s, nch, st);
+    const int k4 = (N + 255) / 256;
+    if (k4 <= 1) launch_la_fused<1>(a, s, nch, st);
+    else if (k4 <= 2) launch_la_fused<2>(a, s, nch, st);
+    else if (k4 <= 4) launch_la_fused<4>(a, s, nch, st);
+    else launch_la_fused<8>(a, s, nch, st);
     hipLaunchKernelGGL(col_arg_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s, nch, N, B * N);
     hipLaunchKernelGGL(filter_kernel, dim3((B * (M + N) + 255) / 256), dim3(256), 0, st, s, B, M, N, a.th, a.m0, a.m1,
                        a.s0, a.s1);

@@ -604,7 +604,7 @@ __device__ __forceinline__ float sum_x16_32(float v) {
 // s_setprio 1 once.  tools/kbench_attn.hip: 862 us vs 907-918 us for the register-staged
 // attention_h3f_kernel (tools/attn_experiments.hip) at the bench shape.
 template <int SUBS, int PRIO, int WAVES = 8>
-__global__ __launch_bounds__(64 * WAVES, 8 / WAVES + (WAVES == 8)) void attention_h3g_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+__global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
                                                                 float scale_log2e) {
   constexpr int QB = 32 * WAVES;
   constexpr int KT = 64;                   // keys per sub-tile (one softmax step)

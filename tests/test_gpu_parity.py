@@ -106,6 +106,34 @@ def test_forward_golden_all_launch_shapes(name, tile, waves, assign, monkeypatch
     check_against_golden(pred, g)
 
 
+def test_weight_changes_after_first_forward_are_picked_up():
+    """The forward re-uploads weights when a parameter changes in place (version bump) or is
+    replaced by a new tensor object, like a torch module would use its current parameters."""
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1}
+    sd = synthetic_state_dict(conf, seed=0)
+    data = _gpu_data(synthetic_pair(B=1, M=200, N=180, seed=4))
+    model = _model(conf, sd)
+    with torch.no_grad():
+        model(data)
+        model.log_assignment[-1].final_proj.weight.mul_(0.5)  # in place
+        a = model(data)
+        model.log_assignment[-1].matchability.bias = torch.nn.Parameter(  # new object
+            model.log_assignment[-1].matchability.bias.detach() + 1.0)
+        b = model(data)
+    sd2 = {k: v.copy() for k, v in sd.items()}
+    sd2["log_assignment.8.final_proj.weight"] = sd2["log_assignment.8.final_proj.weight"] * np.float32(0.5)
+    ref_a = _model(conf, sd2)
+    sd2["log_assignment.8.matchability.bias"] = sd2["log_assignment.8.matchability.bias"] + np.float32(1.0)
+    ref_b = _model(conf, sd2)
+    with torch.no_grad():
+        ra, rb = ref_a(data), ref_b(data)
+    for got, ref in ((a, ra), (b, rb)):
+        assert torch.equal(got["matches0"], ref["matches0"])
+        assert torch.equal(got["log_assignment"], ref["log_assignment"])
+
+
 def test_fp16_range_guard_reruns_in_bf16x6():
     """Descriptors beyond the fp16 range (|x| > 65504) trip the guard: the forward is recomputed
     in bf16x6 and gives exactly the bf16x6 result."""

@@ -257,11 +257,11 @@ __global__ __launch_bounds__(kAsW * 64) void stats_fused_kernel(const float* __r
                    : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       m = fmaxf(m, fmaxf(fmaxf(x[k][0], x[k][1]), fmaxf(x[k][2], x[k][3])));
     }
-    m = wave_max(m);
+    m = wave_max_dpp(m);
     float sum = 0.f;
 #pragma unroll
     for (int k = 0; k < K4; ++k) sum += (expf(x[k][0] - m) + expf(x[k][1] - m)) + (expf(x[k][2] - m) + expf(x[k][3] - m));
-    sum = wave_sum(sum);
+    sum = wave_sum_dpp(sum);
     if (lane == 0) {
       rmax[(size_t)b * M + i] = m;
       rlog[(size_t)b * M + i] = logf(sum);
@@ -378,12 +378,7 @@ __global__ __launch_bounds__(kAsW * 64) void la_fused_kernel(const float* __rest
         }
       }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const float ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
-    }
+    wave_argmax_dpp(best, bi);
     if (lane == 0) {
       st.max0[ri] = best;
       st.arg0[ri] = bi;

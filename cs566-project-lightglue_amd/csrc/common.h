@@ -44,6 +44,66 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// wave-wide max / sum without an LDS round trip: DPP within 16 lanes (quad xor 1, xor 2,
+// half-row mirror, row mirror), then v_permlane16_swap / v_permlane32_swap across rows; every
+// lane ends with bitwise the same value
+template <int C>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return max_xor32(fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return sum_xor32(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+}
+
+// wave-wide (max value, smallest index among the maxima) with the same DPP / permlane steps
+template <int C>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, C, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void argmax_merge(float& best, int& bi, float ov, int oi) {
+  if (ov > best || (ov == best && oi < bi)) {
+    best = ov;
+    bi = oi;
+  }
+}
+__device__ __forceinline__ void wave_argmax_dpp(float& best, int& bi) {
+  argmax_merge(best, bi, dppf<0xB1>(best), dppi<0xB1>(bi));
+  argmax_merge(best, bi, dppf<0x4E>(best), dppi<0x4E>(bi));
+  argmax_merge(best, bi, dppf<0x141>(best), dppi<0x141>(bi));
+  argmax_merge(best, bi, dppf<0x140>(best), dppi<0x140>(bi));
+  {
+    const auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+    const auto i = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
+    float b0 = __uint_as_float(v[0]);
+    int i0 = (int)i[0];
+    argmax_merge(b0, i0, __uint_as_float(v[1]), (int)i[1]);
+    best = b0;
+    bi = i0;
+  }
+  {
+    const auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+    const auto i = __builtin_amdgcn_permlane32_swap((unsigned)bi, (unsigned)bi, false, false);
+    float b0 = __uint_as_float(v[0]);
+    int i0 = (int)i[0];
+    argmax_merge(b0, i0, __uint_as_float(v[1]), (int)i[1]);
+    best = b0;
+    bi = i0;
+  }
+}
+
 // Exact (IEEE, non-contracted) elementwise ops: used where the reference's torch-CPU op order
 // is mirrored bit-for-bit (positional encoding, keypoint normalisation, rotary).
 __device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }

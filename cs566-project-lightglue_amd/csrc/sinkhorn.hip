@@ -315,30 +315,6 @@ __global__ void sinkhorn_colmerge_kernel(const float2* part, float* v, int B, in
 }
 
 
-// wave-wide max / sum without an LDS round trip: DPP within 16 lanes (quad xor 1, xor 2,
-// half-row mirror, row mirror), then v_permlane16_swap / v_permlane32_swap across rows; every
-// lane ends with bitwise the same value
-template <int C>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float wave_max_dpp(float v) {
-  v = fmaxf(v, dppf<0xB1>(v));
-  v = fmaxf(v, dppf<0x4E>(v));
-  v = fmaxf(v, dppf<0x141>(v));
-  v = fmaxf(v, dppf<0x140>(v));
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return max_xor32(fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])));
-}
-__device__ __forceinline__ float wave_sum_dpp(float v) {
-  v += dppf<0xB1>(v);
-  v += dppf<0x4E>(v);
-  v += dppf<0x141>(v);
-  v += dppf<0x140>(v);
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return sum_xor32(__uint_as_float(r[0]) + __uint_as_float(r[1]));
-}
-
 // Scaled variant (default): the column statistics reuse the row pass's exponentials.  With
 // e_ij = exp(Zc_ij + v_j - m_i) (m_i the row max, so e_ij <= 1) and a_i = exp(u_i + m_i)
 // = exp(log_mu_i) / s_i <= 1, e_ij * a_i = exp(Zc_ij + u_i + v_j): every row adds into the same

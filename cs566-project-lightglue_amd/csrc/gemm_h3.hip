@@ -568,7 +568,7 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
     if (use_small_tiles((a.R + 127) / 128)) return gemm_h3_ln_launch<64, 64>(a, st);
     return gemm_h3_ln_launch<LG_GEMM_LN_WN>(a, st);
   }
-  if (use_small_tiles((long long)((a.R + TB - 1) / TB) * (a.Nout / TB))) return gemm_h3_launch<64, 2, 64, 64>(a, epi, st);
+  if (use_small_tiles((long long)((a.R + TB - 1) / TB) * (a.Nout / TB))) return gemm_h3_launch<64, 4, 64, 64>(a, epi, st);
   return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
 }
 

@@ -557,6 +557,11 @@ static bool use_small_tiles(long long big_tiles) {
 #define LG_GEMM_H3_TILE 256, 2
 #endif
 
+// ffn.0 + LN + GELU at small row counts: even 64 x 512 tiles leave most CUs idle, so the caller
+// runs ffn.0 as a 64 x 64-tile EPI_STORE GEMM and LayerNorm + GELU as a row kernel
+// (layernorm_gelu_512, which writes the same plane image)
+bool gemm_h3_ln_split(int R) { return use_small_tiles((R + 127) / 128) && gemm_tile_override() != TILE_BIG; }
+
 hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
   if (a.R <= 0) return hipSuccess;
   if (a.Nout % TB || a.K % kKB || a.K0 % kKB || a.K0 <= 0 || a.K0 > a.K || (a.K0 < a.K && !a.A1.p) || !a.A0.p ||

@@ -124,6 +124,7 @@ hipError_t positional_encoding(const PEArgs& a, hipStream_t st);
 hipError_t kpt_extent(const float* kpts, int B, int n, float* size_out, hipStream_t st);
 
 // In place (planes == null, PREC_X6) or into a plane image of K = 512 (PREC_H3).
+bool gemm_h3_ln_split(int R);
 hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, _Float16* planes, int rows_pad,
                               int* ovf, hipStream_t st);
 // y[r] = dot(x[r,:256], w) + b ; optional sigmoid

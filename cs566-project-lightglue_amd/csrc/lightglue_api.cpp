@@ -703,8 +703,14 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         GemmH3Args g = gemm_h3_base();
         g.A0 = image(w.Xp, D); g.K0 = D; g.A1 = image(h->fold ? w.Cp : w.Mp, D); g.K = 2 * D;
         wplanes(g, bw.W1); g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D;
-        g.Yp = w.Hp; g.yps = (long long)RP * 2 * D; g.yrows_pad = RP; g.ln_g = Wb + bw.g; g.ln_b = Wb + bw.be;
-        LG_HIP(gemmh(g, EPI_LN_GELU));
+        if (gemm_h3_ln_split(R)) {  // small R: 64x64-tile GEMM into H1, then the LN + GELU row kernel
+          g.Y = w.H1; g.ldy = 2 * D;
+          LG_HIP(gemmh(g, EPI_STORE));
+          LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, w.Hp, RP, w.ovf, st));
+        } else {
+          g.Yp = w.Hp; g.yps = (long long)RP * 2 * D; g.yrows_pad = RP; g.ln_g = Wb + bw.g; g.ln_b = Wb + bw.be;
+          LG_HIP(gemmh(g, EPI_LN_GELU));
+        }
         g = gemm_h3_base();
         g.A0 = image(w.Hp, 2 * D); g.K0 = 2 * D; g.K = 2 * D; wplanes(g, bw.W2); g.bias = Wb + bw.b2;
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;

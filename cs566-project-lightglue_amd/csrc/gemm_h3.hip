@@ -578,8 +578,10 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
 }
 
 // fp32 rows -> plane image; one thread per 8-element chunk
+// (xc != nullptr: the fp32 rows are also copied to xc, row stride K -- the residual stream's
+// initial value taken in the same read)
 __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
-                                      int* ovf) {
+                                      int* ovf, float* xc) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int nch = K / 8;
   bool bad = false;
@@ -587,6 +589,11 @@ __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Flo
     const int r = (int)(i / nch), c = (int)(i % nch);
     const float* p = x + (size_t)r * ld + c * 8;
     const f32x4 v0 = *reinterpret_cast<const f32x4*>(p), v1 = *reinterpret_cast<const f32x4*>(p + 4);
+    if (xc) {
+      float* q = xc + (size_t)r * K + c * 8;
+      *reinterpret_cast<f32x4*>(q) = v0;
+      *reinterpret_cast<f32x4*>(q + 4) = v1;
+    }
     f16x8 h, l;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -605,12 +612,12 @@ __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Flo
 }
 
 hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0, int* ovf,
-                          hipStream_t st) {
+                          hipStream_t st, float* xcopy) {
   if (R <= 0) return hipSuccess;
   if (K % kKB || rows_pad < row0 + R) return hipErrorInvalidValue;
   const size_t n = (size_t)R * (K / 8);
   hipLaunchKernelGGL(rows_to_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, R, K, ld, planes,
-                     rows_pad, row0, ovf);
+                     rows_pad, row0, ovf, xcopy);
   return hipGetLastError();
 }
 

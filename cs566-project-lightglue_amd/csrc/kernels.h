@@ -87,9 +87,9 @@ struct GemmH3Args {
 };
 hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st);
 // fp32 rows [R][K] (row stride ld) -> rows row0 .. row0+R-1 of a plane image (rows_pad), with
-// the fp16-range guard
+// the fp16-range guard; xcopy (optional) also receives the fp32 rows, row stride K
 hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0, int* ovf,
-                          hipStream_t st);
+                          hipStream_t st, float* xcopy = nullptr);
 
 // Attention over head-major Q/K/V ([set][b][h][n][64]); O written row-major into ctx
 // [rows][256] at column h*64 (rows in GEMM order).  Two "sets" per launch (blockIdx.z).

@@ -623,9 +623,16 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       LG_HIP(gemm(g, EPI_STORE, 1));
     }
   } else {
-    LG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
-    LG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
-    if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, B * (M + N), D, D, w.Xp, RP, 0, w.ovf, st));
+    const bool a16 = ((uintptr_t)in->descriptors0 % 16 == 0) && ((uintptr_t)in->descriptors1 % 16 == 0);
+    if (prec == PREC_H3 && a16) {
+      // residual stream and its plane image from one read of the descriptors
+      LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, w.ovf, st, w.X));
+      LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, w.ovf, st, w.X + (size_t)B * M * D));
+    } else {
+      LG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
+      LG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
+      if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, B * (M + N), D, D, w.Xp, RP, 0, w.ovf, st));
+    }
   }
 
   // ---- keypoint normalisation + positional encoding (lightglue.py:455-456,490-494)

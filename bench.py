@@ -4,6 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--npts N]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py spawns the N ranks itself
+(torch.multiprocessing.spawn before the parent touches the GPU, like the reference's
+gluefactory/train.py:696); under torch.distributed.run it joins the launcher's process group.
+
 Workload (BASELINE.json configs[2]): SuperPoint-shaped synthetic pairs, N=2048 keypoints per
 image, 9 layers, no pruning, B=32 pairs per GPU per step (weak scaling: every rank matches its own
 32 pairs; a step also all-gathers the match results to every rank over RCCL when N > 1).
@@ -18,16 +22,19 @@ CPU oracle's throughput on this host (rank 0, N=1 only, bounded sample).
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
+import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import lgamd  # noqa: E402,F401
-from lightglue_amd import LightGlue  # noqa: E402
+from lightglue_amd import parallel  # noqa: E402
 from lightglue_amd.weights import synthetic_state_dict  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
@@ -85,126 +92,186 @@ def total_flops_per_pair(N, d=256, L=9):
     return L * (76 * N * d * d + 14 * N * N * d) + 4 * N * d * d + 2 * N * N * d
 
 
+def cpu_threads():
+    """Host cores this process may use: the launcher's OMP_NUM_THREADS share when set (16 on the
+    GPU box, whose os.cpu_count() reports the whole machine), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    return int(env) if env and env.isdigit() and int(env) > 0 else len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(npts, budget_s):
-    """The CPU oracle (torch-CPU restatement of the reference forward) on this host's cores."""
+    """The CPU oracle (torch-CPU restatement of the reference forward) on this host's cores, with
+    the reference's benchmark() protocol (gluefactory/utils/benchmark.py:7-33): 10 warm-up
+    forwards, then timed forwards (at most r = 100, bounded by `budget_s`), mean and std."""
     import oracle
     from lightglue_amd.weights import synthetic_pair
 
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    torch.set_num_threads(cpu_threads())
     conf = {"filter_threshold": 0.1}
     sd = synthetic_state_dict(conf, seed=0)
     data = synthetic_pair(B=1, M=npts, seed=1)
-    oracle.lightglue_forward(sd, data, conf)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        oracle.lightglue_forward(sd, data, conf)
-        n += 1
-        el = time.perf_counter() - t0
-        if el > budget_s or n >= 50:
-            break
+    with torch.no_grad():
+        for _ in range(10):  # benchmark.py:13-14
+            oracle.lightglue_forward(sd, data, conf)
+        times, t_start = [], time.perf_counter()
+        while len(times) < 100 and (time.perf_counter() - t_start) < budget_s:
+            t0 = time.perf_counter()
+            oracle.lightglue_forward(sd, data, conf)
+            times.append((time.perf_counter() - t0) * 1e3)
+    t = np.array(times)
     return {
-        "value": n / el,
+        "value": 1000.0 / t.mean(),
         "unit": "image-pairs/s",
         "cores": torch.get_num_threads(),
         "kind": "port",
-        "sample": f"{n} pairs x N={npts} (B=1, 9 layers, fp32) in {el:.1f}s, torch-CPU oracle (oracle/lightglue_ref.py)",
+        "mean_ms": round(float(t.mean()), 2),
+        "std_ms": round(float(t.std()), 2),
+        "sample": f"benchmark() protocol: 10 warm-ups + {len(t)} timed forwards of 1 pair x N={npts} "
+                  f"(B=1, 9 layers, fp32), torch-CPU oracle (oracle/lightglue_ref.py), "
+                  f"{torch.get_num_threads()} threads",
     }
 
 
-def main():
+class _CpuStandIn:
+    """--selftest-cpu: a stand-in matcher with the forward() contract (no GPU, no compute) so the
+    launch / sharding / gather / timing logic of this script runs on CPU with gloo."""
+
+    last_precision_used = "none"
+
+    def __call__(self, data):
+        b, m = data["keypoints0"].shape[:2]
+        n = data["keypoints1"].shape[1]
+        return {
+            "matches0": torch.full((b, m), -1, dtype=torch.int64),
+            "matches1": torch.full((b, n), -1, dtype=torch.int64),
+            "matching_scores0": torch.zeros((b, m)),
+            "matching_scores1": torch.zeros((b, n)),
+        }
+
+
+def cpu_pairs(B, N, dim, seed):
+    g = torch.Generator().manual_seed(seed)
+    k = torch.rand((B, N, 2), generator=g) * 640
+    d = torch.nn.functional.normalize(torch.randn((B, N, dim), generator=g), dim=-1)
+    isz = torch.full((B, 2), 640.0)
+    return {"keypoints0": k, "keypoints1": k.clone(), "descriptors0": d, "descriptors1": d.clone(),
+            "view0": {"image_size": isz}, "view1": {"image_size": isz}}
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="pairs per GPU per step")
     ap.add_argument("--npts", type=int, default=2048)
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work (0 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of timed CPU-baseline work (0 = skip)")
     ap.add_argument("--precision", default="auto", choices=["auto", "bf16x6"])
-    args = ap.parse_args()
+    ap.add_argument("--selftest-cpu", action="store_true",
+                    help="CPU/gloo rehearsal of the launch and gather logic with a stand-in matcher")
+    return ap.parse_args(argv)
 
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawned(rank, args, port):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(args.gpus),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    run(args)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU; the parent never touches the GPU (no exec after GPU init)
+        mp.spawn(_spawned, nprocs=args.gpus, args=(args, _free_port()), join=True)
+        return
+    run(args)
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     distributed = world > 1
+    selftest = args.selftest_cpu
     if distributed:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        if selftest:
+            dist.init_process_group("gloo")
+        else:
+            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    conf = {"filter_threshold": 0.1}
-    model = LightGlue({**conf, "precision": args.precision}).eval().to(device)
-    sd = synthetic_state_dict(conf, seed=0)
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     B, N = args.batch, args.npts
-    data = gpu_pairs(B, N, 256, seed=1 + rank, device=device)
+    conf = {"filter_threshold": 0.1}
+    if selftest:
+        device = torch.device("cpu")
+        model = _CpuStandIn()
+        data = cpu_pairs(B * world, N, 256, seed=1)
+    else:
+        from lightglue_amd import LightGlue
+
+        device = torch.device("cuda", local)
+        model = LightGlue({**conf, "precision": args.precision}).eval().to(device)
+        sd = synthetic_state_dict(conf, seed=0)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+        # every rank holds the same global batch (B pairs per GPU) and matches its shard
+        data = gpu_pairs(B * world, N, 256, seed=1, device=device)
+
+    def sync():
+        if not selftest:
+            torch.cuda.synchronize()
 
     def step():
+        if distributed:  # this rank's B pairs, then the RCCL all-gather of the match results (SURVEY §8e)
+            return parallel.match_static(model, data)
         with torch.no_grad():
-            pred = model(data)
-        if distributed:  # RCCL all-gather of the match results (SURVEY §8e)
-            packed = torch.cat([pred["matches0"].float(), pred["matches1"].float(),
-                                pred["matching_scores0"], pred["matching_scores1"]], 1)
-            out = torch.empty((world,) + packed.shape, device=device, dtype=packed.dtype)
-            dist.all_gather_into_tensor(out, packed)
-        return pred
+            return model(data)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if distributed:
         dist.barrier()
     # timed region: HIP events only around the roofline kernel (the attention launches)
-    model.profile_enable(True, only=("attention",))
-    torch.cuda.synchronize()
+    if not selftest:
+        model.profile_enable(True, only=("attention",))
+    sync()
+    if distributed:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pred = step()
-    torch.cuda.synchronize()
+    sync()
     if distributed:
         dist.barrier()
     el = time.perf_counter() - t0
-    att_ms, att_n, att_fl, att_by = model.profile_read("attention")
-    # per-family breakdown from a separate, untimed pass with every family evented
-    bsteps = min(args.steps, 3)
-    model.profile_enable(True)
-    for _ in range(bsteps):
-        step()
-    torch.cuda.synchronize()
-    gem_ms, gem_n, gem_fl, _ = model.profile_read("gemm")
-    asg_ms, asg_n, _, asg_by = model.profile_read("assign")
-    model.profile_enable(False)
-    if distributed:
-        t = torch.tensor([el], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-
-    pairs = B * args.steps * world
-    value = pairs / el
-    prec = model.last_precision_used
-    peak, kname, peak_note = PEAKS[prec]
-    traffic, traffic_src = measured_traffic(kname)
-    result = {
-        "metric": "image-pairs/sec at N=2048 kpts, d=256; HPatches AUC@3px parity",
-        "value": round(value, 3),
-        "unit": "image-pairs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1000.0 * el / args.steps, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (SuperPoint-shaped keypoints/descriptors, random-init weights)",
-        "config": {
-            "workload": "configs[2]: SuperPoint+LightGlue N=2048, 9 layers, no pruning, batch=32 per GPU",
-            "npts": N, "descriptor_dim": 256, "n_layers": 9, "pairs_per_gpu_per_step": B,
-            "global_batch": B * world, "parallelism": f"pair-sharded x{world} (+RCCL all-gather of matches)",
-            "matrix_operands": prec,
-        },
-        "achieved_tflops_total": round(total_flops_per_pair(N) * pairs / el / 1e12, 2),
-        "roofline": {
+    result_kernels, roofline = None, None
+    if not selftest:
+        att_ms, att_n, att_fl, att_by = model.profile_read("attention")
+        # per-family breakdown from a separate, untimed pass with every family evented
+        bsteps = min(args.steps, 3)
+        model.profile_enable(True)
+        for _ in range(bsteps):
+            step()
+        sync()
+        gem_ms, gem_n, gem_fl, _ = model.profile_read("gemm")
+        asg_ms, asg_n, _, asg_by = model.profile_read("assign")
+        model.profile_enable(False)
+        prec = model.last_precision_used
+        peak, kname, peak_note = PEAKS[prec]
+        traffic, traffic_src = measured_traffic(kname)
+        roofline = {
             "kernel": f"{kname} (flash self/cross attention, {prec} fp32-accurate products)",
             "bound": "mfma",
             "achieved": round(att_fl / (att_ms * 1e-3) / 1e12, 2) if att_ms > 0 else None,
@@ -217,15 +284,47 @@ def main():
             "launches": att_n,
             "avg_launch_ms": round(att_ms / max(att_n, 1), 4),
             "algorithmic_flops_per_launch": att_fl / max(att_n, 1),
-        },
-        "kernels": {
+        }
+        result_kernels = {
             "attention_ms_per_step": round(att_ms / args.steps, 3),
             "breakdown_note": f"gemm/assign from {bsteps} untimed steps with every kernel family evented",
             "gemm_ms_per_step": round(gem_ms / bsteps, 3),
             "gemm_tflops": round(gem_fl / (gem_ms * 1e-3) / 1e12, 2) if gem_ms > 0 else None,
             "assign_ms_per_step": round(asg_ms / bsteps, 3),
             "assign_gbs": round(asg_by / (asg_ms * 1e-3) / 1e9, 1) if asg_ms > 0 else None,
+        }
+    if distributed:  # max over ranks of the timed region
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    pairs = B * args.steps * world  # every rank matched B pairs per step
+    value = pairs / el
+    result = {
+        "metric": "image-pairs/sec at N=2048 kpts, d=256; HPatches AUC@3px parity",
+        "value": round(value, 3),
+        "unit": "image-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * el / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SuperPoint-shaped keypoints/descriptors, random-init weights)"
+                + (" [CPU self-test: stand-in matcher, no compute]" if selftest else ""),
+        "config": {
+            "workload": "configs[2]: SuperPoint+LightGlue N=2048, 9 layers, no pruning, batch=32 per GPU",
+            "npts": N, "descriptor_dim": 256, "n_layers": 9, "pairs_per_gpu_per_step": B,
+            "global_batch": B * world,
+            "parallelism": f"pair-sharded x{world}" + (" (parallel.match_static: RCCL all-gather of matches)" if distributed else ""),
+            "matrix_operands": model.last_precision_used,
         },
+        "achieved_tflops_total": round(total_flops_per_pair(N) * pairs / el / 1e12, 2),
+        "roofline": roofline,
+        "kernels": result_kernels,
+        "pairs_timed": pairs,
         "matches_per_pair": float((pred["matches0"] > -1).float().sum(1).mean()),
     }
     if rank == 0 and world == 1 and args.cpu_budget > 0:

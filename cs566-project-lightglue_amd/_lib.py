@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LIGHTGLUE_MI355X_LIB", os.path.join(_HERE, "liblightglue_mi355x.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE = 0, -1, -2, -3, -4
 
@@ -70,7 +70,11 @@ class LGInputs(ctypes.Structure):
         ("oris0", _P),
         ("scales1", _P),
         ("oris1", _P),
+        ("flags", ctypes.c_int32),
     ]
+
+
+LG_FWD_TRAINING_GATE = 1  # lg_inputs_t.flags: training mode, no early stop / pruning
 
 
 class LGOutputs(ctypes.Structure):
@@ -84,6 +88,8 @@ class LGOutputs(ctypes.Structure):
         ("ref_descriptors1", _P),
         ("prune0", _P),
         ("prune1", _P),
+        ("layer_descriptors0", _P),
+        ("layer_descriptors1", _P),
         ("stop_layer", ctypes.c_int32),
         ("kept0", ctypes.c_int32),
         ("kept1", ctypes.c_int32),

@@ -129,6 +129,7 @@ struct lg_handle {
   std::map<size_t, Planes> planes;
   _Float16* wplanes = nullptr;
   bool loaded = false;
+  bool pass_started = false;  // forward_pass got past argument checks (work was enqueued)
   // fold out_proj / to_out into ffn.0 at load time (env LG_FOLD_OUT_PROJ=0 disables)
   bool fold = true;
   // profiling (lg_profile_enable / lg_profile_read)
@@ -282,6 +283,7 @@ struct Work {
   // PREC_H3 plane images (common.h), rows_pad rows: x, context, message (unfolded out_proj),
   // FFN hidden, input descriptors (input_dim != 256)
   _Float16 *Xp, *Cp, *Mp, *Hp, *Dp;
+  float* Dst;
   int rows_pad;
   size_t R;
   int *flags, *pos, *ind0, *ind1, *ind0b, *ind1b, *counts;
@@ -321,6 +323,7 @@ Work carve(char* base, int B, int M, int N, bool prune, int din) {
   w.Mp = th(2 * RP * D);
   w.Hp = th(2 * RP * 2 * D);
   w.Dp = din != D ? th(2 * RP * din) : nullptr;
+  w.Dst = din != D ? tf(R * din) : nullptr;  // staging for 16-byte-unaligned input descriptors
   w.md = tf(R * D);
   w.z = tf(R);
   w.tok = tf(R);
@@ -537,6 +540,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   using namespace lg;
   if (!h || !in || !out) return fail(LG_E_INVALID, "null argument");
   if (!h->loaded) return fail(LG_E_WEIGHTS, "weights not loaded");
+  h->pass_started = false;
   const lg_config_t& c = h->cfg;
   const int B = in->B, M0 = in->M, N0 = in->N, H = c.num_heads, L = c.n_layers;
   if (B <= 0) return fail(LG_E_INVALID, "batch must be >= 1");
@@ -548,10 +552,15 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     return fail(LG_E_INVALID, "add_scale_ori requires scales0/1 and oris0/1");
   if (!out->matches0 || !out->matches1 || !out->matching_scores0 || !out->matching_scores1)
     return fail(LG_E_INVALID, "missing output tensor");
-  const bool do_stop = c.depth_confidence > 0.f, do_prune = c.width_confidence > 0.f;
+  // training-mode gating (lightglue.py:502-503): no early stop, no pruning
+  const bool gated = (in->flags & LG_FWD_TRAINING_GATE) != 0;
+  const bool do_stop = !gated && c.depth_confidence > 0.f, do_prune = !gated && c.width_confidence > 0.f;
   if ((do_stop || do_prune) && B != 1) return fail(LG_E_INVALID, "pruning / early stop require batch size 1");
+  if ((out->layer_descriptors0 || out->layer_descriptors1) && (do_stop || do_prune))
+    return fail(LG_E_INVALID, "layer_descriptors need early stop and pruning off (training-mode outputs)");
   if (do_prune && (!out->prune0 || !out->prune1)) return fail(LG_E_INVALID, "prune0/prune1 outputs required with pruning");
   const Work need = carve(nullptr, B, M0, N0, prune_enabled(c), c.input_dim);
+  const bool din_a16 = ((uintptr_t)in->descriptors0 % 16 == 0) && ((uintptr_t)in->descriptors1 % 16 == 0);
   if (!workspace || workspace_bytes < need.bytes)
     return fail(LG_E_WORKSPACE, "workspace too small: need " + std::to_string(need.bytes));
   LG_HIP(hipSetDevice(h->device));
@@ -603,11 +612,20 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
 
   // ---- input projection (lightglue.py:370-373,486-487); H3 also builds x's plane image
   if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.ovf, 0, sizeof(int), st));
+  h->pass_started = true;
   if (c.input_dim != D) {
     if (prec == PREC_H3) {
       const int din = c.input_dim;
-      LG_HIP(rows_to_planes(in->descriptors0, B * M, din, din, w.Dp, RP, 0, w.ovf, st));
-      LG_HIP(rows_to_planes(in->descriptors1, B * N, din, din, w.Dp, RP, B * M, w.ovf, st));
+      const float* d0 = in->descriptors0;
+      const float* d1 = in->descriptors1;
+      if (!din_a16) {  // rows_to_planes reads 16-byte vectors: stage unaligned inputs first
+        LG_HIP(hipMemcpyAsync(w.Dst, d0, sizeof(float) * B * M * din, hipMemcpyDeviceToDevice, st));
+        LG_HIP(hipMemcpyAsync(w.Dst + (size_t)B * M * din, d1, sizeof(float) * B * N * din, hipMemcpyDeviceToDevice, st));
+        d0 = w.Dst;
+        d1 = w.Dst + (size_t)B * M * din;
+      }
+      LG_HIP(rows_to_planes(d0, B * M, din, din, w.Dp, RP, 0, w.ovf, st));
+      LG_HIP(rows_to_planes(d1, B * N, din, din, w.Dp, RP, B * M, w.ovf, st));
       GemmH3Args g = gemm_h3_base();
       g.A0 = image(w.Dp, din); g.K0 = din; g.K = din; wplanes(g, h->Wi);
       g.bias = Wb + h->bi; g.R = B * (M + N); g.Nout = D; g.Y = w.X; g.ldy = D;
@@ -623,8 +641,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       LG_HIP(gemm(g, EPI_STORE, 1));
     }
   } else {
-    const bool a16 = ((uintptr_t)in->descriptors0 % 16 == 0) && ((uintptr_t)in->descriptors1 % 16 == 0);
-    if (prec == PREC_H3 && a16) {
+    if (prec == PREC_H3 && din_a16) {
       // residual stream and its plane image from one read of the descriptors
       LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, w.ovf, st, w.X));
       LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, w.ovf, st, w.X + (size_t)B * M * D));
@@ -741,6 +758,15 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         LG_HIP(gemm(g, EPI_STORE, 1));
       }
     }
+    // training-mode outputs: every layer's descriptors (lightglue.py:521-524)
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float* dst = s2 == 0 ? out->layer_descriptors0 : out->layer_descriptors1;
+      if (!dst) continue;
+      const int n = s2 == 0 ? M : N;
+      const size_t row = sizeof(float) * (size_t)n * D;
+      LG_HIP(hipMemcpy2DAsync(reinterpret_cast<char*>(dst) + row * i, row * L, w.X + (s2 == 0 ? 0 : (size_t)B * M * D),
+                              row, row, B, hipMemcpyDeviceToDevice, st));
+    }
     if (i == L - 1) break;
 
     // ---- early stop (lightglue.py:527-531, check_if_stop :595-606; thresholds per :581-584)
@@ -842,7 +868,10 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
   if (!h || !in || !out) return fail(LG_E_INVALID, "null argument");
   const int first = h->cfg.precision == LG_PREC_X6 ? lg::PREC_X6 : lg::PREC_H3;
   int rc = forward_pass(h, in, out, workspace, workspace_bytes, stream, first);
-  if (rc != LG_OK || first != lg::PREC_H3) return rc;
+  // a failed pass is re-checked too: a value outside the fp16 range turns into inf/NaN, which can
+  // make the pass fail (e.g. NaN matchability prunes every point) where bf16x6 would not
+  if (first != lg::PREC_H3 || (rc != LG_OK && rc != LG_E_INVALID)) return rc;
+  if (rc == LG_E_INVALID && !h->pass_started) return rc;  // argument error: nothing was enqueued
   // fp16-range guard: an operand outside the fp16 range makes the fp16x3 result unreliable;
   // recompute the whole forward in bf16x6 (full fp32 range) -- rare by design
   const Work w = carve((char*)workspace, in->B, in->M, in->N, prune_enabled(h->cfg), h->cfg.input_dim);

@@ -13,7 +13,9 @@ Deliberate behaviour differences from the reference:
   crashes in ``torch.stack([])``, :572);
 * without ``view*['image_size']`` the keypoints are normalised by their extent (:25-26) instead of
   raising ``UnboundLocalError`` (:452-455);
-* ``ref_descriptors*`` is ``[B, 1, M', 256]`` (final layer only, as the reference's eval path).
+* ``ref_descriptors*`` is ``[B, 1, M', 256]`` in eval mode and ``[B, L, M, 256]`` (every layer) in
+  training mode, as the reference (:521-524,572); training mode also turns early stop and pruning
+  off (:502-503).  There is no autograd: a training-mode call with gradients enabled raises.
 """
 import ctypes
 import warnings
@@ -135,6 +137,7 @@ class LightGlue(nn.Module):
         self._handle_device = None
         self._weights_key = None
         self._weight_entries = None
+        self._weight_modules = None
         self._ws = None
 
         state_dict = None
@@ -218,13 +221,22 @@ class LightGlue(nn.Module):
             self._weights_key = self._weights_signature()
         return lib
 
+    def reload_weights(self):
+        """Force the next forward to re-upload every parameter.  Needed only after writes the
+        forward cannot see: in-place writes through ``p.data`` (``p.data.copy_(...)``, EMA
+        updates) bump the version counter of a temporary tensor, not of ``p``."""
+        self._weights_key = None
+
     def _weights_signature(self):
-        """(data_ptr, _version) of every parameter / persistent buffer, from a cached list of
-        (owner dict, name, tensor): ~70 us per forward instead of ~800 us for state_dict() + key
-        (the forward's host time sits between two GPU forwards).  A replaced tensor object (owner
-        dict no longer holds it) rebuilds the list; .to()/.cuda() clear it through _apply."""
+        """(data_ptr, _version) of every parameter / persistent buffer plus the identity of every
+        submodule, from a cached list of (owner dict, name, tensor): ~0.1 ms per forward instead of
+        ~0.8 ms for state_dict() + key (the forward's host time sits between two GPU forwards).
+        A replaced submodule (``model.log_assignment[3] = ...``) or tensor object rebuilds the list;
+        .to()/.cuda() clear it through _apply.  Writes through ``p.data`` are not seen: call
+        :meth:`reload_weights` after them."""
         while True:
-            if self._weight_entries is None:
+            mods = tuple(map(id, self.modules()))
+            if self._weight_entries is None or self._weight_modules != mods:
                 ent = []
                 for mod in self.modules():
                     for n, t in mod._parameters.items():
@@ -234,7 +246,8 @@ class LightGlue(nn.Module):
                         if t is not None and n not in mod._non_persistent_buffers_set:
                             ent.append((mod._buffers, n, t))
                 self._weight_entries = ent
-            sig = []
+                self._weight_modules = mods
+            sig = [mods]
             for d, n, t in self._weight_entries:
                 if d.get(n) is not t:
                     self._weight_entries = None
@@ -289,18 +302,28 @@ class LightGlue(nn.Module):
             sc0, o0 = per_point(data["scales0"]), per_point(data["oris0"])
             sc1, o1 = per_point(data["scales1"]), per_point(data["oris1"])
 
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "lightglue_amd: the HIP forward has no autograd; training is out of scope (SURVEY.md §2). "
+                "Use torch.no_grad() or .eval()"
+            )
         lib = self._ensure_handle(device)
-        pruning = c.width_confidence > 0 or c.depth_confidence > 0
+        # early stop / pruning only in eval mode (lightglue.py:502-503)
+        pruning = (c.width_confidence > 0 or c.depth_confidence > 0) and not self.training
         if pruning and b != 1:
             raise AssertionError("pruning / early stop require batch size 1")  # :528,533
-        L = int(c.n_layers)
+        L, dd = int(c.n_layers), int(c.descriptor_dim)
         m0 = torch.empty((b, m), dtype=torch.int64, device=device)
         m1 = torch.empty((b, n), dtype=torch.int64, device=device)
         ms0 = torch.empty((b, m), dtype=torch.float32, device=device)
         ms1 = torch.empty((b, n), dtype=torch.float32, device=device)
         la = torch.empty((b, m + 1, n + 1), dtype=torch.float32, device=device)
-        rd0 = torch.empty((b, m, 256), dtype=torch.float32, device=device)
-        rd1 = torch.empty((b, n, 256), dtype=torch.float32, device=device)
+        if self.training:  # every layer's descriptors, torch.stack(all_desc0, 1) (:521-524,572)
+            rd0 = torch.empty((b, L, m, dd), dtype=torch.float32, device=device)
+            rd1 = torch.empty((b, L, n, dd), dtype=torch.float32, device=device)
+        else:
+            rd0 = torch.empty((b, m, dd), dtype=torch.float32, device=device)
+            rd1 = torch.empty((b, n, dd), dtype=torch.float32, device=device)
         p0 = torch.empty((b, m), dtype=torch.int64, device=device)
         p1 = torch.empty((b, n), dtype=torch.int64, device=device)
 
@@ -308,8 +331,11 @@ class LightGlue(nn.Module):
         _lib.check(lib.lg_workspace_bytes(self._handle, b, m, n, ctypes.byref(ws_bytes)), "lg_workspace_bytes")
         if self._ws is None or self._ws.numel() < ws_bytes.value or self._ws.device != device:
             self._ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=device)
-        inp = _lib.LGInputs(b, m, n, *[_ptr(t) for t in (k0, k1, d0, d1, s0, s1, sc0, o0, sc1, o1)])
-        out = _lib.LGOutputs(*[_ptr(t) for t in (m0, m1, ms0, ms1, la, rd0, rd1, p0, p1)], 0, 0, 0, 0)
+        flags = _lib.LG_FWD_TRAINING_GATE if self.training else 0
+        inp = _lib.LGInputs(b, m, n, *[_ptr(t) for t in (k0, k1, d0, d1, s0, s1, sc0, o0, sc1, o1)], flags)
+        final, layers = (None, rd0) if self.training else (rd0, None)
+        final1, layers1 = (None, rd1) if self.training else (rd1, None)
+        out = _lib.LGOutputs(*[_ptr(t) for t in (m0, m1, ms0, ms1, la, final, final1, p0, p1, layers, layers1)], 0, 0, 0, 0)
         stream = torch.cuda.current_stream(device).cuda_stream
         _lib.check(
             lib.lg_forward(self._handle, ctypes.byref(inp), ctypes.byref(out), _ptr(self._ws), ws_bytes.value, ctypes.c_void_p(stream)),
@@ -319,7 +345,7 @@ class LightGlue(nn.Module):
         kept0, kept1 = out.kept0, out.kept1
         if kept0 != m or kept1 != n:  # log_assignment was written for the kept points
             la = la.view(-1)[: b * (kept0 + 1) * (kept1 + 1)].view(b, kept0 + 1, kept1 + 1)
-        if c.width_confidence > 0:
+        if c.width_confidence > 0 and not self.training:
             prune0, prune1 = p0, p1
         else:
             prune0 = torch.full((b, m), float(L), device=device)
@@ -329,8 +355,8 @@ class LightGlue(nn.Module):
             "matches1": m1,
             "matching_scores0": ms0,
             "matching_scores1": ms1,
-            "ref_descriptors0": rd0[:, None, :kept0],
-            "ref_descriptors1": rd1[:, None, :kept1],
+            "ref_descriptors0": rd0 if self.training else rd0[:, None, :kept0],
+            "ref_descriptors1": rd1 if self.training else rd1[:, None, :kept1],
             "log_assignment": la,
             "prune0": prune0,
             "prune1": prune1,

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define LG_ABI_VERSION 2
+#define LG_ABI_VERSION 3
 
 enum {
   LG_OK = 0,
@@ -78,7 +78,13 @@ typedef struct {
   const float* oris0;           /* device [B,M] */
   const float* scales1;         /* device [B,N] */
   const float* oris1;           /* device [B,N] */
+  int32_t flags;                /* OR of LG_FWD_*: per-call options (no reference counterpart) */
 } lg_inputs_t;
+
+/* lg_inputs_t.flags
+ *   LG_FWD_TRAINING_GATE  the module is in training mode: early stop and point pruning are off
+ *                         whatever the config says (lightglue.py:502-503 `... and not self.training`) */
+enum { LG_FWD_TRAINING_GATE = 1 };
 
 typedef struct {
   int64_t* matches0;            /* device [B,M]  (required) */
@@ -90,6 +96,10 @@ typedef struct {
   float* ref_descriptors1;      /* device [B,N,256] or NULL */
   int64_t* prune0;              /* device [B,M] or NULL: layer count per point (lightglue.py:511,540,564) */
   int64_t* prune1;              /* device [B,N] or NULL */
+  float* layer_descriptors0;    /* device [B,L,M,256] or NULL: descriptors after every layer (the
+                                 * reference's training-mode ref_descriptors, lightglue.py:521-524,
+                                 * torch.stack(all_desc0, 1) at :572); needs pruning / early stop off */
+  float* layer_descriptors1;    /* device [B,L,N,256] or NULL */
   int32_t stop_layer;           /* host out: index of the last executed layer */
   int32_t kept0, kept1;         /* host out: M', N' after width pruning (= M, N without) */
   int32_t precision_used;       /* host out: 0 = fp16x3, 1 = bf16x6 (LG_PREC_X6, or the guarded rerun) */

@@ -35,13 +35,31 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert lib.lg_abi_version() == _lib.ABI_VERSION
 
 
-def test_ctypes_structs_match_header_layout():
-    # lg_config_t: 5 x int32, pad, 3 doubles, int32 precision, pad -> 56 bytes
-    assert ctypes.sizeof(_lib.LGConfig) == 56
-    assert _lib.LGConfig.precision.offset == 48
-    assert ctypes.sizeof(_lib.LGInputs) == 16 + 10 * 8
-    # lg_outputs_t: 9 pointers, stop_layer, kept0, kept1, precision_used
-    assert ctypes.sizeof(_lib.LGOutputs) == 9 * 8 + 16
+def test_ctypes_structs_match_header_layout(tmp_path):
+    """Every field offset and struct size of the ctypes mirrors equals what a C compiler makes of
+    include/lightglue_mi355x.h (gcc on a generated offsetof table)."""
+    import subprocess
+
+    structs = {"lg_config_t": _lib.LGConfig, "lg_inputs_t": _lib.LGInputs, "lg_outputs_t": _lib.LGOutputs}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{os.path.join(ROOT, "include", "lightglue_mi355x.h")}"',
+             "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines += ["return 0; }"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        c, f, v = line.split()
+        got[(c, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
 
 
 def test_error_path_without_gpu_reports_message():

@@ -85,3 +85,50 @@ def test_shard_range_covers_batch():
                 a, b = shard_range(B, world, r)
                 idx += list(range(a, b))
             assert idx == list(range(B))
+
+
+def _bench_json(cmd, env=None):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, OMP_NUM_THREADS="1")
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable] + cmd, cwd=root, env=e, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_gpus_ranks_itself():
+    """bench.py --gpus 2 without a launcher spawns two ranks (CPU/gloo rehearsal): n_gpus and the
+    pair count cover both ranks, and the step goes through parallel.match_static."""
+    res = _bench_json(["bench.py", "--gpus", "2", "--selftest-cpu", "--steps", "3", "--warmup", "1",
+                       "--batch", "3", "--npts", "32", "--cpu-budget", "0"])
+    assert res["n_gpus"] == 2
+    assert res["pairs_timed"] == 3 * 3 * 2
+    assert res["config"]["global_batch"] == 6
+    assert "match_static" in res["config"]["parallelism"]
+    assert res["value"] == pytest.approx(res["pairs_timed"] / (res["ms_per_step"] * res["steps"] / 1000.0), rel=1e-2)
+
+
+def test_bench_under_torchrun_launcher():
+    port = _free_port()
+    res = _bench_json(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                       "--master-port", str(port), "bench.py", "--gpus", "2", "--selftest-cpu", "--steps", "2",
+                       "--warmup", "1", "--batch", "2", "--npts", "16", "--cpu-budget", "0"])
+    assert res["n_gpus"] == 2 and res["pairs_timed"] == 2 * 2 * 2
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--selftest-cpu", "--cpu-budget", "0"], cwd=root,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)

@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "../cs566-project-lightglue_amd/csrc/attention.hip"
+#include "attn_h3_legacy.hip"
 
 namespace lg {
 

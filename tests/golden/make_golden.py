@@ -124,6 +124,13 @@ def sha(arrs):
 # unpruned logits).
 PRUNE_BIAS = [-2.97, -2.32, -2.90, -2.29, -3.00, -2.80, -2.14, -2.37]
 
+# configs[3]-shaped case (N = 2048, width = depth = 0.95): per-layer biases from
+# tools/tune_prune_golden.py -- layers 0..4 prune ~10 % of the points each, layer 5 stops early;
+# every decision threshold sits in a >= 1e-3 gap of the sorted decision logits.  None = keep the
+# recipe value (layers the forward never reaches, and the head of the stopping layer).
+PRUNE2K_TOKEN_BIAS = [2.0127, 2.2824, 1.7838, 1.715, 0.9317, 6.3066, None, None]
+PRUNE2K_MATCH_BIAS = [-2.5056, -2.4873, -1.8882, -3.3078, -2.4224, None, None, None]
+
 # name -> (conf overrides, pair kwargs, weight kwargs, weight overrides, store_full)
 CASES = {
     "tiny_ragged_b2": ({"filter_threshold": 0.1}, dict(B=2, M=48, N=40, seed=11), dict(seed=0), {}, True),
@@ -149,6 +156,19 @@ CASES = {
         {"matchability_bias": PRUNE_BIAS},
         False,
     ),
+    "prune_depth_width_n2048": (
+        {"filter_threshold": 0.1, "width_confidence": 0.95, "depth_confidence": 0.95},
+        dict(B=1, M=2048, N=2048, seed=41),
+        dict(seed=8),
+        {"token_bias": PRUNE2K_TOKEN_BIAS, "matchability_bias": PRUNE2K_MATCH_BIAS},
+        False,
+    ),
+    # configs[4]-shaped forward (N = 4096, the Sinkhorn config's matcher size)
+    "n4096": ({"filter_threshold": 0.1}, dict(B=1, M=4096, seed=1), dict(seed=0), {}, False),
+    # near-tie stress: unsharpened (default-init-like) weights and noisy view-1 descriptors, so
+    # the assignment is nearly flat and many rows / columns have tiny top-1 / top-2 margins
+    "unsharp_n1024": ({"filter_threshold": 0.0}, dict(B=1, M=1024, seed=51, noise=0.3), dict(seed=9, sharpen=False), {}, False),
+    "unsharp_n2048": ({"filter_threshold": 0.0}, dict(B=1, M=2048, seed=52, noise=2.0), dict(seed=10, sharpen=False), {}, False),
     "early_stop_n256": (
         {"filter_threshold": 0.1, "depth_confidence": 0.9},
         dict(B=1, M=256, N=240, seed=23),
@@ -164,7 +184,12 @@ def make_weights(conf, wkw, over):
     L = conf.get("n_layers", 9)
     if "matchability_bias" in over:
         for i in range(L - 1):
-            sd[f"log_assignment.{i}.matchability.bias"][:] = over["matchability_bias"][i]
+            if over["matchability_bias"][i] is not None:
+                sd[f"log_assignment.{i}.matchability.bias"][:] = over["matchability_bias"][i]
+    if "token_bias" in over:
+        for i in range(L - 1):
+            if over["token_bias"][i] is not None:
+                sd[f"token_confidence.{i}.token.0.bias"][:] = over["token_bias"][i]
     if "token_bias_layer" in over:
         li, val = over["token_bias_layer"]
         sd[f"token_confidence.{li}.token.0.bias"][:] = val
@@ -264,27 +289,47 @@ def run_case(lg_mod, name, spec):
     print(f"{name}: layers_run={len(layers)} matches={nm} prune0_min={out['prune0'].min()}", flush=True)
 
 
-def run_sinkhorn(sg_mod):
-    for name, (B, M, N, alpha, iters, seed) in {
-        "sinkhorn_b2_60x50": (2, 60, 50, 1.0, 50, 31),
-        "sinkhorn_b1_257x300": (1, 257, 300, 0.5, 50, 32),
-        "sinkhorn_b1_64x64_it3": (1, 64, 64, 2.0, 3, 33),
-    }.items():
+# Sinkhorn cases: (B, M, N, alpha, iters, seed, full).  Large cases (configs[4]: 4096 x 4096,
+# 50 iterations) store the dustbin row / column, every row's and column's max and argmax with
+# their top-1 / top-2 margins, and 16 evenly spaced full rows instead of the 134 MB Z.
+SINKHORN_CASES = {
+    "sinkhorn_b2_60x50": (2, 60, 50, 1.0, 50, 31, True),
+    "sinkhorn_b1_257x300": (1, 257, 300, 0.5, 50, 32, True),
+    "sinkhorn_b1_64x64_it3": (1, 64, 64, 2.0, 3, 33, True),
+    "sinkhorn_b2_4096x4096": (2, 4096, 4096, 1.0, 50, 34, False),
+}
+
+
+def run_sinkhorn(sg_mod, only=()):
+    for name, (B, M, N, alpha, iters, seed, full) in SINKHORN_CASES.items():
+        if only and name not in only and "sinkhorn" not in only:
+            continue
         rng = np.random.Generator(np.random.PCG64(seed))
         scores = (rng.standard_normal((B, M, N)) * 2.0).astype(np.float32)
         with torch.no_grad():
             Z = sg_mod.log_optimal_transport(torch.from_numpy(scores), torch.tensor(alpha), iters)
         Zi = Z[:, :-1, :-1]
         max0, max1 = Zi.max(2), Zi.max(1)
-        meta = {"B": B, "M": M, "N": N, "alpha": alpha, "iters": iters, "seed": seed, "scale": 2.0}
-        np.savez_compressed(
-            os.path.join(HERE, f"{name}.npz"),
-            Z=Z.numpy(),
+        meta = {"B": B, "M": M, "N": N, "alpha": alpha, "iters": iters, "seed": seed, "scale": 2.0, "full": full}
+        out = dict(
             scores_sha256=np.array(sha({"scores": scores})),
             row_argmax=max0.indices.numpy(),
             col_argmax=max1.indices.numpy(),
             meta_json=np.array(json.dumps(meta)),
         )
+        if full:
+            out["Z"] = Z.numpy()
+        else:
+            rows = np.linspace(0, M, 16).round().astype(np.int64)  # includes the dustbin row M
+            out["sample_rows"] = rows
+            out["Z_rows"] = Z[:, rows].numpy()
+            out["Z_dustbin_col"] = Z[:, :, -1].numpy()
+            out["row_max"] = max0.values.numpy()
+            out["col_max"] = max1.values.numpy()
+            t0, t1 = Zi.topk(2, dim=2).values, Zi.topk(2, dim=1).values
+            out["row_margin"] = (t0[..., 0] - t0[..., 1]).numpy()
+            out["col_margin"] = (t1[:, 0] - t1[:, 1]).numpy()
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
         print(f"{name}: Z range [{Z.min().item():.3f}, {Z.max().item():.3f}]", flush=True)
 
 
@@ -296,8 +341,8 @@ def main():
         if only and name not in only:
             continue
         run_case(lg_mod, name, spec)
-    if not only or "sinkhorn" in only:
-        run_sinkhorn(sg_mod)
+    if not only or any(o.startswith("sinkhorn") for o in only):
+        run_sinkhorn(sg_mod, only)
 
 
 if __name__ == "__main__":

@@ -39,7 +39,12 @@ def case_inputs(meta):
     L = conf.get("n_layers", 9)
     if "matchability_bias" in over:
         for i in range(L - 1):
-            sd[f"log_assignment.{i}.matchability.bias"][:] = over["matchability_bias"][i]
+            if over["matchability_bias"][i] is not None:
+                sd[f"log_assignment.{i}.matchability.bias"][:] = over["matchability_bias"][i]
+    if "token_bias" in over:
+        for i in range(L - 1):
+            if over["token_bias"][i] is not None:
+                sd[f"token_confidence.{i}.token.0.bias"][:] = over["token_bias"][i]
     if "token_bias_layer" in over:
         li, val = over["token_bias_layer"]
         sd[f"token_confidence.{li}.token.0.bias"][:] = val

@@ -2,11 +2,18 @@
 
 Bar (BASELINE north star): match indices bit-exact, matching scores |d| <= 1e-4,
 log-assignment |d| <= 1e-3 (fp32 vs fp64 already differs by 2.2e-3), prune counts exact.
-Rows/columns whose fp64 top-1/top-2 margin is below NEAR_TIE (fixture keys margin0/margin1) are
-reported separately and allowed to flip; with the committed recipe there are none.
+Near-ties: a row / column whose fp64 top-1 / top-2 margin (fixture keys margin0 / margin1) is below
+NEAR_TIE = 1e-4 is not decidable by fp32 arithmetic (the reference's own fp32 result differs from
+fp64 by more than that in log-assignment units); its index may flip and is counted, never silently
+skipped: every forward test reports (rows below NEAR_TIE, flips among them) and asserts that NO
+index flips at a margin >= NEAR_TIE.  With LG_PARITY_REPORT=<path> the counts are appended there
+as JSON lines (profiles/<round>/parity_report.jsonl).
 Both matrix-core operand formats are held to the same bar: "auto" (fp16x3, the default) and
 "bf16x6" (the guarded fallback).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -14,9 +21,11 @@ import torch
 import lgamd  # noqa: F401
 from golden_util import case_inputs, case_names, load, sinkhorn_inputs, sinkhorn_names
 
-NEAR_TIE = 2e-3
+NEAR_TIE = 1e-4
 SCORE_TOL = 1e-4
 LA_TOL = 1e-3
+# descriptors after 9 layers: |d| <= DESC_ATOL + DESC_RTOL * |ref|
+DESC_ATOL, DESC_RTOL = 5e-4, 1e-4
 
 pytestmark = pytest.mark.gpu
 
@@ -37,13 +46,31 @@ def _gpu_data(data):
     return d
 
 
-def check_against_golden(pred, g):
+def _report(**kw):
+    path = os.environ.get("LG_PARITY_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(kw) + "\n")
+
+
+def check_against_golden(pred, g, label=""):
+    """Assert the golden bar; return the near-tie / error report of this forward."""
     m0, m1 = pred["matches0"].cpu().numpy(), pred["matches1"].cpu().numpy()
     ok0 = np.ones_like(m0, dtype=bool)
     ok1 = np.ones_like(m1, dtype=bool)
     if "margin0" in g:
         ok0 = g["margin0"] >= NEAR_TIE
         ok1 = g["margin1"] >= NEAR_TIE
+    f0, f1 = m0 != g["matches0"], m1 != g["matches1"]
+    rep = {
+        "case": label,
+        "near_tie_rows": int((~ok0).sum()), "near_tie_cols": int((~ok1).sum()),
+        "flips_near_tie": int((f0 & ~ok0).sum() + (f1 & ~ok1).sum()),
+        "flips_decidable": int((f0 & ok0).sum() + (f1 & ok1).sum()),
+    }
+    if "margin0" in g:
+        rep["min_margin"] = float(min(g["margin0"].min(), g["margin1"].min()))
+        rep["rows_margin_below_1e-3"] = int((g["margin0"] < 1e-3).sum() + (g["margin1"] < 1e-3).sum())
     np.testing.assert_array_equal(m0[ok0], g["matches0"][ok0])
     np.testing.assert_array_equal(m1[ok1], g["matches1"][ok1])
     s0, s1 = pred["matching_scores0"].cpu().numpy(), pred["matching_scores1"].cpu().numpy()
@@ -51,6 +78,8 @@ def check_against_golden(pred, g):
     same1 = ok1 & ((m1 > -1) == (g["matches1"] > -1))
     np.testing.assert_allclose(s0[same0], g["matching_scores0"][same0], atol=SCORE_TOL, rtol=0)
     np.testing.assert_allclose(s1[same1], g["matching_scores1"][same1], atol=SCORE_TOL, rtol=0)
+    rep["max_score_err"] = float(max(np.abs(s0[same0] - g["matching_scores0"][same0]).max(initial=0),
+                                     np.abs(s1[same1] - g["matching_scores1"][same1]).max(initial=0)))
     p0, p1 = pred["prune0"].cpu().numpy(), pred["prune1"].cpu().numpy()
     np.testing.assert_array_equal(p0, g["prune0"])
     np.testing.assert_array_equal(p1, g["prune1"])
@@ -66,8 +95,13 @@ def check_against_golden(pred, g):
         np.testing.assert_allclose(la.cpu().numpy(), g["log_assignment"], atol=LA_TOL)
     if "ref_descriptors0" in g:
         k0, k1 = g["ref_descriptors0"].shape[2], g["ref_descriptors1"].shape[2]
-        np.testing.assert_allclose(pred["ref_descriptors0"][:, :, :k0].cpu().numpy(), g["ref_descriptors0"], atol=2e-3, rtol=1e-3)
-        np.testing.assert_allclose(pred["ref_descriptors1"][:, :, :k1].cpu().numpy(), g["ref_descriptors1"], atol=2e-3, rtol=1e-3)
+        r0 = pred["ref_descriptors0"][:, :, :k0].cpu().numpy()
+        r1 = pred["ref_descriptors1"][:, :, :k1].cpu().numpy()
+        np.testing.assert_allclose(r0, g["ref_descriptors0"], atol=DESC_ATOL, rtol=DESC_RTOL)
+        np.testing.assert_allclose(r1, g["ref_descriptors1"], atol=DESC_ATOL, rtol=DESC_RTOL)
+        rep["max_desc_err"] = float(max(np.abs(r0 - g["ref_descriptors0"]).max(), np.abs(r1 - g["ref_descriptors1"]).max()))
+    _report(**rep)
+    return rep
 
 
 @pytest.mark.parametrize("precision", ["auto", "bf16x6"])
@@ -81,7 +115,7 @@ def test_forward_matches_reference_golden(name, precision):
     torch.cuda.synchronize()
     assert model.last_precision_used == ("fp16x3" if precision == "auto" else "bf16x6")
     assert pred["stop_layer"] + 1 == int(g["n_layers_run"])
-    check_against_golden(pred, g)
+    check_against_golden(pred, g, f"{name}/{precision}")
 
 
 @pytest.mark.parametrize("tile,waves,assign", [("big", "8", "fused"), ("small", "4", "fused"), ("small", "2", "unfused")])
@@ -103,7 +137,7 @@ def test_forward_golden_all_launch_shapes(name, tile, waves, assign, monkeypatch
         pred = model(_gpu_data(data))
     torch.cuda.synchronize()
     assert model.last_precision_used == "fp16x3"
-    check_against_golden(pred, g)
+    check_against_golden(pred, g, f"{name}/tile={tile},waves={waves},{assign}")
 
 
 def test_weight_changes_after_first_forward_are_picked_up():
@@ -221,16 +255,31 @@ def test_cpu_inputs_fail_loudly():
 
 @pytest.mark.parametrize("name", sinkhorn_names())
 def test_sinkhorn_matches_reference_golden(name):
+    """configs[4]'s assignment head against the reference: the small cases compare all of Z, the
+    4096 x 4096 x B=2 50-iteration case (the configs[4] shape) 16 sampled rows, the dustbin
+    column, every row / column maximum and every argmax whose top-1 / top-2 margin is >= 1e-4."""
     from lightglue_amd import log_optimal_transport
 
     g = load(name)
     meta = g["meta"]
     scores = torch.from_numpy(sinkhorn_inputs(meta)).cuda()
     Z = log_optimal_transport(scores, torch.tensor(meta["alpha"]), meta["iters"]).cpu()
-    np.testing.assert_allclose(Z.numpy(), g["Z"], atol=1e-4, rtol=1e-5)
     inner = Z[:, :-1, :-1]
-    np.testing.assert_array_equal(inner.max(2).indices.numpy(), g["row_argmax"])
-    np.testing.assert_array_equal(inner.max(1).indices.numpy(), g["col_argmax"])
+    if "Z" in g:
+        np.testing.assert_allclose(Z.numpy(), g["Z"], atol=1e-4, rtol=1e-5)
+        np.testing.assert_array_equal(inner.max(2).indices.numpy(), g["row_argmax"])
+        np.testing.assert_array_equal(inner.max(1).indices.numpy(), g["col_argmax"])
+        return
+    np.testing.assert_allclose(Z[:, g["sample_rows"]].numpy(), g["Z_rows"], atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(Z[:, :, -1].numpy(), g["Z_dustbin_col"], atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(inner.max(2).values.numpy(), g["row_max"], atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(inner.max(1).values.numpy(), g["col_max"], atol=1e-4, rtol=1e-5)
+    r_ok, c_ok = g["row_margin"] >= NEAR_TIE, g["col_margin"] >= NEAR_TIE
+    np.testing.assert_array_equal(inner.max(2).indices.numpy()[r_ok], g["row_argmax"][r_ok])
+    np.testing.assert_array_equal(inner.max(1).indices.numpy()[c_ok], g["col_argmax"][c_ok])
+    _report(case=name, near_tie_rows=int((~r_ok).sum()), near_tie_cols=int((~c_ok).sum()),
+            flips_near_tie=int((inner.max(2).indices.numpy() != g["row_argmax"])[~r_ok].sum()
+                               + (inner.max(1).indices.numpy() != g["col_argmax"])[~c_ok].sum()))
 
 
 @pytest.mark.parametrize(
@@ -317,3 +366,160 @@ def test_profile_family_mask():
     assert att[1] == 2 * 9 and att[0] > 0  # self + cross per layer
     assert gem[1] == 0
     assert gem_all[1] > 0 and gem_all[2] > 0
+
+
+def test_configs2_batch32_equals_golden():
+    """configs[2] shape (N = 2048, 9 layers, B = 32 pairs in one forward): the n2048 golden pair
+    tiled 32 times, every odd pair with its image-1 keypoints permuted.  Every pair must give the
+    golden matches exactly (mapped through its permutation) and scores within 1e-4."""
+    g = load("n2048")
+    conf, sd, data = case_inputs(g["meta"])
+    B, N = 32, data["keypoints1"].shape[1]
+    rng = np.random.default_rng(0)
+    batch = {k: np.repeat(v, B, axis=0) for k, v in data.items()}
+    perms = []
+    for b in range(B):
+        perm = rng.permutation(N) if b % 2 else np.arange(N)
+        batch["keypoints1"][b] = data["keypoints1"][0][perm]
+        batch["descriptors1"][b] = data["descriptors1"][0][perm]
+        perms.append(perm)
+    model = _model(conf, sd)
+    with torch.no_grad():
+        pred = model(_gpu_data(batch))
+    m0, m1 = pred["matches0"].cpu().numpy(), pred["matches1"].cpu().numpy()
+    s0, s1 = pred["matching_scores0"].cpu().numpy(), pred["matching_scores1"].cpu().numpy()
+    for b, perm in enumerate(perms):
+        inv = np.argsort(perm)
+        e0 = np.where(g["matches0"][0] > -1, inv[np.maximum(g["matches0"][0], 0)], -1)
+        np.testing.assert_array_equal(m0[b], e0, err_msg=f"pair {b}")
+        np.testing.assert_array_equal(m1[b], g["matches1"][0][perm], err_msg=f"pair {b}")
+        np.testing.assert_allclose(s0[b], g["matching_scores0"][0], atol=SCORE_TOL, rtol=0)
+        np.testing.assert_allclose(s1[b], g["matching_scores1"][0][perm], atol=SCORE_TOL, rtol=0)
+
+
+@pytest.mark.parametrize("name", [n for n in case_names() if "layer0_desc0" in load(n)])
+def test_every_layer_matches_reference_layers(name):
+    """Training mode returns every layer's descriptors (lightglue.py:521-524,572); each layer is
+    compared with the reference's per-layer outputs stored in the tiny fixtures, so a layer-local
+    regression shows at its own layer instead of after 9 layers of mixing."""
+    g = load(name)
+    conf, sd, data = case_inputs(g["meta"])
+    model = _model(conf, sd).train()
+    with torch.no_grad():
+        pred = model(_gpu_data(data))
+    L = model.conf.n_layers
+    assert pred["ref_descriptors0"].shape[1] == L
+    errs = []
+    for i in range(L):
+        for s in (0, 1):
+            got = pred[f"ref_descriptors{s}"][:, i].cpu().numpy()
+            ref = g[f"layer{i}_desc{s}"]
+            np.testing.assert_allclose(got, ref, atol=DESC_ATOL, rtol=DESC_RTOL, err_msg=f"layer {i} image {s}")
+            errs.append(float(np.abs(got - ref).max()))
+    _report(case=f"{name}/layers", max_desc_err_per_layer=[max(errs[2 * i], errs[2 * i + 1]) for i in range(L)])
+    # training mode: the final outputs are those of the full-depth eval forward
+    model.eval()
+    with torch.no_grad():
+        ev = model(_gpu_data(data))
+    assert torch.equal(ev["matches0"], pred["matches0"])
+    assert torch.equal(ev["ref_descriptors0"][:, 0], pred["ref_descriptors0"][:, -1])
+
+
+def test_training_mode_gates_pruning_and_early_stop():
+    """lightglue.py:502-503: early stop and point pruning only run in eval mode."""
+    g = load("prune_depth_width_n512")
+    conf, sd, data = case_inputs(g["meta"])
+    model = _model(conf, sd)
+    with torch.no_grad():
+        ev = model(_gpu_data(data))
+        model.train()
+        tr = model(_gpu_data(data))
+    assert ev["prune0"].dtype == torch.int64 and int(ev["prune0"].min()) < model.conf.n_layers
+    assert tr["prune0"].dtype == torch.float32 and bool((tr["prune0"] == model.conf.n_layers).all())
+    assert tr["stop_layer"] == model.conf.n_layers - 1
+    assert tr["ref_descriptors0"].shape[1] == model.conf.n_layers
+    off = _model({k: v for k, v in conf.items() if k not in ("width_confidence", "depth_confidence")}, sd)
+    with torch.no_grad():
+        full = off(_gpu_data(data))
+    assert torch.equal(tr["matches0"], full["matches0"])
+
+
+def test_training_mode_with_autograd_raises():
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    model = _model({}, synthetic_state_dict({}, seed=0)).train()
+    with pytest.raises(NotImplementedError):
+        model(_gpu_data(synthetic_pair(B=1, M=16, seed=3)))
+
+
+@pytest.mark.parametrize("name", ["tiny_ragged_b2", "input_proj_n128"])
+def test_unaligned_descriptor_views(name):
+    """Descriptors passed as views 4 bytes past a 16-byte boundary (input_dim 256 and != 256)
+    give exactly the result of the aligned copies."""
+    g = load(name)
+    conf, sd, data = case_inputs(g["meta"])
+    model = _model(conf, sd)
+    d = _gpu_data(data)
+    with torch.no_grad():
+        ref = model(d)
+        for k in ("descriptors0", "descriptors1"):
+            t = d[k]
+            buf = torch.empty(t.numel() + 1, device=t.device, dtype=t.dtype)
+            view = buf[1:].view(t.shape)
+            view.copy_(t)
+            assert view.data_ptr() % 16 == 4
+            d[k] = view
+        got = model(d)
+    for k in ("matches0", "matches1", "matching_scores0", "matching_scores1", "log_assignment"):
+        assert torch.equal(got[k], ref[k]), k
+
+
+def test_submodule_replacement_and_data_writes_are_picked_up():
+    """a replaced submodule is seen by the next forward; writes through p.data are not
+    (they bypass the version counter) until reload_weights()."""
+    from lightglue_amd import LightGlue
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1}
+    sd = synthetic_state_dict(conf, seed=0)
+    data = _gpu_data(synthetic_pair(B=1, M=200, N=180, seed=4))
+    model = _model(conf, sd)
+    sd2 = {k: v.copy() for k, v in sd.items()}
+    sd2["log_assignment.8.final_proj.weight"] = sd2["log_assignment.8.final_proj.weight"] * np.float32(0.5)
+    ref = _model(conf, sd2)
+    with torch.no_grad():
+        base = model(data)
+        new = type(model.log_assignment[8])(256).cuda()
+        new.load_state_dict({"matchability.weight": torch.from_numpy(sd2["log_assignment.8.matchability.weight"]),
+                             "matchability.bias": torch.from_numpy(sd2["log_assignment.8.matchability.bias"]),
+                             "final_proj.weight": torch.from_numpy(sd2["log_assignment.8.final_proj.weight"]),
+                             "final_proj.bias": torch.from_numpy(sd2["log_assignment.8.final_proj.bias"])})
+        model.log_assignment[8] = new
+        swapped = model(data)
+        r = ref(data)
+        assert torch.equal(swapped["log_assignment"], r["log_assignment"])
+        assert not torch.equal(swapped["log_assignment"], base["log_assignment"])
+        # .data write: invisible until reload_weights()
+        model2 = _model(conf, sd)
+        model2(data)
+        model2.log_assignment[8].final_proj.weight.data.mul_(0.5)
+        model2.reload_weights()
+        assert torch.equal(model2(data)["log_assignment"], r["log_assignment"])
+    assert isinstance(model, LightGlue)
+
+
+def test_fp16_range_guard_with_pruning():
+    """with width pruning on, an out-of-range forward must still end in the bf16x6
+    result, not in an 'all keypoints pruned' error from NaN matchability."""
+    from lightglue_amd.weights import synthetic_pair
+
+    g = load("prune_width_n512")
+    conf, sd, data = case_inputs(g["meta"])
+    data = synthetic_pair(B=1, M=256, N=240, seed=2)
+    data["descriptors0"] = data["descriptors0"] * np.float32(2.0e5)
+    auto, x6 = _model(conf, sd, "auto"), _model(conf, sd, "bf16x6")
+    with torch.no_grad():
+        a = auto(_gpu_data(data))
+        b = x6(_gpu_data(data))
+    for k in ("matches0", "matches1", "matching_scores0", "prune0", "prune1"):
+        assert torch.equal(a[k], b[k]), k

@@ -24,8 +24,8 @@ from golden_util import case_inputs, case_names, load, sinkhorn_inputs, sinkhorn
 NEAR_TIE = 1e-4
 SCORE_TOL = 1e-4
 LA_TOL = 1e-3
-# descriptors after 9 layers: |d| <= DESC_ATOL + DESC_RTOL * |ref|
-DESC_ATOL, DESC_RTOL = 5e-4, 1e-4
+# descriptors (every layer): |d| <= DESC_ATOL + DESC_RTOL * |ref| (measured max 1.1e-5, profiles/r02/parity_report.jsonl)
+DESC_ATOL, DESC_RTOL = 5e-5, 1e-5
 
 pytestmark = pytest.mark.gpu
 

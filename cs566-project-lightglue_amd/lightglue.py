@@ -360,7 +360,8 @@ class LightGlue(nn.Module):
             "log_assignment": la,
             "prune0": prune0,
             "prune1": prune1,
-            "stop_layer": out.stop_layer,
+            # extension key (no reference counterpart): index of the last executed layer, per pair
+            "stop_layer": torch.full((b,), out.stop_layer, dtype=torch.int64),
         }
 
     # ------------------------------------------------------------ profiling (bench.py)

@@ -114,7 +114,7 @@ def test_forward_matches_reference_golden(name, precision):
         pred = model(_gpu_data(data))
     torch.cuda.synchronize()
     assert model.last_precision_used == ("fp16x3" if precision == "auto" else "bf16x6")
-    assert pred["stop_layer"] + 1 == int(g["n_layers_run"])
+    assert int(pred["stop_layer"][0]) + 1 == int(g["n_layers_run"])
     check_against_golden(pred, g, f"{name}/{precision}")
 
 
@@ -436,7 +436,7 @@ def test_training_mode_gates_pruning_and_early_stop():
         tr = model(_gpu_data(data))
     assert ev["prune0"].dtype == torch.int64 and int(ev["prune0"].min()) < model.conf.n_layers
     assert tr["prune0"].dtype == torch.float32 and bool((tr["prune0"] == model.conf.n_layers).all())
-    assert tr["stop_layer"] == model.conf.n_layers - 1
+    assert int(tr["stop_layer"][0]) == model.conf.n_layers - 1
     assert tr["ref_descriptors0"].shape[1] == model.conf.n_layers
     off = _model({k: v for k, v in conf.items() if k not in ("width_confidence", "depth_confidence")}, sd)
     with torch.no_grad():

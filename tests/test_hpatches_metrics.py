@@ -102,3 +102,18 @@ def test_eval_homography_dlt_pipeline():
     # error then evaluates to nan (inf/inf in from_homogeneous), which we reproduce
     pred["matches0"] = torch.full((60,), -1)
     assert np.isnan(hm.eval_homography_dlt(data, pred)["H_error_dlt"])
+
+
+def test_homography_corner_error_matches_reference_golden():
+    """Pinned against the reference's own homography_corner_error (geometry/homography.py:336-342)
+    on committed vectors (tests/golden/make_metric_golden.py): single and batched homographies,
+    float64 and float32."""
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "metric_corner_error.json")))
+    for i, c in enumerate(g["cases"]):
+        dt = getattr(torch, c["dtype"])
+        T = torch.tensor(c["T"], dtype=torch.float64).to(dt)
+        T_gt = torch.tensor(c["T_gt"], dtype=torch.float64).to(dt)
+        size = torch.tensor(c["image_size"], dtype=torch.float64).to(dt)
+        got = hm.homography_corner_error(T, T_gt, size).double().reshape(-1).numpy()
+        tol = 1e-12 if dt == torch.float64 else 1e-6
+        np.testing.assert_allclose(got, c["error"], rtol=tol, atol=tol, err_msg=f"case {i}")

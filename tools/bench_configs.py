@@ -72,7 +72,7 @@ def cfg3(dev, reps):
         for d in pairs:
             with torch.no_grad():
                 p = m(d)
-            layers.append(int(p["stop_layer"]))
+            layers.append(int(p["stop_layer"][0]))
         return p
 
     s, _ = timed(run, max(1, reps // 4), warm=1)

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = [
     "lg_attention",
 ]
 KERNEL_IDS = {"attention": 0, "gemm": 1, "assign": 2}
-# lg_config_t.precision (include/lightglue_mi355x.h): "auto" = fp16x3 with a guarded bf16x6 rerun
+# lg_config_t.precision (include/lightglue_mi355x.h): "auto" = fp16x3 (device-side range scaling)
 PRECISIONS = {"auto": 0, "bf16x6": 1}
 
 

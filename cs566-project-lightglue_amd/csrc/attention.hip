@@ -347,6 +347,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
 
   f16x8 qh[2][2], qhs[2][2], ql[2][2];
   float c_lane[2];
+  const int ek = range_slot_exp(S.rtab, S.k_slot);  // key planes hold k * 2^-ek (RangeOut)
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int qrow = min(q_blk + wave * 32 + qt * 16 + r16, Nq - 1);
@@ -367,7 +368,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       (void)frexpf(mx, &E);
       ex = min(max(4 - E, -100), 100);
     }
-    c_lane[qt] = ldexpf(scale_log2e, -(11 + ex));
+    c_lane[qt] = ldexpf(scale_log2e, ek - (11 + ex));
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -559,7 +560,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   }
 
   // context rows into the plane image: o = 2^11 sum(v p) (the MFMA scale), l_run = 2^11 sum(p),
-  // so 1 / l_run is the old 2^-11 / l exactly
+  // so 1 / l_run is the old 2^-11 / l exactly; v arrived as v * 2^-E[v] and the context leaves
+  // as ctx * 2^-E[v] (its consumer reads the value slot)
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const float l_tot = sum_x16_32(l_run[qt]);

@@ -144,8 +144,9 @@ __device__ __forceinline__ f32x16 mfma_x6(const bf16x8& a0, const bf16x8& a1, co
 // supplies h * 2^11 (exact: |h| <= 16 * 2^11 by construction), so that all three terms land in
 // ONE accumulator at the common scale 2^11:
 //   2^11 * (x . y) ~= x_h . (y_h 2^11) + x_h . y_l + x_l . y_h        (x_l y_l ~ 2^-22 dropped)
-// Operand ranges: |x| <= 65504 (checked where x is produced at run time);
-// y is scaled so |y| < 16 (weights: per matrix at load time; queries: per row; P <= 1).
+// Operand ranges: |x| <= 2^15 (run-time values are written scaled by a per-tensor power of two
+// chosen on the device, RangeOut in kernels.h); y is scaled so |y| < 16 (weights:
+// per matrix at load time; queries: per row; P <= 8).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 constexpr float kLoScale = 2048.f;    // 2^11
@@ -195,6 +196,34 @@ __device__ __forceinline__ int plane_swz(int row) { return (0x78 >> (((row >> 2)
 // element offset of (row, k) inside one plane of an image with `rows_pad` rows
 __device__ __forceinline__ size_t plane_off(int row, int k, int rows_pad) {
   return ((size_t)(k >> 5) * rows_pad + row) * kKB + ((((k >> 3) & 3) ^ plane_swz(row)) << 3) + (k & 7);
+}
+
+// ---- run-time range scaling of plane images (kernels.h RangeOut) ----------------------------
+constexpr float kRangeLimit = 32768.f;  // 2^15: half the fp16 range, so rounding cannot reach inf
+template <class RO>
+__device__ __forceinline__ int range_exponent(const RO& r) {
+  if (!r.tab) return 0;
+  float b = r.add;
+  if (r.in0 >= 0) b += r.g0 * __uint_as_float(r.tab[2 * r.in0]);
+  if (r.in1 >= 0) b += r.g1 * __uint_as_float(r.tab[2 * r.in1]);
+  if (!(b > kRangeLimit) || !(b <= 3.0e38f)) return 0;  // in range, or non-finite data
+  int E;
+  (void)frexpf(b * (1.f / kRangeLimit), &E);  // b / 2^15 = m 2^E, m in [0.5, 1)  ->  2^E >= it
+  return E;
+}
+__device__ __forceinline__ int range_slot_exp(const unsigned* tab, int slot) {
+  return (tab && slot >= 0) ? (int)tab[2 * slot + 1] : 0;
+}
+// wave-wide max of |x| written -> M[out], and E[out] (every writing wave stores the same value);
+// called by all 64 lanes of a wave that wrote planes under `r`
+template <class RO>
+__device__ __forceinline__ void range_commit(const RO& r, float lane_max, int e) {
+  if (!r.tab) return;
+  const float m = wave_max_dpp(lane_max);
+  if ((threadIdx.x & 63) == 0) {
+    if (m > 0.f) atomicMax(r.tab + 2 * r.out, __float_as_uint(m));
+    r.tab[2 * r.out + 1] = (unsigned)e;
+  }
 }
 
 // ---- LDS-DMA ------------------------------------------------------------------------------

@@ -84,10 +84,12 @@ hipError_t kpt_extent(const float* kpts, int B, int n, float* size_out, hipStrea
 // One wave per row: lane holds columns [4l, 4l+4) and [256+4l, 256+4l+4).
 // ----------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void ln_gelu_kernel(float* x, const float* g, const float* bta, int rows,
-                                                      _Float16* planes, int rows_pad, int* ovf) {
+                                                      _Float16* planes, int rows_pad, RangeOut ro) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  bool bad = false;
+  const int eo = planes ? range_exponent(ro) : 0;
+  const float so = ldexpf(1.f, -eo);
+  float wmax = 0.f;
   if (row < rows) {
     float* xr = x + (size_t)row * 512;
     f32x4 v0 = *reinterpret_cast<f32x4*>(xr + lane * 4);
@@ -123,9 +125,9 @@ __global__ __launch_bounds__(256) void ln_gelu_kernel(float* x, const float* g, 
         f16x4 h, l;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          bad |= !(fabsf(v[e]) <= kF16Max);
+          wmax = fmaxf(wmax, fabsf(v[e]));
           _Float16 a, b;
-          split2h(v[e], a, b);
+          split2h(v[e] * so, a, b);
           h[e] = a;
           l[e] = b;
         }
@@ -135,13 +137,13 @@ __global__ __launch_bounds__(256) void ln_gelu_kernel(float* x, const float* g, 
       }
     }
   }
-  if (ovf && __ballot(bad) != 0ull && lane == 0) atomicOr(ovf, 1);
+  if (planes) range_commit(ro, wmax, eo);
 }
 
 hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, _Float16* planes, int rows_pad,
-                              int* ovf, hipStream_t st) {
+                              const RangeOut& ro, hipStream_t st) {
   if (rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(ln_gelu_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, g, b, rows, planes, rows_pad, ovf);
+  hipLaunchKernelGGL(ln_gelu_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, g, b, rows, planes, rows_pad, ro);
   return hipGetLastError();
 }
 
@@ -414,15 +416,16 @@ hipError_t remap_matches(const int64_t* m0c, const int64_t* m1c, const float* s0
 // ----------------------------------------------------------------------------------------
 // Kernel-check helpers (lg_attention): fp32 -> operand planes, plane image -> fp32 rows.
 // ----------------------------------------------------------------------------------------
-__global__ void split_planes_kernel(const float* x, size_t n, void* planes, int prec, int* ovf) {
+__global__ void split_planes_kernel(const float* x, size_t n, void* planes, int prec, RangeOut ro) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool bad = false;
+  const int eo = prec == PREC_H3 ? range_exponent(ro) : 0;
+  float wmax = 0.f;
   if (i < n) {
     const float v = x[i];
     if (prec == PREC_H3) {
       _Float16 h, l;
-      split2h(v, h, l);
-      bad = !(fabsf(v) <= kF16Max);
+      split2h(ldexpf(v, -eo), h, l);
+      wmax = fabsf(v);
       static_cast<_Float16*>(planes)[i] = h;
       static_cast<_Float16*>(planes)[n + i] = l;
     } else {
@@ -433,28 +436,82 @@ __global__ void split_planes_kernel(const float* x, size_t n, void* planes, int 
       static_cast<__bf16*>(planes)[2 * n + i] = l;
     }
   }
-  if (ovf && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+  if (prec == PREC_H3) range_commit(ro, wmax, eo);
 }
 
-hipError_t split_planes(const float* x, size_t n, void* planes, int prec, int* ovf, hipStream_t st) {
+hipError_t split_planes(const float* x, size_t n, void* planes, int prec, const RangeOut& ro, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, planes, prec, ovf);
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, planes, prec, ro);
   return hipGetLastError();
 }
 
-__global__ void image_to_rows_kernel(const _Float16* p, long long ps, int rows_pad, int K, float* out, int rows) {
+__global__ void image_to_rows_kernel(const _Float16* p, long long ps, int rows_pad, int K, float* out, int rows,
+                                     const unsigned* tab, int slot) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)rows * K) return;
   const int r = (int)(i / K), c = (int)(i % K);
   const size_t off = plane_off(r, c, rows_pad);
-  out[i] = (float)p[off] + (float)p[ps + off] * (1.f / kLoScale);
+  out[i] = ldexpf((float)p[off] + (float)p[ps + off] * (1.f / kLoScale), range_slot_exp(tab, slot));
 }
 
-hipError_t image_to_rows(const _Float16* planes, long long ps, int rows_pad, int K, float* out, int rows, hipStream_t st) {
+hipError_t image_to_rows(const _Float16* planes, long long ps, int rows_pad, int K, float* out, int rows,
+                         const unsigned* tab, int slot, hipStream_t st) {
   if (rows <= 0) return hipSuccess;
   const size_t n = (size_t)rows * K;
   hipLaunchKernelGGL(image_to_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, planes, ps, rows_pad, K,
-                     out, rows);
+                     out, rows, tab, slot);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// Load-time weight statistics for the run-time range bounds (kernels.h RangeOut)
+// ----------------------------------------------------------------------------------------
+// out[0] = max_r sum_k |W[r,k]|, out[1] = max |bias| (one block; load time only)
+__global__ __launch_bounds__(1024) void weight_range_stats_kernel(const float* W, int rows, int K, const float* bias,
+                                                                 float* out) {
+  __shared__ float red[2][16];
+  float l1max = 0.f, bmax = 0.f;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int r = wave; r < rows; r += 16) {
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s += fabsf(W[(size_t)r * K + k]);
+    l1max = fmaxf(l1max, wave_sum(s));
+  }
+  if (bias)
+    for (int r = threadIdx.x; r < rows; r += 1024) bmax = fmaxf(bmax, fabsf(bias[r]));
+  bmax = wave_max(bmax);
+  if (lane == 0) {
+    red[0][wave] = l1max;
+    red[1][wave] = bmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f;
+    for (int w = 0; w < 16; ++w) {
+      a = fmaxf(a, red[0][w]);
+      b = fmaxf(b, red[1][w]);
+    }
+    out[0] = a;
+    out[1] = b;
+  }
+}
+
+hipError_t weight_range_stats(const float* W, int rows, int K, const float* bias, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(weight_range_stats_kernel, dim3(1), dim3(1024), 0, st, W, rows, K, bias, out);
+  return hipGetLastError();
+}
+
+// LayerNorm output bound: |(x - mean) / std| <= sqrt(n - 1) for any row, so
+// |LN(x)_k| <= |g_k| sqrt(n - 1) + |b_k|; GELU(y) <= |y| (and > -0.17)
+__global__ void layernorm_bound_kernel(const float* g, const float* b, int n, float* out) {
+  float m = 0.f;
+  for (int k = threadIdx.x; k < n; k += 64) m = fmaxf(m, fabsf(g[k]) * sqrtf((float)(n - 1)) + fabsf(b[k]));
+  m = wave_max(m);
+  if (threadIdx.x == 0) *out = m;
+}
+
+hipError_t layernorm_bound(const float* g, const float* b, int n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(layernorm_bound_kernel, dim3(1), dim3(64), 0, st, g, b, n, out);
   return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@
 // 256 x 256 x 32 beat 128 x 256 at two workgroups per CU and every k-tile of 16 with 2-4
 // stages).  blockIdx -> tile through a bijective XCD remap so the column tiles of one row panel
 // share an XCD's L2.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -95,6 +96,11 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, half = lane >> 5;
   const int wm0 = (wave / WGN) * 64, wn0 = (wave % WGN) * WN;
+
+  // run-time range exponents of the A plane images (RangeOut): A0 holds a0 * 2^-e0, A1 a1 * 2^-e1
+  const int e0 = range_slot_exp(g.rtab, g.a0_slot);
+  const int e1 = g.K0 < g.K ? range_slot_exp(g.rtab, g.a1_slot) : e0;
+  const float accs = ldexpf(g.acc_scale, e1);  // after the k-loop the accumulator holds 2^-e1 units
 
   const int num_m = (g.R + BM - 1) / BM, num_n = g.Nout / BN;
   const int tile = xcd_remap_h3(blockIdx.x, num_m * num_n);
@@ -223,6 +229,15 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    if (kt == nk0 && e0 != e1) {  // switching from A0 to A1 units (exact power of two; rare)
+      const float f = ldexpf(1.f, e0 - e1);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < TR; ++r) acc[i][j][r] *= f;
+    }
 #if LG_GEMM_SETPRIO
     __builtin_amdgcn_s_setprio(1);  // keeps the MFMA cluster between the barriers (guide T5)
 #endif
@@ -236,7 +251,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   asm volatile("" ::: "memory");
 
   // ------------------------------------------------------------------ epilogues
-  bool bad = false;
+  float wmax = 0.f;  // max |x| this lane wrote into planes (RangeOut tracking)
   if constexpr (EPI == EPI_PROBE) {
     // timing probe (tools/kbench_gemm.hip): keeps the accumulators live, stores nothing
     float t = 0.f;
@@ -278,7 +293,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      visit(i, [&](int, int c, float v) { return fmaf(v, g.acc_scale, bj_[c / LC]); });
+      visit(i, [&](int, int c, float v) { return fmaf(v, accs, bj_[c / LC]); });
     // row sum of f(v) over the 512 columns: lane partials over its TJ columns -> table ->
     // PARTS threads per row -> shuffle
     auto row_total = [&](auto f, float* out) {
@@ -314,6 +329,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     __syncthreads();
     // normalise + GELU, then 16-byte plane-image stores through the per-wave transpose buffer
     const int cq = (lane & 7) * 8;
+    const int eo = range_exponent(g.ro);
+    const float so = ldexpf(1.f, -eo);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       constexpr int jh = 0;  // WN == 64: one 64-column pass per row pass
@@ -337,9 +354,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float v = e < 4 ? v0[e] : v1[e - 4];
-              bad |= !(fabsf(v) <= kF16Max);
+              wmax = fmaxf(wmax, fabsf(v));
               _Float16 a, c;
-              split2h(v, a, c);
+              split2h(v * so, a, c);
               h[e] = a;
               l[e] = c;
             }
@@ -351,6 +368,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
       }
     }
+    range_commit(g.ro, wmax, eo);
   } else if constexpr (EPI == EPI_STORE) {
     static_assert(WN == 64, "EPI_STORE tile");
     // Transposed through LDS (free after the k-loop; 8 KiB per wave per 32-row pass) so that every
@@ -361,6 +379,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
     const int cq = (lane & 7) * 8;                     // first of the lane's 8 columns (in the wave tile)
     const int col0 = n0 + wn0 + cq;
+    const int eo = g.Yp ? range_exponent(g.ro) : 0;
+    const float so = ldexpf(1.f, -eo);
     f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
     if (g.bias) {
       b0 = *reinterpret_cast<const f32x4*>(g.bias + col0);
@@ -383,8 +403,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         if (row < g.R) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v0[e] = fmaf(v0[e], g.acc_scale, b0[e]) * g.out_scale;
-            v1[e] = fmaf(v1[e], g.acc_scale, b1[e]) * g.out_scale;
+            v0[e] = fmaf(v0[e], accs, b0[e]) * g.out_scale;
+            v1[e] = fmaf(v1[e], accs, b1[e]) * g.out_scale;
           }
           if (g.res) {
             const float* rp = g.res + (size_t)row * g.ldr + col0;
@@ -405,9 +425,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float v = e < 4 ? v0[e] : v1[e - 4];
-              bad |= !(fabsf(v) <= kF16Max);
+              wmax = fmaxf(wmax, fabsf(v));
               _Float16 a, c;
-              split2h(v, a, c);
+              split2h(v * so, a, c);
               h[e] = a;
               l[e] = c;
             }
@@ -419,6 +439,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
+    if (g.Yp) range_commit(g.ro, wmax, eo);
   } else {
     static_assert(WN == 64, "QKV epilogue tile");
     // Head-major scatter through the same LDS transpose as EPI_STORE.  The wave's 64 columns are
@@ -443,6 +464,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     const bool to_kp = EPI == EPI_QKV_ROT ? t == 1 : t == 0;
     const bool to_vp = EPI == EPI_QKV_ROT ? t == 2 : t == 1;
     const float sc = (EPI == EPI_CROSS_QKV && t == 0) ? hl.qk_scale : 1.f;
+    const int eo = to_kp ? range_exponent(g.ro) : to_vp ? range_exponent(g.ro_v) : 0;
+    const float so = ldexpf(1.f, -eo);
     float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
     const int d0 = (lane & 7) * 8;  // the lane's first dim
     float bd[8];                    // bias in dim order: dim d <- GEMM column (d & 1) * 32 + d / 2
@@ -467,7 +490,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         if (row >= g.R) continue;
         float x[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = fmaf(e < 4 ? v0[e] : v1[e - 4], g.acc_scale, bd[e]);
+        for (int e = 0; e < 8; ++e) x[e] = fmaf(e < 4 ? v0[e] : v1[e - 4], accs, bd[e]);
         if (rot) {
           // t*cos + rotate_half(t)*sin, rotate_half(x)[2p] = -x[2p+1], [2p+1] = x[2p]; freq p = dim / 2
           const f32x4 c4 = *reinterpret_cast<const f32x4*>(hl.cosb + (size_t)row * kFreq + d0 / 2);
@@ -491,9 +514,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
           f16x8 h, l;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            bad |= !(fabsf(x[e]) <= kF16Max);
+            wmax = fmaxf(wmax, fabsf(x[e]));
             _Float16 a, c;
-            split2h(x[e], a, c);
+            split2h(x[e] * so, a, c);
             h[e] = a;
             l[e] = c;
           }
@@ -503,8 +526,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
+    if (to_kp) range_commit(g.ro, wmax, eo);
+    else if (to_vp) range_commit(g.ro_v, wmax, eo);
   }
-  if (g.ovf && __ballot(bad) != 0ull && lane == 0) atomicOr(g.ovf, 1);
 }
 
 template <int BM, int NSTAGE, int BN = TB, int WN = 64>
@@ -577,14 +601,16 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
   return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
 }
 
-// fp32 rows -> plane image; one thread per 8-element chunk
+// fp32 rows -> plane image (scaled by 2^-E, RangeOut); one thread per 8-element chunk
 // (xc != nullptr: the fp32 rows are also copied to xc, row stride K -- the residual stream's
 // initial value taken in the same read)
 __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
-                                      int* ovf, float* xc) {
+                                      RangeOut ro, float* xc) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int nch = K / 8;
-  bool bad = false;
+  const int eo = range_exponent(ro);
+  const float so = ldexpf(1.f, -eo);
+  float wmax = 0.f;
   if (i < (size_t)R * nch) {
     const int r = (int)(i / nch), c = (int)(i % nch);
     const float* p = x + (size_t)r * ld + c * 8;
@@ -598,9 +624,9 @@ __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Flo
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float v = e < 4 ? v0[e] : v1[e - 4];
-      bad |= !(fabsf(v) <= kF16Max);
+      wmax = fmaxf(wmax, fabsf(v));
       _Float16 a, b;
-      split2h(v, a, b);
+      split2h(v * so, a, b);
       h[e] = a;
       l[e] = b;
     }
@@ -608,17 +634,35 @@ __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Flo
     *reinterpret_cast<f16x8*>(planes + off) = h;
     *reinterpret_cast<f16x8*>(planes + (size_t)rows_pad * K + off) = l;
   }
-  if (ovf && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+  range_commit(ro, wmax, eo);
 }
 
-hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0, int* ovf,
-                          hipStream_t st, float* xcopy) {
+hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
+                          const RangeOut& ro, hipStream_t st, float* xcopy) {
   if (R <= 0) return hipSuccess;
   if (K % kKB || rows_pad < row0 + R) return hipErrorInvalidValue;
   const size_t n = (size_t)R * (K / 8);
   hipLaunchKernelGGL(rows_to_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, R, K, ld, planes,
-                     rows_pad, row0, ovf, xcopy);
+                     rows_pad, row0, ro, xcopy);
   return hipGetLastError();
 }
 
+}  // namespace lg
+
+namespace lg {
+// max |x| -> M[slot] of a range table (the inputs' bound for the first plane images)
+__global__ void range_absmax_kernel(const float* x, size_t n, unsigned* tab, int slot) {
+  float m = 0.f;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+  m = wave_max_dpp(m);
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(tab + 2 * slot, __float_as_uint(m));
+}
+
+hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(range_absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, tab, slot);
+  return hipGetLastError();
+}
 }  // namespace lg

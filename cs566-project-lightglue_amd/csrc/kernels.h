@@ -14,10 +14,30 @@ enum EpiKind {
 };
 
 // Operand formats of the fp32-accurate matrix-core arithmetic (common.h):
-//   PREC_H3  fp16x3 -- 3 fp16 MFMAs per product; runtime operands must satisfy |x| <= 65504
-//            (a device flag records any violation, lg_forward then reruns in PREC_X6)
+//   PREC_H3  fp16x3 -- 3 fp16 MFMAs per product; run-time operands are written as plane images
+//            scaled by a per-tensor power of two chosen on the device (RangeOut below), so the
+//            fp16 range cannot be exceeded and no host check is needed
 //   PREC_X6  bf16x6 -- 6 bf16 MFMAs per product; full fp32 range
 enum Prec { PREC_H3 = 0, PREC_X6 = 1 };
+
+// Run-time range scaling of fp16x3 plane images.  A forward keeps a small table
+// in its workspace, zeroed at the start; slot s holds
+//   tab[2s]     M[s]: max |x| over the values written (float bits; atomicMax of non-negative floats)
+//   tab[2s + 1] E[s]: the exponent the planes were written with -- they hold x * 2^-E[s]
+// A producer chooses E before writing from an upper bound of what it will write,
+//   bound = g0 * M[in0] + g1 * M[in1] + add     (in0/in1: slots of its inputs, -1 = unused;
+//                                                g0/g1/add: weight row-L1 norms and bias maxima)
+// E = 0 while bound <= 2^15 (the plane image is then exactly the unscaled one), else the smallest
+// E with bound * 2^-E <= 2^15.  Consumers fold 2^E into a scale they apply anyway (the GEMM
+// epilogue's accumulator scale, the attention's softmax scale).  Every workgroup of a producer
+// derives the same E from the same table entries; a null tab disables scaling (E = 0).
+struct RangeOut {
+  unsigned* tab;
+  int in0, in1;
+  float g0, g1, add;
+  int out;
+};
+inline RangeOut range_none() { return RangeOut{nullptr, -1, -1, 0.f, 0.f, 0.f, 0}; }
 
 // Head-major destinations [set][b][h][n][64] for the QKV epilogues; set 0 = image 0 (B*M rows),
 // set 1 = image 1 (B*N rows), rows in GEMM order (image 0 rows first).  All in natural dim order.
@@ -80,7 +100,10 @@ struct GemmH3Args {
   _Float16* Yp;       // EPI_STORE: also write Y as a plane image (nullable), with its rows_pad
   long long yps;
   int yrows_pad;
-  int* ovf;           // set to 1 when a value written into Yp / K, V planes leaves the fp16 range
+  const unsigned* rtab;  // range table of the A plane images (nullable: both exponents 0)
+  int a0_slot, a1_slot;  // their slots (-1: exponent 0)
+  RangeOut ro;        // Yp / EPI_LN_GELU planes (EPI_QKV_*: the key planes)
+  RangeOut ro_v;      // EPI_QKV_*: the value planes
   const float* ln_g;  // EPI_LN_GELU: LayerNorm weight / bias [Nout]
   const float* ln_b;
   HeadLayout hl;      // EPI_QKV_ROT / EPI_CROSS_QKV
@@ -88,8 +111,10 @@ struct GemmH3Args {
 hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st);
 // fp32 rows [R][K] (row stride ld) -> rows row0 .. row0+R-1 of a plane image (rows_pad), with
 // the fp16-range guard; xcopy (optional) also receives the fp32 rows, row stride K
-hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0, int* ovf,
-                          hipStream_t st, float* xcopy = nullptr);
+hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
+                          const RangeOut& ro, hipStream_t st, float* xcopy = nullptr);
+// max |x| over n floats, atomicMax'ed into slot `slot` of a range table (M only)
+hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipStream_t st);
 
 // Attention over head-major Q/K/V ([set][b][h][n][64]); O written row-major into ctx
 // [rows][256] at column h*64 (rows in GEMM order).  Two "sets" per launch (blockIdx.z).
@@ -103,6 +128,11 @@ struct AttnSet {
   _Float16* op;      // PREC_H3: ctx plane image (K = 256), rows of this set start at o_row0
   long long ops;
   int o_rows_pad, o_row0;
+  // PREC_H3 range exponents (RangeOut): the key planes hold k * 2^-E[k_slot] (folded into the
+  // softmax scale); the value planes v * 2^-E[v_slot], so the context planes come out as
+  // ctx * 2^-E[v_slot] and their consumer reads v_slot.  Null rtab: exponents 0.
+  const unsigned* rtab;
+  int k_slot;
 };
 hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st);
 
@@ -126,7 +156,7 @@ hipError_t kpt_extent(const float* kpts, int B, int n, float* size_out, hipStrea
 // In place (planes == null, PREC_X6) or into a plane image of K = 512 (PREC_H3).
 bool gemm_h3_ln_split(int R);
 hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows, _Float16* planes, int rows_pad,
-                              int* ovf, hipStream_t st);
+                              const RangeOut& ro, hipStream_t st);
 // y[r] = dot(x[r,:256], w) + b ; optional sigmoid
 hipError_t gemv_256(const float* x, const float* w, const float* b, float* y, int rows, int sigmoid, hipStream_t st);
 
@@ -157,10 +187,16 @@ hipError_t fold_out_proj(float* W1, float* b1, const float* Wo, const float* bo,
 hipError_t absmax(const float* src, size_t n, float* out, hipStream_t st);
 hipError_t split_weight_h3(const float* src, int rows, int K, float scale, _Float16* planes, hipStream_t st);
 
-// lg_attention (kernel-level checks): fp32 [n] -> operand planes of `prec` (plane stride n; fp16
-// range guard into ovf for PREC_H3), and a plane image (K columns) -> fp32 rows.
-hipError_t split_planes(const float* x, size_t n, void* planes, int prec, int* ovf, hipStream_t st);
-hipError_t image_to_rows(const _Float16* planes, long long ps, int rows_pad, int K, float* out, int rows, hipStream_t st);
+// lg_attention (kernel-level checks): fp32 [n] -> operand planes of `prec` (plane stride n; PREC_H3
+// range-scaled by ro), and a plane image (K columns) -> fp32 rows, times 2^E[slot] of tab.
+hipError_t split_planes(const float* x, size_t n, void* planes, int prec, const RangeOut& ro, hipStream_t st);
+hipError_t image_to_rows(const _Float16* planes, long long ps, int rows_pad, int K, float* out, int rows,
+                         const unsigned* tab, int slot, hipStream_t st);
+// Load-time weight statistics for the range bounds: out[0] = max over rows of sum_k |W[r,k]|,
+// out[1] = max |bias| (bias may be null), over rows [0, rows) of W [rows][K]; and the LayerNorm
+// output bound max_k |g_k| sqrt(n - 1) + |b_k|.
+hipError_t weight_range_stats(const float* W, int rows, int K, const float* bias, float* out, hipStream_t st);
+hipError_t layernorm_bound(const float* g, const float* b, int n, float* out, hipStream_t st);
 
 // Weight repacking: dst[r,:] = src[idx[r],:] (row length `cols`).
 hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st);

@@ -92,6 +92,7 @@ std::vector<Tensor> make_schema(const lg_config_t& c) {
 }
 
 constexpr int D = 256;
+constexpr int kRangeSlots = 256;  // range-table slots per forward (about 5 per block are used)
 
 // Packed per-layer weights (offsets in floats into one device buffer).
 struct BlockW {
@@ -128,6 +129,16 @@ struct lg_handle {
   };
   std::map<size_t, Planes> planes;
   _Float16* wplanes = nullptr;
+  // run-time range bounds (kernels.h RangeOut), per layer and block: row-L1 maxima and bias
+  // maxima of the matrices whose outputs become plane images, and the LayerNorm output bound
+  struct BlockGain {
+    float gK, bK, gV, bV;  // key / value rows of Wqkv (self: rotary x1.5) or to_qk (x scale^0.5) / to_v
+    float hb;              // |GELU(LN(.))| <= hb
+    float g2, b2;          // ffn.3
+    float go, bo;          // out_proj / to_out (unfolded path only)
+  };
+  std::vector<BlockGain> gains;  // [layer * 2 + block]
+  float gi = 0.f, bi_max = 0.f;  // input_proj
   bool loaded = false;
   bool pass_started = false;  // forward_pass got past argument checks (work was enqueued)
   // fold out_proj / to_out into ffn.0 at load time (env LG_FOLD_OUT_PROJ=0 disables)
@@ -287,7 +298,7 @@ struct Work {
   int rows_pad;
   size_t R;
   int *flags, *pos, *ind0, *ind1, *ind0b, *ind1b, *counts;
-  int* ovf;  // PREC_H3 fp16-range guard
+  unsigned* rtab;  // PREC_H3 range table (kernels.h RangeOut), kRangeSlots slots
   int64_t *m0c, *m1c;
   float *s0c, *s1c;
   size_t bytes;
@@ -329,7 +340,7 @@ Work carve(char* base, int B, int M, int N, bool prune, int din) {
   w.tok = tf(R);
   w.sim = tf((size_t)B * M * N);
   w.aws = tf(lg::assign_workspace_floats(B, M, N));
-  w.ovf = ti(64);
+  w.rtab = reinterpret_cast<unsigned*>(ti(2 * kRangeSlots));
   if (prune) {
     w.X2 = tf(R * D);
     w.cos2 = tf(R * 32);
@@ -524,6 +535,42 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
       off += 2 * n;
     }
   }
+  // range-bound statistics (one read-back at load time)
+  {
+    const int L = h->cfg.n_layers;
+    const int per = 2 * 4 + 1;  // per block: K, V, W2, Wo stats (2 floats each) + LN bound
+    const int nf = L * 2 * per + 2;
+    float* dst = nullptr;
+    LG_HIP(hipMallocAsync((void**)&dst, nf * sizeof(float), st));
+    const float* W = h->wbuf;
+    for (int i = 0; i < L; ++i)
+      for (int b = 0; b < 2; ++b) {
+        const BlockW& w = b == 0 ? h->layers[i].self : h->layers[i].cross;
+        float* o = dst + (i * 2 + b) * per;
+        const size_t k0 = b == 0 ? (size_t)D : 0, v0 = b == 0 ? 2 * (size_t)D : (size_t)D;
+        LG_HIP(lg::weight_range_stats(W + w.Wqkv + k0 * D, D, D, W + w.bqkv + k0, o + 0, st));
+        LG_HIP(lg::weight_range_stats(W + w.Wqkv + v0 * D, D, D, W + w.bqkv + v0, o + 2, st));
+        LG_HIP(lg::weight_range_stats(W + w.W2, D, 2 * D, W + w.b2, o + 4, st));
+        LG_HIP(lg::weight_range_stats(W + w.Wo, D, D, W + w.bo, o + 6, st));
+        LG_HIP(lg::layernorm_bound(W + w.g, W + w.be, 2 * D, o + 8, st));
+      }
+    if (h->cfg.input_dim != D) LG_HIP(lg::weight_range_stats(W + h->Wi, D, h->cfg.input_dim, W + h->bi, dst + nf - 2, st));
+    else LG_HIP(hipMemsetAsync(dst + nf - 2, 0, 2 * sizeof(float), st));
+    std::vector<float> hs(nf);
+    LG_HIP(hipMemcpyAsync(hs.data(), dst, nf * sizeof(float), hipMemcpyDeviceToHost, st));
+    LG_HIP(hipStreamSynchronize(st));
+    LG_HIP(hipFreeAsync(dst, st));
+    h->gains.assign((size_t)L * 2, {});
+    const float qk_scale = std::sqrt(1.f / std::sqrt(64.f));
+    for (int i = 0; i < L * 2; ++i) {
+      const float* o = hs.data() + i * per;
+      // self keys are rotated: |k cos - k' sin| <= sqrt(2) max(|k|, |k'|) < 1.5 max
+      const float kf = (i % 2 == 0) ? 1.5f : qk_scale;
+      h->gains[i] = {o[0] * kf, o[1] * kf, o[2], o[3], o[8], o[4], o[5], o[6], o[7]};
+    }
+    h->gi = hs[nf - 2];
+    h->bi_max = hs[nf - 1];
+  }
   h->loaded = true;
   return LG_OK;
 }
@@ -589,7 +636,6 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     const auto& pl = h->planes.at(off);
     g.W = {h->wplanes + pl.off, pl.pstride, pl.rows};
     g.acc_scale = pl.unscale;
-    g.ovf = w.ovf;
   };
   auto image = [&](_Float16* p, int K) { return PlaneRef{p, (long long)RP * K, RP}; };
   auto attn = [&](const AttnSet& a0, const AttnSet& a1, float scale, bool cross) -> hipError_t {
@@ -610,9 +656,19 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     return e;
   };
 
-  // ---- input projection (lightglue.py:370-373,486-487); H3 also builds x's plane image
-  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.ovf, 0, sizeof(int), st));
+  // ---- run-time range table (PREC_H3): every plane image written below picks its power-of-two
+  // scale on the device from the maxima of its inputs (kernels.h RangeOut), so the fp16 range
+  // cannot be exceeded and nothing is read back -- the forward stays asynchronous
+  unsigned* rt = prec == PREC_H3 ? w.rtab : nullptr;
+  int nslot = 0;
+  auto slot = [&]() { return nslot < kRangeSlots ? nslot++ : kRangeSlots - 1; };
+  auto ro = [&](int in0, float g0, int in1, float g1, float add, int out) {
+    return RangeOut{rt, in0, in1, g0, g1, add, out};
+  };
+  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.rtab, 0, 2 * kRangeSlots * sizeof(unsigned), st));
   h->pass_started = true;
+  int s_x = -1;  // slot of the current residual-stream plane image Xp
+  // ---- input projection (lightglue.py:370-373,486-487); H3 also builds x's plane image
   if (c.input_dim != D) {
     if (prec == PREC_H3) {
       const int din = c.input_dim;
@@ -624,12 +680,16 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         d0 = w.Dst;
         d1 = w.Dst + (size_t)B * M * din;
       }
-      LG_HIP(rows_to_planes(d0, B * M, din, din, w.Dp, RP, 0, w.ovf, st));
-      LG_HIP(rows_to_planes(d1, B * N, din, din, w.Dp, RP, B * M, w.ovf, st));
+      const int s_in = slot(), s_d = slot();
+      s_x = slot();
+      LG_HIP(range_absmax(d0, (size_t)B * M * din, rt, s_in, st));
+      LG_HIP(range_absmax(d1, (size_t)B * N * din, rt, s_in, st));
+      LG_HIP(rows_to_planes(d0, B * M, din, din, w.Dp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_d), st));
+      LG_HIP(rows_to_planes(d1, B * N, din, din, w.Dp, RP, B * M, ro(s_in, 1.f, -1, 0.f, 0.f, s_d), st));
       GemmH3Args g = gemm_h3_base();
-      g.A0 = image(w.Dp, din); g.K0 = din; g.K = din; wplanes(g, h->Wi);
+      g.A0 = image(w.Dp, din); g.K0 = din; g.K = din; wplanes(g, h->Wi); g.rtab = rt; g.a0_slot = s_d;
       g.bias = Wb + h->bi; g.R = B * (M + N); g.Nout = D; g.Y = w.X; g.ldy = D;
-      g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP;
+      g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP; g.ro = ro(s_d, h->gi, -1, 0.f, h->bi_max, s_x);
       LG_HIP(gemmh(g, EPI_STORE));
     } else {
       GemmArgs g = gemm_base();
@@ -641,14 +701,21 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       LG_HIP(gemm(g, EPI_STORE, 1));
     }
   } else {
+    const int s_in = prec == PREC_H3 ? slot() : -1;
+    s_x = prec == PREC_H3 ? slot() : -1;
+    if (prec == PREC_H3) {
+      LG_HIP(range_absmax(in->descriptors0, (size_t)B * M * D, rt, s_in, st));
+      LG_HIP(range_absmax(in->descriptors1, (size_t)B * N * D, rt, s_in, st));
+    }
     if (prec == PREC_H3 && din_a16) {
       // residual stream and its plane image from one read of the descriptors
-      LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, w.ovf, st, w.X));
-      LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, w.ovf, st, w.X + (size_t)B * M * D));
+      LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x), st, w.X));
+      LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, ro(s_in, 1.f, -1, 0.f, 0.f, s_x), st,
+                            w.X + (size_t)B * M * D));
     } else {
       LG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
       LG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
-      if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, B * (M + N), D, D, w.Xp, RP, 0, w.ovf, st));
+      if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, B * (M + N), D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x), st));
     }
   }
 
@@ -688,9 +755,14 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       hl.q = w.Q; hl.kp = w.KP; hl.vp = w.VP; hl.pstride = (long long)w.R * D;
       hl.qk_scale = std::sqrt(1.f / std::sqrt(64.f));  // scale**0.5 (lightglue.py:235)
       const int epi_qkv = blk == 0 ? EPI_QKV_ROT : EPI_CROSS_QKV;
+      const lg_handle::BlockGain& gn = h->gains[(size_t)i * 2 + blk];
+      const int s_k = slot(), s_v = slot();
       if (prec == PREC_H3) {
         GemmH3Args g = gemm_h3_base();
         g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, bw.Wqkv); g.bias = Wb + bw.bqkv;
+        g.rtab = rt; g.a0_slot = s_x;
+        g.ro = ro(s_x, gn.gK, -1, 0.f, gn.bK, s_k);
+        g.ro_v = ro(s_x, gn.gV, -1, 0.f, gn.bV, s_v);
         g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D; g.hl = hl;
         LG_HIP(gemmh(g, epi_qkv));
       } else {
@@ -707,18 +779,22 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       const void* vp1 = static_cast<const char*>(w.VP) + 2 * img1;
       float* ctx1 = w.ctx + (size_t)B * M * D;
       if (blk == 0) {  // self: q/k/v of the same image, scale 1/sqrt(64) (SDPA default)
-        a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M, w.Cp, (long long)RP * D, RP, 0};
-        a1 = {w.Q + img1, kp1, vp1, ps, ctx1, N, N, w.Cp, (long long)RP * D, RP, B * M};
+        a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M, w.Cp, (long long)RP * D, RP, 0, rt, s_k};
+        a1 = {w.Q + img1, kp1, vp1, ps, ctx1, N, N, w.Cp, (long long)RP * D, RP, B * M, rt, s_k};
       } else {  // cross: qk fp32 in w.Q and as planes in w.KP, v planes in w.VP
-        a0 = {w.Q, kp1, vp1, ps, w.ctx, M, N, w.Cp, (long long)RP * D, RP, 0};
-        a1 = {w.Q + img1, w.KP, w.VP, ps, ctx1, N, M, w.Cp, (long long)RP * D, RP, B * M};
+        a0 = {w.Q, kp1, vp1, ps, w.ctx, M, N, w.Cp, (long long)RP * D, RP, 0, rt, s_k};
+        a1 = {w.Q + img1, w.KP, w.VP, ps, ctx1, N, M, w.Cp, (long long)RP * D, RP, B * M, rt, s_k};
       }
       LG_HIP(attn(a0, a1, blk == 0 ? 0.125f : 1.0f, blk == 1));
       if (prec == PREC_H3) {
         // out projection (skipped when folded into ffn.0 at load time: ffn.0 then reads ctx)
+        // the context planes carry the value planes' exponent (attention.hip)
+        int s_msg = s_v;
         if (!h->fold) {
+          s_msg = slot();
           GemmH3Args g = gemm_h3_base();
           g.A0 = image(w.Cp, D); g.K0 = D; g.K = D; wplanes(g, bw.Wo); g.bias = Wb + bw.bo;
+          g.rtab = rt; g.a0_slot = s_v; g.ro = ro(s_v, gn.go, -1, 0.f, gn.bo, s_msg);
           g.R = R; g.Nout = D; g.Yp = w.Mp; g.yps = (long long)RP * D; g.yrows_pad = RP;
           LG_HIP(gemmh(g, EPI_STORE));
         }
@@ -727,19 +803,27 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         GemmH3Args g = gemm_h3_base();
         g.A0 = image(w.Xp, D); g.K0 = D; g.A1 = image(h->fold ? w.Cp : w.Mp, D); g.K = 2 * D;
         wplanes(g, bw.W1); g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D;
+        g.rtab = rt; g.a0_slot = s_x; g.a1_slot = s_msg;
+        const int s_h = slot();
+        const RangeOut ro_h = ro(-1, 0.f, -1, 0.f, gn.hb, s_h);
         if (gemm_h3_ln_split(R)) {  // small R: 64x64-tile GEMM into H1, then the LN + GELU row kernel
           g.Y = w.H1; g.ldy = 2 * D;
           LG_HIP(gemmh(g, EPI_STORE));
-          LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, w.Hp, RP, w.ovf, st));
+          LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, w.Hp, RP, ro_h, st));
         } else {
           g.Yp = w.Hp; g.yps = (long long)RP * 2 * D; g.yrows_pad = RP; g.ln_g = Wb + bw.g; g.ln_b = Wb + bw.be;
+          g.ro = ro_h;
           LG_HIP(gemmh(g, EPI_LN_GELU));
         }
+        const int s_xn = slot();
         g = gemm_h3_base();
         g.A0 = image(w.Hp, 2 * D); g.K0 = 2 * D; g.K = 2 * D; wplanes(g, bw.W2); g.bias = Wb + bw.b2;
+        g.rtab = rt; g.a0_slot = s_h;
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
         g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP;
+        g.ro = ro(s_x, 1.f, s_h, gn.g2, gn.b2, s_xn);  // |x + ffn(..)| <= M_x + |W2|_1 M_h + |b2|
         LG_HIP(gemmh(g, EPI_STORE));
+        s_x = s_xn;
       } else {
         if (!h->fold) {
           GemmArgs g = gemm_base();
@@ -751,7 +835,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         g.A0 = w.X; g.lda0 = D; g.K0 = D; g.A1 = h->fold ? w.ctx : w.msg; g.lda1 = D; g.K = 2 * D;
         g.W = Wb + bw.W1; g.ldw = 2 * D; g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
         LG_HIP(gemm(g, EPI_STORE, 1));
-        LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, nullptr, 0, nullptr, st));
+        LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, nullptr, 0, range_none(), st));
         g = gemm_base();
         g.A0 = w.H1; g.lda0 = 2 * D; g.K0 = 2 * D; g.K = 2 * D; g.W = Wb + bw.W2; g.ldw = 2 * D; g.bias = Wb + bw.b2;
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
@@ -812,7 +896,11 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       N = N2;
       if (M == 0 || N == 0)
         return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size (all keypoints pruned)");
-      if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, M + N, D, D, w.Xp, RP, 0, w.ovf, st));
+      if (prec == PREC_H3) {
+        const int s_c = slot();
+        LG_HIP(rows_to_planes(w.X, M + N, D, D, w.Xp, RP, 0, ro(s_x, 1.f, -1, 0.f, 0.f, s_c), st));
+        s_x = s_c;
+      }
     }
   }
   out->stop_layer = stop;
@@ -827,6 +915,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     if (prec == PREC_H3) {
       GemmH3Args g = gemm_h3_base();
       g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, la.Wf); g.bias = Wb + la.bf;
+      g.rtab = rt; g.a0_slot = s_x;
       g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
       LG_HIP(gemmh(g, EPI_STORE));
     } else {
@@ -866,21 +955,9 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
 int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* workspace, size_t workspace_bytes,
                void* stream) {
   if (!h || !in || !out) return fail(LG_E_INVALID, "null argument");
-  const int first = h->cfg.precision == LG_PREC_X6 ? lg::PREC_X6 : lg::PREC_H3;
-  int rc = forward_pass(h, in, out, workspace, workspace_bytes, stream, first);
-  // a failed pass is re-checked too: a value outside the fp16 range turns into inf/NaN, which can
-  // make the pass fail (e.g. NaN matchability prunes every point) where bf16x6 would not
-  if (first != lg::PREC_H3 || (rc != LG_OK && rc != LG_E_INVALID)) return rc;
-  if (rc == LG_E_INVALID && !h->pass_started) return rc;  // argument error: nothing was enqueued
-  // fp16-range guard: an operand outside the fp16 range makes the fp16x3 result unreliable;
-  // recompute the whole forward in bf16x6 (full fp32 range) -- rare by design
-  const Work w = carve((char*)workspace, in->B, in->M, in->N, prune_enabled(h->cfg), h->cfg.input_dim);
-  int flag = 0;
-  hipStream_t st = (hipStream_t)stream;
-  LG_HIP(hipMemcpyAsync(&flag, w.ovf, sizeof(int), hipMemcpyDeviceToHost, st));
-  LG_HIP(hipStreamSynchronize(st));
-  if (flag) rc = forward_pass(h, in, out, workspace, workspace_bytes, stream, lg::PREC_X6);
-  return rc;
+  // fp16x3 needs no guard or rerun: run-time operands are range-scaled on the device
+  return forward_pass(h, in, out, workspace, workspace_bytes, stream,
+                      h->cfg.precision == LG_PREC_X6 ? lg::PREC_X6 : lg::PREC_H3);
 }
 
 int lg_profile_enable(lg_handle_t* h, int enable) {
@@ -953,7 +1030,7 @@ namespace {
 size_t attention_ws(int B, int H, int Nq, int Nk, size_t& kv_off, size_t& img_off, int& rp) {
   const size_t n = (size_t)B * H * Nk * 64;
   rp = (int)(((size_t)B * Nq + 255) / 256 * 256);
-  kv_off = 256;                              // [ovf flag | k planes (3 max) | v planes | ctx image]
+  kv_off = 256;                              // [range table | k planes (3 max) | v planes | ctx image]
   img_off = kv_off + 2 * 3 * n * 2;
   return img_off + (size_t)2 * rp * 256 * 2;
 }
@@ -978,28 +1055,27 @@ int lg_attention(const float* q, const float* k, const float* v, int32_t B, int3
   if (B == 0 || Nq == 0) return LG_OK;
   hipStream_t st = (hipStream_t)stream;
   char* ws = static_cast<char*>(workspace);
-  int* ovf = reinterpret_cast<int*>(ws);
+  unsigned* rtab = reinterpret_cast<unsigned*>(ws);  // slots 0/1: max|k|, max|v|; 2/3: k, v planes
   const size_t n = (size_t)B * H * Nk * 64;
   const int prec = precision == LG_PREC_X6 ? lg::PREC_X6 : lg::PREC_H3;
   const int np = prec == lg::PREC_X6 ? 3 : 2;
   void* kp = ws + kv_off;
   void* vp = ws + kv_off + np * n * 2;
   _Float16* img = reinterpret_cast<_Float16*>(ws + img_off);
-  LG_HIP(hipMemsetAsync(ovf, 0, sizeof(int), st));
-  LG_HIP(lg::split_planes(k, n, kp, prec, ovf, st));
-  LG_HIP(lg::split_planes(v, n, vp, prec, ovf, st));
-  if (prec == lg::PREC_H3) {
-    int flag = 0;
-    LG_HIP(hipMemcpyAsync(&flag, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
-    LG_HIP(hipStreamSynchronize(st));
-    if (flag) return fail(LG_E_INVALID, "k or v outside the fp16 range (use LG_PREC_X6)");
+  const bool h3 = prec == lg::PREC_H3;
+  LG_HIP(hipMemsetAsync(rtab, 0, 8 * sizeof(unsigned), st));
+  if (h3) {
+    LG_HIP(lg::range_absmax(k, n, rtab, 0, st));
+    LG_HIP(lg::range_absmax(v, n, rtab, 1, st));
   }
+  LG_HIP(lg::split_planes(k, n, kp, prec, lg::RangeOut{h3 ? rtab : nullptr, 0, -1, 1.f, 0.f, 0.f, 2}, st));
+  LG_HIP(lg::split_planes(v, n, vp, prec, lg::RangeOut{h3 ? rtab : nullptr, 1, -1, 1.f, 0.f, 0.f, 3}, st));
   // one set; the second set is empty (Nq = 0: its workgroups exit at once)
-  const lg::AttnSet s0{q, kp, vp, (long long)n, ctx, Nq, Nk, img, (long long)rp * 256, rp, 0};
+  const lg::AttnSet s0{q, kp, vp, (long long)n, ctx, Nq, Nk, img, (long long)rp * 256, rp, 0, h3 ? rtab : nullptr, 2};
   lg::AttnSet s1 = s0;
   s1.Nq = 0;
   LG_HIP(lg::attention_f32(s0, s1, B, H, scale, prec, st));
-  if (prec == lg::PREC_H3) LG_HIP(lg::image_to_rows(img, (long long)rp * 256, rp, 256, ctx, B * Nq, st));
+  if (h3) LG_HIP(lg::image_to_rows(img, (long long)rp * 256, rp, 256, ctx, B * Nq, rtab, 3, st));
   LG_HIP(hipStreamSynchronize(st));
   return LG_OK;
 }

@@ -111,7 +111,7 @@ def _ptr(t):
 
 
 # Extension keys (no reference counterpart).  "precision": matrix-core operand format of the HIP
-# kernels, both fp32-accurate -- "auto" (fp16x3 with a guarded bf16x6 rerun) or "bf16x6"
+# kernels, both fp32-accurate -- "auto" (fp16x3, run-time operands range-scaled on the device) or "bf16x6"
 # (DESIGN.md §3).
 EXTENSION_CONF = {"precision": "auto"}
 

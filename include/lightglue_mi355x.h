@@ -14,9 +14,9 @@
  *   - Every pointer argument marked "device" is caller-allocated HIP device memory on the
  *     handle's device (torch CUDA tensors on ROCm); the library never frees caller memory.
  *   - All device work is stream-ordered on `stream` (a hipStream_t; NULL = default stream).
- *     lg_forward synchronises the stream when pruning / early stop is enabled (the kept point
- *     counts decide launch sizes, as the reference's torch.where does) and, with
- *     LG_PREC_AUTO, once at the end to read the fp16-range guard.
+ *     lg_forward is fully asynchronous without pruning / early stop; with them it synchronises
+ *     the stream where the kept point counts decide launch sizes (as the reference's torch.where
+ *     does).
  *   - Functions return 0 on success and a negative LG_E* code on failure; lg_last_error()
  *     returns a thread-local message for the last failure on the calling thread.
  *   - A handle belongs to one device; it is not re-entrant (one forward at a time), separate
@@ -59,9 +59,10 @@ typedef struct {
    * (e.g. 1 - width_confidence, :590) before the fp32 comparison. */
   int32_t precision;        /* matrix-core operand format (no reference counterpart; both are
                              * fp32-accurate):
-                             *   LG_PREC_AUTO  fp16x3, guarded: if any run-time operand leaves the
-                             *                 fp16 range the forward is recomputed in bf16x6
-                             *   LG_PREC_X6    always bf16x6 */
+                             *   LG_PREC_AUTO  fp16x3; run-time operands are written scaled by a
+                             *                 per-tensor power of two chosen on the device, so
+                             *                 any fp32 magnitude is handled without a host check
+                             *   LG_PREC_X6    bf16x6 */
 } lg_config_t;
 
 enum { LG_PREC_AUTO = 0, LG_PREC_X6 = 1 };
@@ -102,7 +103,7 @@ typedef struct {
   float* layer_descriptors1;    /* device [B,L,N,256] or NULL */
   int32_t stop_layer;           /* host out: index of the last executed layer */
   int32_t kept0, kept1;         /* host out: M', N' after width pruning (= M, N without) */
-  int32_t precision_used;       /* host out: 0 = fp16x3, 1 = bf16x6 (LG_PREC_X6, or the guarded rerun) */
+  int32_t precision_used;       /* host out: 0 = fp16x3, 1 = bf16x6 (LG_PREC_X6) */
 } lg_outputs_t;
 
 int lg_abi_version(void);
@@ -166,8 +167,8 @@ int lg_log_optimal_transport(const float* scores, float alpha, int32_t B, int32_
  * lightglue.py:139-149 in isolation): one launch of the forward's attention kernel.
  * q, k, v: fp32 head-major [B][H][Nq or Nk][64] device tensors, H * 64 == 256; ctx: fp32
  * [B][Nq][256] (column h*64 + d), softmax(scale * q k^T) v.  precision LG_PREC_AUTO runs the fp16x3
- * kernel (k and v must lie in the fp16 range, else LG_E_INVALID), LG_PREC_X6 the bf16x6 one.
- * Synchronises the stream (reads the range flag).  Workspace: lg_attention_workspace_bytes. */
+ * kernel (k and v range-scaled on the device), LG_PREC_X6 the bf16x6 one.  Synchronises the
+ * stream before returning.  Workspace: lg_attention_workspace_bytes. */
 int lg_attention_workspace_bytes(int32_t B, int32_t H, int32_t Nq, int32_t Nk, size_t* bytes);
 int lg_attention(const float* q, const float* k, const float* v, int32_t B, int32_t H, int32_t Nq,
                  int32_t Nk, float scale, int32_t precision, float* ctx, void* workspace,

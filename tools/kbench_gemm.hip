@@ -117,7 +117,7 @@ int main() {
     CK(hipMalloc(&g_aplanes, (size_t)2 * s.R * s.K * 2));
     // fill() draws from [-1, 1): max|W| < 1 -> scale 2^3 puts max|W 2^sw| in [4, 8) (< 16)
     CK(split_weight_h3(W, s.N, s.K, 8.f, g_planes, 0));
-    CK(rows_to_planes(A, s.R, s.K, s.K, g_aplanes, s.R, 0, nullptr, 0));
+    CK(rows_to_planes(A, s.R, s.K, s.K, g_aplanes, s.R, 0, range_none(), 0));
     g_unscale = ldexpf(1.f, -(11 + 3));
     _Float16* Yp;
     CK(hipMalloc(&Yp, (size_t)2 * s.R * s.N * 2));

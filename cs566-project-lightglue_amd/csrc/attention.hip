@@ -167,13 +167,14 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
     const float m_new = fmaxf(m_run, tmax);
     const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2e);
     m_run = m_new;
-    const float mb = m_new * scale_log2e;
+    // (s - m) first: exact for the keys that matter, whatever the logits' magnitude (the fused
+    // fma(s, c, -m c) loses absolute accuracy once m c is beyond 2^24)
     float psum = 0.f;
 #pragma unroll
     for (int u = 0; u < NSUB; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], scale_log2e, -mb));
+        const float p = __builtin_amdgcn_exp2f((sc[u][r] - m_new) * scale_log2e);
         sc[u][r] = p;
         psum += p;
       }
@@ -348,6 +349,11 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   f16x8 qh[2][2], qhs[2][2], ql[2][2];
   float c_lane[2];
   const int ek = range_slot_exp(S.rtab, S.k_slot);  // key planes hold k * 2^-ek (RangeOut)
+  // |scale q.k log2 e| <= 64 max|q_row| max|k| scale log2 e; beyond 2^21 the fused exponent
+  // argument fma(s, c, -(m c - 11)) loses its absolute accuracy (m c is rounded to fp32), so such
+  // waves form (s - m) first -- one more VALU per score, only for extreme data
+  const float kmax = S.rtab ? range_max(S.rtab, S.k_slot) : INFINITY;
+  bool big = false;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int qrow = min(q_blk + wave * 32 + qt * 16 + r16, Nq - 1);
@@ -362,6 +368,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[ks][0][e]), fabsf(x[ks][1][e])));
     }
     mx = max_x16_32(mx);
+    big |= !(64.f * mx * kmax * scale_log2e <= 2097152.f);
     int ex = 0;
     if (mx > 0.f && mx <= 3.0e38f) {
       int E;
@@ -381,6 +388,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       }
   }
 
+  const bool exact = __builtin_amdgcn_readfirstlane((int)(__ballot(big) != 0ull)) != 0;  // wave-uniform
   // LDS-DMA staging of one LDS tile (keys t0 .. t0+LT-1) into buffer buf: piece q (wave-uniform)
   // = 8 rows of one plane of K (q < PIECES/2) or V; lane i fills LDS slot (row i>>3, chunk i&7)
   // with the source chunk that the swizzle puts there (rows past Nk repeat row Nk-1)
@@ -419,9 +427,10 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
 
   // one 64-key softmax step over LDS rows off .. off+63 of the current buffer (off: element
   // offset buf*2*PL + sub*KT*kHeadDim, a compile-time constant in the main loop)
-  auto body = [&](auto OFFc, auto MASKc, int t0) {
+  auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0) {
     const int off = OFFc;
     constexpr bool MASK = decltype(MASKc)::value;
+    constexpr bool EXACT = decltype(EXc)::value;
     // from the __shared__ arrays themselves (not captured pointers), so the reads stay ds_read
     const _Float16* Kc = Ks + r16 * kHeadDim + off;
     const _Float16* Vc = Vs + vrow * kHeadDim + 4 * (vp4 & 1) + off;
@@ -488,16 +497,27 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
           for (int r = 0; r < 4; ++r) o[dt][qt][r] *= alpha;
       }
       // e = p 2^11
-      const float mb = fmaf(m_use[qt], c_lane[qt], -11.f);
       float ps4[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (!EXACT) {
+        const float mb = fmaf(m_use[qt], c_lane[qt], -11.f);
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt)
+        for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][qt][r], c_lane[qt], -mb));
-          sc[kt][qt][r] = e;
-          ps4[r] += e;
-        }
+          for (int r = 0; r < 4; ++r) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][qt][r], c_lane[qt], -mb));
+            sc[kt][qt][r] = e;
+            ps4[r] += e;
+          }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][qt][r] - m_use[qt], c_lane[qt], 11.f));
+            sc[kt][qt][r] = e;
+            ps4[r] += e;
+          }
+      }
       l_run[qt] += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
     }
 #pragma unroll
@@ -535,29 +555,38 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int t = 0;
-  for (; t + 2 <= nfull; t += 2) {
-    if (t + 1 < nlt) issue((t + 1) * LT, 1);  // buffer 1 was released by the last barrier
-    body(IC0{}, NoMask{}, t * LT);
-    if constexpr (SUBS == 2) body(IC1{}, NoMask{}, t * LT + KT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 2 < nlt) issue((t + 2) * LT, 0);
-    body(IC2{}, NoMask{}, (t + 1) * LT);
-    if constexpr (SUBS == 2) body(IC3{}, NoMask{}, (t + 1) * LT + KT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  // the tile loop in two copies (normal / exact exponent arguments): the choice is one uniform
+  // branch here, none inside the loop, so the common copy keeps its schedule (a macro, not a
+  // lambda: a closure around `issue` would leave its uniform operands in VGPRs)
+#define LG_ATTN_TILES(EXc)                                                          \
+  {                                                                                 \
+    int t = 0;                                                                      \
+    for (; t + 2 <= nfull; t += 2) {                                                \
+      if (t + 1 < nlt) issue((t + 1) * LT, 1); /* buffer 1 released by the barrier */ \
+      body(IC0{}, NoMask{}, EXc, t * LT);                                           \
+      if constexpr (SUBS == 2) body(IC1{}, NoMask{}, EXc, t * LT + KT);             \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
+      __syncthreads();                                                              \
+      if (t + 2 < nlt) issue((t + 2) * LT, 0);                                      \
+      body(IC2{}, NoMask{}, EXc, (t + 1) * LT);                                     \
+      if constexpr (SUBS == 2) body(IC3{}, NoMask{}, EXc, (t + 1) * LT + KT);       \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
+      __syncthreads();                                                              \
+    }                                                                               \
+    for (; t < nlt; ++t) { /* at most two LDS tiles: masked steps, runtime buffer */ \
+      const int buf = t & 1;                                                        \
+      if (t + 1 < nlt) issue((t + 1) * LT, buf ^ 1);                                \
+      for (int sub = 0; sub < SUBS; ++sub) {                                        \
+        const int s0 = t * LT + sub * KT;                                           \
+        if (s0 < Nk) body(buf * 2 * PL + sub * KT * kHeadDim, Mask{}, EXc, s0);     \
+      }                                                                             \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
+      __syncthreads();                                                              \
+    }                                                                               \
   }
-  for (; t < nlt; ++t) {  // at most two LDS tiles: masked steps, runtime buffer
-    const int buf = t & 1;
-    if (t + 1 < nlt) issue((t + 1) * LT, buf ^ 1);
-    for (int sub = 0; sub < SUBS; ++sub) {
-      const int s0 = t * LT + sub * KT;
-      if (s0 < Nk) body(buf * 2 * PL + sub * KT * kHeadDim, Mask{}, s0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  if (exact) LG_ATTN_TILES((std::integral_constant<bool, true>{}))
+  else LG_ATTN_TILES((std::integral_constant<bool, false>{}))
+#undef LG_ATTN_TILES
 
   // context rows into the plane image: o = 2^11 sum(v p) (the MFMA scale), l_run = 2^11 sum(p),
   // so 1 / l_run is the old 2^-11 / l exactly; v arrived as v * 2^-E[v] and the context leaves

@@ -199,31 +199,60 @@ __device__ __forceinline__ size_t plane_off(int row, int k, int rows_pad) {
 }
 
 // ---- run-time range scaling of plane images (kernels.h RangeOut) ----------------------------
+// Table layout: slot s occupies kRangeStride words -- M as kRangeShards shards (a writing
+// workgroup updates shard blockIdx.x % kRangeShards, so thousands of workgroups do not serialise
+// on one address; M = max over the shards), then E.
+constexpr int kRangeShards = 16, kRangeStride = 32;
 constexpr float kRangeLimit = 32768.f;  // 2^15: half the fp16 range, so rounding cannot reach inf
+__device__ __forceinline__ float range_max(const unsigned* tab, int s) {
+  const unsigned* p = tab + s * kRangeStride;
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < kRangeShards; ++i) m = fmaxf(m, __uint_as_float(p[i]));
+  return m;
+}
 template <class RO>
 __device__ __forceinline__ int range_exponent(const RO& r) {
   if (!r.tab) return 0;
   float b = r.add;
-  if (r.in0 >= 0) b += r.g0 * __uint_as_float(r.tab[2 * r.in0]);
-  if (r.in1 >= 0) b += r.g1 * __uint_as_float(r.tab[2 * r.in1]);
+  if (r.in0 >= 0) b += r.g0 * range_max(r.tab, r.in0);
+  if (r.in1 >= 0) b += r.g1 * range_max(r.tab, r.in1);
   if (!(b > kRangeLimit) || !(b <= 3.0e38f)) return 0;  // in range, or non-finite data
   int E;
   (void)frexpf(b * (1.f / kRangeLimit), &E);  // b / 2^15 = m 2^E, m in [0.5, 1)  ->  2^E >= it
   return E;
 }
 __device__ __forceinline__ int range_slot_exp(const unsigned* tab, int slot) {
-  return (tab && slot >= 0) ? (int)tab[2 * slot + 1] : 0;
+  return (tab && slot >= 0) ? (int)tab[slot * kRangeStride + kRangeShards] : 0;
 }
-// wave-wide max of |x| written -> M[out], and E[out] (every writing wave stores the same value);
-// called by all 64 lanes of a wave that wrote planes under `r`
+// Block-wide max of |x| written -> one atomicMax into this workgroup's shard of M[out], and
+// E[out] (stored only when not the table's initial 0; every writer stores the same value).
+// Called by every thread of the workgroup (it contains a barrier).
+// range_commit_lds reuses 16 floats of the caller's LDS (kernels that declare all of it) and
+// first waits for every wave to be done with it.
+template <class RO>
+__device__ __forceinline__ void range_commit_lds(const RO& r, float lane_max, int e, float* red) {
+  if (!r.tab) return;
+  if (!r.track) {  // E only: no reduction, no barrier (E != 0 is rare)
+    if (e != 0 && (threadIdx.x & 63) == 0) r.tab[r.out * kRangeStride + kRangeShards] = (unsigned)e;
+    return;
+  }
+  const float m = wave_max_dpp(lane_max);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float mm = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) mm = fmaxf(mm, red[w]);
+    unsigned* slot = r.tab + r.out * kRangeStride;
+    if (mm > 0.f) atomicMax(slot + (blockIdx.x % kRangeShards), __float_as_uint(mm));
+    if (e != 0) slot[kRangeShards] = (unsigned)e;
+  }
+}
 template <class RO>
 __device__ __forceinline__ void range_commit(const RO& r, float lane_max, int e) {
-  if (!r.tab) return;
-  const float m = wave_max_dpp(lane_max);
-  if ((threadIdx.x & 63) == 0) {
-    if (m > 0.f) atomicMax(r.tab + 2 * r.out, __float_as_uint(m));
-    r.tab[2 * r.out + 1] = (unsigned)e;
-  }
+  __shared__ float range_red[16];
+  range_commit_lds(r, lane_max, e, range_red);
 }
 
 // ---- LDS-DMA ------------------------------------------------------------------------------

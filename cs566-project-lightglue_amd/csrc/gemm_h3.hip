@@ -101,6 +101,10 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   const int e0 = range_slot_exp(g.rtab, g.a0_slot);
   const int e1 = g.K0 < g.K ? range_slot_exp(g.rtab, g.a1_slot) : e0;
   const float accs = ldexpf(g.acc_scale, e1);  // after the k-loop the accumulator holds 2^-e1 units
+  // exponents of the planes this launch writes, read here so the loads are long done by the
+  // epilogue (QKV: waves of a workgroup share one output type -- a 256-column tile is one of q/k/v)
+  const int eo_main = range_exponent(g.ro);
+  const int eo_v = (EPI == EPI_QKV_ROT || EPI == EPI_CROSS_QKV) ? range_exponent(g.ro_v) : 0;
 
   const int num_m = (g.R + BM - 1) / BM, num_n = g.Nout / BN;
   const int tile = xcd_remap_h3(blockIdx.x, num_m * num_n);
@@ -329,7 +333,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     __syncthreads();
     // normalise + GELU, then 16-byte plane-image stores through the per-wave transpose buffer
     const int cq = (lane & 7) * 8;
-    const int eo = range_exponent(g.ro);
+    const int eo = eo_main;
     const float so = ldexpf(1.f, -eo);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -368,7 +372,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
       }
     }
-    range_commit(g.ro, wmax, eo);
+    range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem));
   } else if constexpr (EPI == EPI_STORE) {
     static_assert(WN == 64, "EPI_STORE tile");
     // Transposed through LDS (free after the k-loop; 8 KiB per wave per 32-row pass) so that every
@@ -379,7 +383,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
     const int cq = (lane & 7) * 8;                     // first of the lane's 8 columns (in the wave tile)
     const int col0 = n0 + wn0 + cq;
-    const int eo = g.Yp ? range_exponent(g.ro) : 0;
+    const int eo = g.Yp ? eo_main : 0;
     const float so = ldexpf(1.f, -eo);
     f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
     if (g.bias) {
@@ -439,7 +443,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
-    if (g.Yp) range_commit(g.ro, wmax, eo);
+    if (g.Yp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem));
   } else {
     static_assert(WN == 64, "QKV epilogue tile");
     // Head-major scatter through the same LDS transpose as EPI_STORE.  The wave's 64 columns are
@@ -464,7 +468,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     const bool to_kp = EPI == EPI_QKV_ROT ? t == 1 : t == 0;
     const bool to_vp = EPI == EPI_QKV_ROT ? t == 2 : t == 1;
     const float sc = (EPI == EPI_CROSS_QKV && t == 0) ? hl.qk_scale : 1.f;
-    const int eo = to_kp ? range_exponent(g.ro) : to_vp ? range_exponent(g.ro_v) : 0;
+    const int eo = to_kp ? eo_main : to_vp ? eo_v : 0;
     const float so = ldexpf(1.f, -eo);
     float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
     const int d0 = (lane & 7) * 8;  // the lane's first dim
@@ -526,8 +530,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
-    if (to_kp) range_commit(g.ro, wmax, eo);
-    else if (to_vp) range_commit(g.ro_v, wmax, eo);
+    if (to_kp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem));
+    else if (to_vp) range_commit_lds(g.ro_v, wmax, eo, reinterpret_cast<float*>(smem));
   }
 }
 
@@ -606,12 +610,11 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
 // initial value taken in the same read)
 __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
                                       RangeOut ro, float* xc) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int nch = K / 8;
   const int eo = range_exponent(ro);
   const float so = ldexpf(1.f, -eo);
   float wmax = 0.f;
-  if (i < (size_t)R * nch) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)R * nch; i += (size_t)gridDim.x * blockDim.x) {
     const int r = (int)(i / nch), c = (int)(i % nch);
     const float* p = x + (size_t)r * ld + c * 8;
     const f32x4 v0 = *reinterpret_cast<const f32x4*>(p), v1 = *reinterpret_cast<const f32x4*>(p + 4);
@@ -642,7 +645,7 @@ hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes
   if (R <= 0) return hipSuccess;
   if (K % kKB || rows_pad < row0 + R) return hipErrorInvalidValue;
   const size_t n = (size_t)R * (K / 8);
-  hipLaunchKernelGGL(rows_to_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, R, K, ld, planes,
+  hipLaunchKernelGGL(rows_to_planes_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 2048)), dim3(256), 0, st, x, R, K, ld, planes,
                      rows_pad, row0, ro, xcopy);
   return hipGetLastError();
 }
@@ -655,8 +658,7 @@ __global__ void range_absmax_kernel(const float* x, size_t n, unsigned* tab, int
   float m = 0.f;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     m = fmaxf(m, fabsf(x[i]));
-  m = wave_max_dpp(m);
-  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(tab + 2 * slot, __float_as_uint(m));
+  range_commit(RangeOut{tab, -1, -1, 0.f, 0.f, 0.f, slot, 1}, m, 0);
 }
 
 hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipStream_t st) {

@@ -21,9 +21,10 @@ enum EpiKind {
 enum Prec { PREC_H3 = 0, PREC_X6 = 1 };
 
 // Run-time range scaling of fp16x3 plane images.  A forward keeps a small table
-// in its workspace, zeroed at the start; slot s holds
-//   tab[2s]     M[s]: max |x| over the values written (float bits; atomicMax of non-negative floats)
-//   tab[2s + 1] E[s]: the exponent the planes were written with -- they hold x * 2^-E[s]
+// in its workspace, zeroed at the start; slot s holds (common.h: sharded layout)
+//   M[s]: max |x| over the values written (float bits; atomicMax of non-negative floats), kept
+//         only where a later bound needs it (track = 1: the residual stream)
+//   E[s]: the exponent the planes were written with -- they hold x * 2^-E[s]
 // A producer chooses E before writing from an upper bound of what it will write,
 //   bound = g0 * M[in0] + g1 * M[in1] + add     (in0/in1: slots of its inputs, -1 = unused;
 //                                                g0/g1/add: weight row-L1 norms and bias maxima)
@@ -36,8 +37,9 @@ struct RangeOut {
   int in0, in1;
   float g0, g1, add;
   int out;
+  int track;          // 1: record M[out] (only the residual stream's images need it; E is always kept)
 };
-inline RangeOut range_none() { return RangeOut{nullptr, -1, -1, 0.f, 0.f, 0.f, 0}; }
+inline RangeOut range_none() { return RangeOut{nullptr, -1, -1, 0.f, 0.f, 0.f, 0, 0}; }
 
 // Head-major destinations [set][b][h][n][64] for the QKV epilogues; set 0 = image 0 (B*M rows),
 // set 1 = image 1 (B*N rows), rows in GEMM order (image 0 rows first).  All in natural dim order.

@@ -2,6 +2,7 @@
 // orchestration (reference gluefactory/models/matchers/lightglue.py:444-579).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -12,6 +13,7 @@
 
 #include "../../include/lightglue_mi355x.h"
 #include "kernels.h"
+#include "common.h"
 
 namespace {
 
@@ -340,7 +342,7 @@ Work carve(char* base, int B, int M, int N, bool prune, int din) {
   w.tok = tf(R);
   w.sim = tf((size_t)B * M * N);
   w.aws = tf(lg::assign_workspace_floats(B, M, N));
-  w.rtab = reinterpret_cast<unsigned*>(ti(2 * kRangeSlots));
+  w.rtab = reinterpret_cast<unsigned*>(ti(kRangeSlots * lg::kRangeStride));
   if (prune) {
     w.X2 = tf(R * D);
     w.cos2 = tf(R * 32);
@@ -662,10 +664,10 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   unsigned* rt = prec == PREC_H3 ? w.rtab : nullptr;
   int nslot = 0;
   auto slot = [&]() { return nslot < kRangeSlots ? nslot++ : kRangeSlots - 1; };
-  auto ro = [&](int in0, float g0, int in1, float g1, float add, int out) {
-    return RangeOut{rt, in0, in1, g0, g1, add, out};
+  auto ro = [&](int in0, float g0, int in1, float g1, float add, int out, int track = 0) {
+    return RangeOut{rt, in0, in1, g0, g1, add, out, track};
   };
-  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.rtab, 0, 2 * kRangeSlots * sizeof(unsigned), st));
+  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.rtab, 0, kRangeSlots * lg::kRangeStride * sizeof(unsigned), st));
   h->pass_started = true;
   int s_x = -1;  // slot of the current residual-stream plane image Xp
   // ---- input projection (lightglue.py:370-373,486-487); H3 also builds x's plane image
@@ -689,7 +691,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       GemmH3Args g = gemm_h3_base();
       g.A0 = image(w.Dp, din); g.K0 = din; g.K = din; wplanes(g, h->Wi); g.rtab = rt; g.a0_slot = s_d;
       g.bias = Wb + h->bi; g.R = B * (M + N); g.Nout = D; g.Y = w.X; g.ldy = D;
-      g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP; g.ro = ro(s_d, h->gi, -1, 0.f, h->bi_max, s_x);
+      g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP; g.ro = ro(s_d, h->gi, -1, 0.f, h->bi_max, s_x, 1);
       LG_HIP(gemmh(g, EPI_STORE));
     } else {
       GemmArgs g = gemm_base();
@@ -709,13 +711,13 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     }
     if (prec == PREC_H3 && din_a16) {
       // residual stream and its plane image from one read of the descriptors
-      LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x), st, w.X));
-      LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, ro(s_in, 1.f, -1, 0.f, 0.f, s_x), st,
+      LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st, w.X));
+      LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st,
                             w.X + (size_t)B * M * D));
     } else {
       LG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
       LG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
-      if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, B * (M + N), D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x), st));
+      if (prec == PREC_H3) LG_HIP(rows_to_planes(w.X, B * (M + N), D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st));
     }
   }
 
@@ -761,8 +763,8 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         GemmH3Args g = gemm_h3_base();
         g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, bw.Wqkv); g.bias = Wb + bw.bqkv;
         g.rtab = rt; g.a0_slot = s_x;
-        g.ro = ro(s_x, gn.gK, -1, 0.f, gn.bK, s_k);
-        g.ro_v = ro(s_x, gn.gV, -1, 0.f, gn.bV, s_v);
+        g.ro = ro(s_x, gn.gK, -1, 0.f, gn.bK, s_k, 1);  // M[k]: the attention's exact-softmax test
+        g.ro_v = ro(s_x, gn.gV, -1, 0.f, gn.bV, s_v, h->fold ? 0 : 1);
         g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D; g.hl = hl;
         LG_HIP(gemmh(g, epi_qkv));
       } else {
@@ -821,7 +823,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         g.rtab = rt; g.a0_slot = s_h;
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
         g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP;
-        g.ro = ro(s_x, 1.f, s_h, gn.g2, gn.b2, s_xn);  // |x + ffn(..)| <= M_x + |W2|_1 M_h + |b2|
+        g.ro = ro(s_x, 1.f, -1, 0.f, gn.g2 * gn.hb + gn.b2, s_xn, 1);  // |x + ffn(..)| <= M_x + |W2|_1 hb + |b2|
         LG_HIP(gemmh(g, EPI_STORE));
         s_x = s_xn;
       } else {
@@ -898,7 +900,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size (all keypoints pruned)");
       if (prec == PREC_H3) {
         const int s_c = slot();
-        LG_HIP(rows_to_planes(w.X, M + N, D, D, w.Xp, RP, 0, ro(s_x, 1.f, -1, 0.f, 0.f, s_c), st));
+        LG_HIP(rows_to_planes(w.X, M + N, D, D, w.Xp, RP, 0, ro(s_x, 1.f, -1, 0.f, 0.f, s_c, 1), st));
         s_x = s_c;
       }
     }
@@ -931,6 +933,20 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     g.W = w.md + (size_t)B * M * D; g.ldw = D; g.sW = (long long)N * D;
     g.R = M; g.Nout = N; g.Y = w.sim; g.ldy = N; g.sY = (long long)M * N;
     LG_HIP(gemm(g, EPI_STORE, B));
+  }
+  if (rt && getenv("LG_DEBUG_RANGE")) {  // diagnostic: the range table of this forward
+    std::vector<unsigned> tab((size_t)nslot * lg::kRangeStride);
+    LG_HIP(hipMemcpyAsync(tab.data(), rt, tab.size() * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    LG_HIP(hipStreamSynchronize(st));
+    for (int k = 0; k < nslot; ++k) {
+      float m = 0.f;
+      for (int j = 0; j < lg::kRangeShards; ++j) {
+        float v;
+        memcpy(&v, &tab[(size_t)k * lg::kRangeStride + j], 4);
+        m = std::max(m, v);
+      }
+      fprintf(stderr, "range slot %d: max %.4g exp %d\n", k, m, (int)tab[(size_t)k * lg::kRangeStride + lg::kRangeShards]);
+    }
   }
   AssignArgs aa;
   aa.sim = w.sim; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = out->log_assignment; aa.ws = w.aws;
@@ -1030,7 +1046,7 @@ namespace {
 size_t attention_ws(int B, int H, int Nq, int Nk, size_t& kv_off, size_t& img_off, int& rp) {
   const size_t n = (size_t)B * H * Nk * 64;
   rp = (int)(((size_t)B * Nq + 255) / 256 * 256);
-  kv_off = 256;                              // [range table | k planes (3 max) | v planes | ctx image]
+  kv_off = 4 * 32 * 4;                       // [range table (4 slots) | k planes (3 max) | v planes | ctx image]
   img_off = kv_off + 2 * 3 * n * 2;
   return img_off + (size_t)2 * rp * 256 * 2;
 }
@@ -1063,13 +1079,13 @@ int lg_attention(const float* q, const float* k, const float* v, int32_t B, int3
   void* vp = ws + kv_off + np * n * 2;
   _Float16* img = reinterpret_cast<_Float16*>(ws + img_off);
   const bool h3 = prec == lg::PREC_H3;
-  LG_HIP(hipMemsetAsync(rtab, 0, 8 * sizeof(unsigned), st));
+  LG_HIP(hipMemsetAsync(rtab, 0, 4 * lg::kRangeStride * sizeof(unsigned), st));
   if (h3) {
     LG_HIP(lg::range_absmax(k, n, rtab, 0, st));
     LG_HIP(lg::range_absmax(v, n, rtab, 1, st));
   }
-  LG_HIP(lg::split_planes(k, n, kp, prec, lg::RangeOut{h3 ? rtab : nullptr, 0, -1, 1.f, 0.f, 0.f, 2}, st));
-  LG_HIP(lg::split_planes(v, n, vp, prec, lg::RangeOut{h3 ? rtab : nullptr, 1, -1, 1.f, 0.f, 0.f, 3}, st));
+  LG_HIP(lg::split_planes(k, n, kp, prec, lg::RangeOut{h3 ? rtab : nullptr, 0, -1, 1.f, 0.f, 0.f, 2, 1}, st));
+  LG_HIP(lg::split_planes(v, n, vp, prec, lg::RangeOut{h3 ? rtab : nullptr, 1, -1, 1.f, 0.f, 0.f, 3, 1}, st));
   // one set; the second set is empty (Nq = 0: its workgroups exit at once)
   const lg::AttnSet s0{q, kp, vp, (long long)n, ctx, Nq, Nk, img, (long long)rp * 256, rp, 0, h3 ? rtab : nullptr, 2};
   lg::AttnSet s1 = s0;

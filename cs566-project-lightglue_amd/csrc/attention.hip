@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "kernels.h"
@@ -629,6 +630,327 @@ static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int
   return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------------------
+// attention_h3m_kernel: attention_h3g_kernel's pipeline (LDS-DMA K/V staging, pre-scaled P with
+// fma_mix low pieces, ballot-gated lazy reference, exact-exponent loop copy) on
+// v_mfma_f32_32x32x16_f16.  Why: the 16x16x32 MFMA holds the SIMD's VALU issue for 8 of its 16
+// cycles, the 32x32x16 one for 8 of its 32 (MI355X_MICROARCH.md, per-instruction constants).  The
+// h3g body issues ~180 VALU per 96 MFMAs per wave, so two waves on a SIMD need ~2 x (96 x 8 + ~820)
+// issue cycles against 2 x 96 x 16 MFMA cycles -- issue-bound with no room for the partner's
+// softmax; with 48 32x32 MFMAs the same work needs 2 x (48 x 8 + ~820) issue cycles against
+// 2 x 1536 MFMA cycles.  Layouts (the register-level mapping of tools/attn_h3_legacy.hip):
+//   S^T[key][query] = K Q^T: A = K (lane: key l&31 of a 32-key sub-tile, dims 16ks + 8(l>>5)..),
+//     B = Q^T (lane: query l&31, the same dims), four k-steps per head;
+//     accumulator register r of lane l: query l&31, key row32(r, l>>5).
+//   O^T[dim][query] += V^T P^T over 16-key steps: B = P^T = S^T registers 8s..8s+7 (keys
+//     ka + j / ka + 8 + j - 4, ka = 16s + 4(l>>5)); A = V^T from two ds_read_b64_tr_b16 per
+//     plane and 32-dim tile (rows ka + (l&15)>>2, +8).
+//   Per-query reductions: in-lane over 32 scores, then lane ^ 32 (v_permlane32_swap).
+// LDS: K as in h3g (16-byte chunk c of row r at c ^ ((r >> 1) & 7): the 32x32 fragment reads hit
+// 16 distinct slots per lane group too); V rows with the two 32-dim halves swapped where key bit 1
+// is set (each transposed read's 4 rows then cover all 64 banks).
+template <int SUBS, int PRIO, int WAVES = 8>
+__global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+                                                                float scale_log2e) {
+  constexpr int QB = 32 * WAVES;
+  constexpr int KT = 64;                   // keys per softmax step
+  constexpr int LT = KT * SUBS;            // keys per LDS tile (one barrier)
+  constexpr int PL = LT * kHeadDim;        // one plane of an LDS tile (elements)
+  constexpr int PIECES = 4 * LT / 8;       // 1 KiB LDS-DMA pieces per tile (K h/l, V h/l; 8 rows each)
+  constexpr int PPW = PIECES / WAVES;
+  static_assert(PIECES % WAVES == 0, "pieces per wave");
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[2 * 2 * PL];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[2 * 2 * PL];
+
+  const int item = xcd_chunk(blockIdx.x, gridDim.x);
+  const int qb = item % nqb;
+  const int sbh = item / nqb;
+  const int set = sbh / (B * H), bh = sbh - set * (B * H);
+  const AttnSet& S = set == 0 ? s0 : s1;
+  const int q_blk = qb * QB;
+  if (q_blk >= S.Nq) return;
+  const int Nq = S.Nq, Nk = S.Nk;
+  const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
+  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
+  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
+  const long long ps = S.pstride;
+  const int head = bh % H;
+  const int b = bh / H;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, half = lane >> 5;
+
+  // queries: lane = query l32 of the wave's 32, dims 16ks + 8 half + j, scaled per row by 2^ex
+  // so that the row max lies in [8, 16) (the per-lane factor folds into the exp argument)
+  const int ek = range_slot_exp(S.rtab, S.k_slot);  // key planes hold k * 2^-ek (RangeOut)
+  const float kmax = S.rtab ? range_max(S.rtab, S.k_slot) : INFINITY;
+  f16x8 qh[4], qhs[4], ql[4];
+  float c_lane;
+  bool big;
+  {
+    const int qrow = min(q_blk + wave * 32 + l32, Nq - 1);
+    const float* qr = Q + (size_t)qrow * kHeadDim + 8 * half;
+    f32x4 x[4][2];
+    float mx = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      x[ks][0] = *reinterpret_cast<const f32x4*>(qr + 16 * ks);
+      x[ks][1] = *reinterpret_cast<const f32x4*>(qr + 16 * ks + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[ks][0][e]), fabsf(x[ks][1][e])));
+    }
+    mx = max_xor32(mx);
+    big = !(64.f * mx * kmax * scale_log2e <= 2097152.f);  // see attention_h3g_kernel
+    int ex = 0;
+    if (mx > 0.f && mx <= 3.0e38f) {
+      int E;
+      (void)frexpf(mx, &E);
+      ex = min(max(4 - E, -100), 100);
+    }
+    c_lane = ldexpf(scale_log2e, ek - (11 + ex));
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 h, l;
+        split2h(ldexpf(x[ks][e >> 2][e & 3], ex), h, l);
+        qh[ks][e] = h;
+        ql[ks][e] = l;
+        qhs[ks][e] = h * (_Float16)kLoScale;
+      }
+  }
+  const bool exact = __builtin_amdgcn_readfirstlane((int)(__ballot(big) != 0ull)) != 0;  // wave-uniform
+
+  // LDS-DMA staging of one LDS tile (keys t0 .. t0+LT-1) into buffer buf, as in h3g, with the V
+  // half-swap swizzle (chunk cs of row r at cs ^ 4 ((r >> 1) & 1))
+  const uint32_t ks_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)Ks);
+  const uint32_t vs_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)Vs);
+  auto issue = [&](int t0, int buf) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;
+      const bool isv = q >= PIECES / 2;
+      const int qq = isv ? q - PIECES / 2 : q;
+      const int pl = qq / (LT / 8), r = (qq % (LT / 8)) * 8 + (lane >> 3), cs = lane & 7;
+      const int c = isv ? cs ^ (((r >> 1) & 1) << 2) : cs ^ ((r >> 1) & 7);
+      const _Float16* base = (isv ? Vp : Kp) + (size_t)pl * ps + (size_t)t0 * kHeadDim;
+      const uint32_t voff = (uint32_t)((min(t0 + r, Nk - 1) - t0) * kHeadDim + c * 8) * 2u;
+      const uint32_t dst = (isv ? vs_lds : ks_lds) + (uint32_t)(((buf * 2 + pl) * PL + (qq % (LT / 8)) * 8 * kHeadDim) * 2);
+      dma16(base, voff, dst);
+    }
+  };
+
+  // per-lane LDS offsets: K fragment row l32, chunk 2ks + half (swizzled); transposed V reads:
+  // 16-lane group covers dims 16 ((lane >> 4) & 1) + 4 (lane & 3) of lane half `half`, rows
+  // ka + ((lane & 15) >> 2) (+8)
+  int kcol[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kcol[ks] = l32 * kHeadDim + (((2 * ks + half) ^ ((l32 >> 1) & 7)) << 3);
+  const int tq = (lane & 15) >> 2, tdim = ((lane >> 4) & 1) * 16 + 4 * (lane & 3);
+  const int vsw = ((tq >> 1) & 1) << 5;
+  const int voff0 = (4 * half + tq) * kHeadDim + (tdim ^ vsw);
+  const int voff1 = (4 * half + tq) * kHeadDim + ((32 + tdim) ^ vsw);
+
+  f32x16 o0 = f32x16{0.f}, o1 = f32x16{0.f};  // O^T (x 2^11): dims [0,32) and [32,64)
+  float m_use = -INFINITY;
+  float l_run = 0.f;
+
+  auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0) {
+    const int off = OFFc;
+    constexpr bool MASK = decltype(MASKc)::value;
+    constexpr bool EXACT = decltype(EXc)::value;
+    f16x8 kf[2][4][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int o = off + u * 32 * kHeadDim + kcol[ks];
+        kf[u][ks][0] = *reinterpret_cast<const f16x8*>(Ks + o);
+        kf[u][ks][1] = *reinterpret_cast<const f16x8*>(Ks + PL + o);
+      }
+    asm volatile("" ::: "memory");
+    f32x16 sc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      sc[u] = f32x16{0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) sc[u] = mfma_h3(kf[u][ks][0], kf[u][ks][1], qhs[ks], ql[ks], qh[ks], sc[u]);
+    }
+    f16x8 vf[2][2][2][2];  // [u][s][dim tile][plane]
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int vr = off + (u * 32 + 16 * ss) * kHeadDim;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const f16x4 a0 = tr_read_h(Vs + p * PL + vr + voff0);
+          const f16x4 a1 = tr_read_h(Vs + p * PL + vr + 8 * kHeadDim + voff0);
+          const f16x4 b0 = tr_read_h(Vs + p * PL + vr + voff1);
+          const f16x4 b1 = tr_read_h(Vs + p * PL + vr + 8 * kHeadDim + voff1);
+          vf[u][ss][0][p] = f16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          vf[u][ss][1][p] = f16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        }
+      }
+    asm volatile("" ::: "memory");
+    if constexpr (MASK) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (t0 + u * 32 + row32(r, half) >= Nk) sc[u][r] = -INFINITY;
+    }
+    float mt[11];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) mt[i] = max3f(sc[(3 * i) >> 4][(3 * i) & 15], sc[(3 * i + 1) >> 4][(3 * i + 1) & 15],
+                                               sc[(3 * i + 2) >> 4][(3 * i + 2) & 15]);
+    mt[10] = fmaxf(sc[1][14], sc[1][15]);
+    const float lmax = fmaxf(max3f(max3f(mt[0], mt[1], mt[2]), max3f(mt[3], mt[4], mt[5]), max3f(mt[6], mt[7], mt[8])),
+                             fmaxf(mt[9], mt[10]));
+    if (__ballot((lmax - m_use) * c_lane > 3.f) != 0ull) {
+      const float tmax = max_xor32(lmax);
+      const bool need = (tmax - m_use) * c_lane > 3.f;
+      const float m_new = need ? tmax : m_use;
+      const float alpha = __builtin_amdgcn_exp2f((m_use - m_new) * c_lane);
+      m_use = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o0[r] *= alpha;
+        o1[r] *= alpha;
+      }
+    }
+    // e = p 2^11
+    float ps8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (!EXACT) {
+      const float mb = fmaf(m_use, c_lane, -11.f);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c_lane, -mb));
+          sc[u][r] = e;
+          ps8[r & 7] += e;
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(sc[u][r] - m_use, c_lane, 11.f));
+          sc[u][r] = e;
+          ps8[r & 7] += e;
+        }
+    }
+    l_run += ((ps8[0] + ps8[1]) + (ps8[2] + ps8[3])) + ((ps8[4] + ps8[5]) + (ps8[6] + ps8[7]));
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        f16x8 ph, phs, pl;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const float e0 = sc[u][8 * ss + j], e1 = sc[u][8 * ss + j + 1];
+          const f16x2 hs = {(_Float16)e0, (_Float16)e1};
+          const f16x2 h = hs * (f16x2){(_Float16)(1.f / kLoScale), (_Float16)(1.f / kLoScale)};
+          const f16x2 lo = lo_pair(e0, e1, hs);
+          phs[j] = hs[0]; phs[j + 1] = hs[1];
+          ph[j] = h[0]; ph[j + 1] = h[1];
+          pl[j] = lo[0]; pl[j + 1] = lo[1];
+        }
+        o0 = mfma_h3(vf[u][ss][0][0], vf[u][ss][0][1], phs, pl, ph, o0);
+        o1 = mfma_h3(vf[u][ss][1][0], vf[u][ss][1][1], phs, pl, ph, o1);
+      }
+  };
+
+  using NoMask = std::integral_constant<bool, false>;
+  using Mask = std::integral_constant<bool, true>;
+  const int nlt = (Nk + LT - 1) / LT;
+  const int nfull = Nk / LT;
+  using IC0 = std::integral_constant<int, 0>;
+  using IC1 = std::integral_constant<int, KT * kHeadDim>;
+  using IC2 = std::integral_constant<int, 2 * PL>;
+  using IC3 = std::integral_constant<int, 2 * PL + KT * kHeadDim>;
+  static_assert(SUBS == 1 || SUBS == 2, "sub-tiles per LDS tile");
+  if (PRIO && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#define LG_ATTN_TILES(EXc)                                                          \
+  {                                                                                 \
+    int t = 0;                                                                      \
+    for (; t + 2 <= nfull; t += 2) {                                                \
+      if (t + 1 < nlt) issue((t + 1) * LT, 1);                                      \
+      body(IC0{}, NoMask{}, EXc, t * LT);                                           \
+      if constexpr (SUBS == 2) body(IC1{}, NoMask{}, EXc, t * LT + KT);             \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
+      __syncthreads();                                                              \
+      if (t + 2 < nlt) issue((t + 2) * LT, 0);                                      \
+      body(IC2{}, NoMask{}, EXc, (t + 1) * LT);                                     \
+      if constexpr (SUBS == 2) body(IC3{}, NoMask{}, EXc, (t + 1) * LT + KT);       \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
+      __syncthreads();                                                              \
+    }                                                                               \
+    for (; t < nlt; ++t) {                                                          \
+      const int buf = t & 1;                                                        \
+      if (t + 1 < nlt) issue((t + 1) * LT, buf ^ 1);                                \
+      for (int sub = 0; sub < SUBS; ++sub) {                                        \
+        const int s0_ = t * LT + sub * KT;                                          \
+        if (s0_ < Nk) body(buf * 2 * PL + sub * KT * kHeadDim, Mask{}, EXc, s0_);   \
+      }                                                                             \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
+      __syncthreads();                                                              \
+    }                                                                               \
+  }
+  if (exact) LG_ATTN_TILES((std::integral_constant<bool, true>{}))
+  else LG_ATTN_TILES((std::integral_constant<bool, false>{}))
+#undef LG_ATTN_TILES
+
+  // context row into the plane image: register r = 4g + e holds dim 8g + 4 half + e (+32 for o1);
+  // o = 2^11 sum(p v), l_run = 2^11 sum(p) -> ctx * 2^-E[v] (RangeOut, as h3g)
+  const float l_tot = sum_xor32(l_run);
+  const float inv = 1.f / l_tot;
+  const int q = q_blk + wave * 32 + l32;
+  if (q < Nq) {
+    const int orow = S.o_row0 + b * Nq + q;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          _Float16 a, c;
+          split2h((hf ? o1 : o0)[4 * g + e] * inv, a, c);
+          h[e] = a;
+          l[e] = c;
+        }
+        const size_t off = plane_off(orow, head * kHeadDim + hf * 32 + 8 * g + 4 * half, S.o_rows_pad);
+        *reinterpret_cast<f16x4*>(S.op + off) = h;
+        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+      }
+  }
+}
+
+template <int SUBS, int PRIO = 0, int WAVES = 8>
+static hipError_t attention_h3m_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+  constexpr int QB = 32 * WAVES;
+  const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
+  if (nq == 0 || B == 0) return hipSuccess;
+  if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
+  const int nqb = (nq + QB - 1) / QB;
+  const int items = nqb * B * H * 2;
+  hipLaunchKernelGGL((attention_h3m_kernel<SUBS, PRIO, WAVES>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
+                     scale * 1.4426950408889634f);
+  return hipGetLastError();
+}
+
+// fp16x3 kernel choice: LG_ATTN_KERNEL=h3g (16x16x32 MFMAs) | h3m (32x32x16 MFMAs, default)
+static bool attention_use_h3m() {
+  const char* e = getenv("LG_ATTN_KERNEL");
+  return !(e && !strcmp(e, "h3g"));
+}
+
 // Query block size: 8 waves (256 queries) per workgroup is the throughput shape; when that gives
 // fewer work items than CUs (B = 1, pruned sets) 4 waves per workgroup spread the queries over
 // twice the CUs (each workgroup still streams all keys).  LG_ATTN_WAVES=8|4|2 forces one.
@@ -664,6 +986,13 @@ hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, flo
   if (prec == PREC_H3) {
     if (!s0.op || !s1.op) return hipErrorInvalidValue;
     const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
+    if (attention_use_h3m()) {
+      switch (attention_waves(B, H, nq)) {
+        case 2: return attention_h3m_launch<2, 1, 2>(s0, s1, B, H, scale, st);
+        case 4: return attention_h3m_launch<2, 1, 4>(s0, s1, B, H, scale, st);
+        default: return attention_h3m_launch<2, 1, 8>(s0, s1, B, H, scale, st);
+      }
+    }
     switch (attention_waves(B, H, nq)) {
       case 2: return attention_h3g_launch<2, 1, 2>(s0, s1, B, H, scale, st);
       case 4: return attention_h3g_launch<2, 1, 4>(s0, s1, B, H, scale, st);

@@ -88,12 +88,16 @@ CASES = ["random_ragged", "increasing_scores", "decreasing_scores", "large_logit
          "one_key_in_last_tile"]
 
 
+@pytest.mark.parametrize("kernel", ["h3m", "h3g"])
 @pytest.mark.parametrize("precision,waves", [("auto", "8"), ("auto", "4"), ("auto", "2"), ("bf16x6", "8")])
 @pytest.mark.parametrize("name", CASES)
-def test_attention_matches_float64(name, precision, waves, monkeypatch):
-    # fp16x3 kernel under every query-block shape (LG_ATTN_WAVES: 256 / 128 / 64 queries per
-    # workgroup); the small shapes here would otherwise always pick 4
+def test_attention_matches_float64(name, precision, waves, kernel, monkeypatch):
+    # fp16x3 kernels (16x16x32 / 32x32x16 MFMAs) under every query-block shape (LG_ATTN_WAVES:
+    # 256 / 128 / 64 queries per workgroup); the small shapes here would otherwise always pick 4
+    if precision == "bf16x6" and kernel == "h3g":
+        pytest.skip("bf16x6 has one kernel")
     monkeypatch.setenv("LG_ATTN_WAVES", waves)
+    monkeypatch.setenv("LG_ATTN_KERNEL", kernel)
     q, k, v, scale = case(name)
     got = run_attention(q, k, v, scale, precision)
     ref = reference(q, k, v, scale)
@@ -112,12 +116,13 @@ def test_increasing_scores_really_rescale():
     assert (tile_max.diff(dim=-1) > 3 * np.log(2)).float().mean() > 0.9
 
 
-@pytest.mark.parametrize("precision", ["auto", "bf16x6"])
-def test_values_beyond_fp16_range_are_range_scaled(precision):
+@pytest.mark.parametrize("precision,kernel", [("auto", "h3m"), ("auto", "h3g"), ("bf16x6", "h3m")])
+def test_values_beyond_fp16_range_are_range_scaled(precision, kernel, monkeypatch):
     """Keys up to ~4e5 and values up to ~4e6 (far past fp16's 65504): the fp16x3 planes are
     written scaled by a device-chosen power of two (kernels.h RangeOut), the key exponent folds
     into the softmax scale and the value exponent into the output, so the result keeps the same
     relative accuracy as O(1) data -- no refusal, no host round trip."""
+    monkeypatch.setenv("LG_ATTN_KERNEL", kernel)
     q, k, v, scale = case("random_ragged")
     k, v, scale = k * 1.0e5, v * 1.0e6, scale / 1.0e5
     got = run_attention(q, k, v, scale, precision)

@@ -118,9 +118,10 @@ def test_forward_matches_reference_golden(name, precision):
     check_against_golden(pred, g, f"{name}/{precision}")
 
 
-@pytest.mark.parametrize("tile,waves,assign", [("big", "8", "fused"), ("small", "4", "fused"), ("small", "2", "unfused")])
+@pytest.mark.parametrize("tile,waves,assign,kernel", [("big", "8", "fused", "h3g"), ("small", "4", "fused", "h3m"),
+                                                       ("small", "2", "unfused", "h3g"), ("big", "2", "fused", "h3m")])
 @pytest.mark.parametrize("name", case_names())
-def test_forward_golden_all_launch_shapes(name, tile, waves, assign, monkeypatch):
+def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, monkeypatch):
     """The fp16x3 GEMM picks 256x256 tiles (throughput) or 64x64 tiles (fewer big tiles than CUs,
     e.g. B = 1) by row count, and the attention 8, 4 or 2 waves (256/128/64 queries) per
     workgroup, and the assignment its two-read fused passes (N % 4 == 0, N <= 2048) or the
@@ -128,6 +129,7 @@ def test_forward_golden_all_launch_shapes(name, tile, waves, assign, monkeypatch
     launch shape is checked against the reference on every golden case."""
     monkeypatch.setenv("LG_GEMM_TILE", tile)
     monkeypatch.setenv("LG_ATTN_WAVES", waves)
+    monkeypatch.setenv("LG_ATTN_KERNEL", kernel)  # fp16x3 attention: 16x16x32 (h3g) / 32x32x16 (h3m) MFMAs
     if assign == "unfused":  # the four-read assignment path (N % 4 != 0 or N > 2048)
         monkeypatch.setenv("LG_ASSIGN_UNFUSED", "1")
     g = load(name)
@@ -137,7 +139,7 @@ def test_forward_golden_all_launch_shapes(name, tile, waves, assign, monkeypatch
         pred = model(_gpu_data(data))
     torch.cuda.synchronize()
     assert model.last_precision_used == "fp16x3"
-    check_against_golden(pred, g, f"{name}/tile={tile},waves={waves},{assign}")
+    check_against_golden(pred, g, f"{name}/tile={tile},waves={waves},{assign},{kernel}")
 
 
 def test_weight_changes_after_first_forward_are_picked_up():

@@ -270,6 +270,8 @@ def run(args):
         model.profile_enable(False)
         prec = model.last_precision_used
         peak, kname, peak_note = PEAKS[prec]
+        if prec == "fp16x3" and os.environ.get("LG_ATTN_KERNEL") == "h3m":
+            kname = "lg::attention_h3m_kernel"
         traffic, traffic_src = measured_traffic(kname)
         roofline = {
             "kernel": f"{kname} (flash self/cross attention, {prec} fp32-accurate products)",

@@ -945,10 +945,13 @@ static hipError_t attention_h3m_launch(const AttnSet& s0, const AttnSet& s1, int
   return hipGetLastError();
 }
 
-// fp16x3 kernel choice: LG_ATTN_KERNEL=h3g (16x16x32 MFMAs) | h3m (32x32x16 MFMAs, default)
+// fp16x3 kernel choice: LG_ATTN_KERNEL=h3g (16x16x32 MFMAs, default) | h3m (32x32x16 MFMAs).
+// Measured equal at the bench shape (profiles/r02/pmc_ab: h3m takes 6 % fewer cycles per launch
+// but the chip holds a 7 % lower clock under it -- 1.84 vs 1.97 GHz, MFMA busy 0.54 vs 0.51), so
+// the saving returns as clock (MI355X_MICROARCH.md, DVFS give-back); h3g stays the default.
 static bool attention_use_h3m() {
   const char* e = getenv("LG_ATTN_KERNEL");
-  return !(e && !strcmp(e, "h3g"));
+  return e && !strcmp(e, "h3m");
 }
 
 // Query block size: 8 waves (256 queries) per workgroup is the throughput shape; when that gives

@@ -972,7 +972,7 @@ static hipError_t attention_h3s_launch(const AttnSet& s0, const AttnSet& s1, int
 }
 
 // ----------------------------------------------------------------------------------------
-// attention_h3m_kernel -- measured, superseded by attention_h3f_kernel (same MFMA data flow,
+// attention_h3m16_kernel -- measured, superseded by attention_h3f_kernel (same MFMA data flow,
 // leaner softmax).  fp16x3 attention on v_mfma_f32_16x16x32_f16: the schedule of attention_h3_kernel
 // (8 waves x 32 queries, 64-key tiles double-buffered in LDS, one barrier per tile, lazy softmax
 // reference, context straight into ffn.0's plane image) with 16 x 16 MFMA tiles, which the chip
@@ -998,7 +998,7 @@ __device__ __forceinline__ float sum_xor16_32(float v) {
 }
 
 template <int KT>
-__global__ __launch_bounds__(512, 2) void attention_h3m_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
+__global__ __launch_bounds__(512, 2) void attention_h3m16_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
                                                                 float scale_log2e) {
   constexpr int WAVES = 8, NT = 64 * WAVES, QB = 32 * WAVES;
   constexpr int NKT = KT / 16;             // 16-key tiles per tile
@@ -1242,14 +1242,14 @@ __global__ __launch_bounds__(512, 2) void attention_h3m_kernel(AttnSet s0, AttnS
 }
 
 template <int KT>
-static hipError_t attention_h3m_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+static hipError_t attention_h3m16_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
   constexpr int QB = 256;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
   if (nq == 0 || B == 0) return hipSuccess;
   if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
   const int nqb = (nq + QB - 1) / QB;
   const int items = nqb * B * H * 2;
-  hipLaunchKernelGGL((attention_h3m_kernel<KT>), dim3(items), dim3(512), 0, st, s0, s1, B, H, nqb,
+  hipLaunchKernelGGL((attention_h3m16_kernel<KT>), dim3(items), dim3(512), 0, st, s0, s1, B, H, nqb,
                      scale * 1.4426950408889634f);
   return hipGetLastError();
 }
@@ -1418,7 +1418,7 @@ __global__ __launch_bounds__(512, 2) void attention_h3f_kernel(AttnSet s0, AttnS
       const float m4 = max3f(sc[3][qt][0], sc[3][qt][1], sc[3][qt][2]);
       const float lmax = fmaxf(max3f(m0, m1, m2), max3f(m3, m4, sc[3][qt][3]));
       // the lane-local max decides whether any query can need a raise; only then are the four
-      // lanes of each query reduced (the raise itself is per query, exactly as in h3/h3m)
+      // lanes of each query reduced (the raise itself is per query, exactly as in h3/h3m16)
       if (__ballot((lmax - m_use[qt]) * c_lane[qt] > 3.f) != 0ull) {
         const float tmax = max_x16_32(lmax);
         const bool need = (tmax - m_use[qt]) * c_lane[qt] > 3.f;

@@ -130,11 +130,26 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&OP, (size_t)2 * rp * 256 * 2));
   AttnSet h0{Q, KH, VH, ps, O, N, N, OP, (long long)rp * 256, rp, 0};
   AttnSet h1{Q + n, (_Float16*)KH + n, (_Float16*)VH + n, ps, O + (size_t)B * N * 256, N, N, OP, (long long)rp * 256, rp, B * N};
+  // range table of the library kernels (kernels.h RangeOut): slot 0 = keys, max |k| = 2, E = 0
+  unsigned* rtab;
+  CK(hipMalloc(&rtab, 4 * kRangeStride * sizeof(unsigned)));
+  {
+    std::vector<unsigned> t(4 * kRangeStride, 0u);
+    const float two = 2.f;
+    memcpy(&t[0], &two, 4);
+    CK(hipMemcpy(rtab, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  }
+  AttnSet l0 = h0, l1 = h1;
+  l0.rtab = l1.rtab = rtab;
+  l0.k_slot = l1.k_slot = 0;
   const size_t on = (size_t)B * N * 256;  // compare set 0
+  run("lib h3m sub2 prio", [&] { return attention_h3m_launch<2, 1, 8>(l0, l1, B, H, scale, 0); }, B, H, l0, l1, Oref, O, on);
+  run("lib h3g sub2 prio", [&] { return attention_h3g_launch<2, 1, 8>(l0, l1, B, H, scale, 0); }, B, H, l0, l1, Oref, O, on);
+  run("lib h3m exact", [&] { return attention_h3m_launch<2, 1, 8>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("x6   w8 kt64", [&] { return attention_x6_launch<8, 64>(x0, x1, B, H, scale, 0); }, B, H, x0, x1, Oref, O, on);
   run("h3 w8 kt64 occ2", [&] { return attention_h3_launch<8, 64, 2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3s staggered", [&] { return attention_h3s_launch<64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
-  run("h3m 16x16x32", [&] { return attention_h3m_launch<64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
+  run("h3m 16x16x32", [&] { return attention_h3m16_launch<64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3f lean softmax", [&] { return attention_h3f_launch<64>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3g dma sub2", [&] { return attention_h3g_launch<2>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);
   run("h3g dma sub1", [&] { return attention_h3g_launch<1>(h0, h1, B, H, scale, 0); }, B, H, h0, h1, Oref, O, on);

@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LIGHTGLUE_MI355X_LIB", os.path.join(_HERE, "liblightglue_mi355x.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE = 0, -1, -2, -3, -4
 
@@ -90,6 +90,8 @@ class LGOutputs(ctypes.Structure):
         ("prune1", _P),
         ("layer_descriptors0", _P),
         ("layer_descriptors1", _P),
+        ("kept", _P),
+        ("stop", _P),
         ("stop_layer", ctypes.c_int32),
         ("kept0", ctypes.c_int32),
         ("kept1", ctypes.c_int32),

@@ -46,26 +46,31 @@ __device__ __forceinline__ float score_at(const float* src, const Stats& st, int
   }
 }
 
-__global__ __launch_bounds__(256) void row_stats_kernel(const float* sim, int rows, int N, float* rmax, float* rlog) {
+// Mb / Nb (nullable): per-pair kept counts of a pruned batch; M, N are then the layout capacities
+__global__ __launch_bounds__(256) void row_stats_kernel(const float* sim, int B, int M, int N, const int* Mb, const int* Nb,
+                                                        float* rmax, float* rlog) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
+  if (row >= B * M) return;
+  const int b = row / M;
+  if (Mb && row - b * M >= Mb[b]) return;
+  const int ne = Nb ? Nb[b] : N;
   const float* x = sim + (size_t)row * N;
   float m = -INFINITY, s = 0.f;
-  if ((N & 3) == 0) {  // 16-byte loads (the second pass re-reads the 8 KiB row from cache)
-    for (int j = 4 * lane; j < N; j += 256) {
+  if (((N | ne) & 3) == 0) {  // 16-byte loads (the second pass re-reads the 8 KiB row from cache)
+    for (int j = 4 * lane; j < ne; j += 256) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(x + j);
       m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
     }
     m = wave_max(m);
-    for (int j = 4 * lane; j < N; j += 256) {
+    for (int j = 4 * lane; j < ne; j += 256) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(x + j);
       s += (expf(v[0] - m) + expf(v[1] - m)) + (expf(v[2] - m) + expf(v[3] - m));
     }
   } else {
-    for (int j = lane; j < N; j += 64) m = fmaxf(m, x[j]);
+    for (int j = lane; j < ne; j += 64) m = fmaxf(m, x[j]);
     m = wave_max(m);
-    for (int j = lane; j < N; j += 64) s += expf(x[j] - m);
+    for (int j = lane; j < ne; j += 64) s += expf(x[j] - m);
   }
   s = wave_sum(s);
   if (lane == 0) { rmax[row] = m; rlog[row] = logf(s); }
@@ -73,13 +78,13 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const float* sim, int ro
 
 // Column statistics of one 64-row chunk in a single read: running (max, sum of exp(x - max))
 // per column, rescaled when the max rises (rare after the first rows).
-__global__ __launch_bounds__(256) void col_stats_partial_kernel(const float* sim, int M, int N, float* pmax,
-                                                                float* psum) {
+__global__ __launch_bounds__(256) void col_stats_partial_kernel(const float* sim, int M, int N, const int* Mb,
+                                                                const int* Nb, float* pmax, float* psum) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int ch = blockIdx.y, b = blockIdx.z;
   const int nch = gridDim.y;
-  if (j >= N) return;
-  const int i0 = ch * CCH, i1 = min(M, i0 + CCH);
+  if (j >= (Nb ? Nb[b] : N)) return;
+  const int i0 = ch * CCH, i1 = min(Mb ? Mb[b] : M, i0 + CCH);
   const float* x = sim + (size_t)b * M * N + j;
   float m = -INFINITY, acc = 0.f;
   for (int i = i0; i < i1; ++i) {
@@ -96,11 +101,12 @@ __global__ __launch_bounds__(256) void col_stats_partial_kernel(const float* sim
 }
 
 // combine the chunk partials in chunk order: cmax = max_c m_c, clog = log(sum_c s_c exp(m_c - cmax))
-__global__ void col_stats_combine_kernel(const float* pmax, const float* psum, int nch, int N, int BN, float* cmax,
-                                         float* clog) {
+__global__ void col_stats_combine_kernel(const float* pmax, const float* psum, int nch, int N, int BN, const int* Nb,
+                                         float* cmax, float* clog) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= BN) return;
   const int b = t / N, j = t - b * N;
+  if (Nb && j >= Nb[b]) return;
   const float* pm = pmax + (size_t)b * nch * N + j;
   const float* pv = psum + (size_t)b * nch * N + j;
   float m = -INFINITY;
@@ -119,15 +125,17 @@ __global__ void logsig_kernel(const float* z, float* ls, int n) {
 // One wave per row: la row write (optional) + row max / first argmax of the inner block.
 template <bool FROM_LA>
 __global__ __launch_bounds__(256) void row_pass_kernel(const float* src, Stats st, const float* z0, float* la, int B, int M,
-                                                       int N) {
+                                                       int N, const int* Mb, const int* Nb) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= B * M) return;
   const int b = row / M, i = row - b * M;
+  if (Mb && i >= Mb[b]) return;
+  const int ne = Nb ? Nb[b] : N;
   float best = -INFINITY;
   int bi = 0x7fffffff;
   float* lr = la ? la + ((size_t)b * (M + 1) + i) * (N + 1) : nullptr;
-  for (int j = lane; j < N; j += 64) {
+  for (int j = lane; j < ne; j += 64) {
     const float v = score_at<FROM_LA>(src, st, b, i, j, M, N);
     if (lr) lr[j] = v;
     if (bi == 0x7fffffff || v > best) { best = v; bi = j; }
@@ -142,23 +150,26 @@ __global__ __launch_bounds__(256) void row_pass_kernel(const float* src, Stats s
   if (lane == 0) {
     st.max0[row] = best;
     st.arg0[row] = bi;
-    if (lr) lr[N] = log_sigmoid(-z0[row]);
+    if (lr) lr[ne] = log_sigmoid(-z0[row]);
   }
 }
 
-__global__ void la_last_row_kernel(const float* z1, float* la, int B, int M, int N) {
+__global__ void la_last_row_kernel(const float* z1, float* la, int B, int M, int N, const int* Mb, const int* Nb) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * (N + 1)) return;
   const int b = t / (N + 1), j = t - b * (N + 1);
-  la[((size_t)b * (M + 1) + M) * (N + 1) + j] = j < N ? log_sigmoid(-z1[b * N + j]) : 0.f;
+  const int me = Mb ? Mb[b] : M, ne = Nb ? Nb[b] : N;
+  if (j > ne) return;
+  la[((size_t)b * (M + 1) + me) * (N + 1) + j] = j < ne ? log_sigmoid(-z1[b * N + j]) : 0.f;
 }
 
 template <bool FROM_LA>
-__global__ __launch_bounds__(256) void col_arg_partial_kernel(const float* src, Stats st, int M, int N) {
+__global__ __launch_bounds__(256) void col_arg_partial_kernel(const float* src, Stats st, int M, int N, const int* Mb,
+                                                              const int* Nb) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int ch = blockIdx.y, b = blockIdx.z, nch = gridDim.y;
-  if (j >= N) return;
-  const int i0 = ch * CCH, i1 = min(M, i0 + CCH);
+  if (j >= (Nb ? Nb[b] : N)) return;
+  const int i0 = ch * CCH, i1 = min(Mb ? Mb[b] : M, i0 + CCH);
   float best = -INFINITY;
   int bi = i0;
   for (int i = i0; i < i1; ++i) {
@@ -169,10 +180,11 @@ __global__ __launch_bounds__(256) void col_arg_partial_kernel(const float* src, 
   st.pi[((size_t)b * nch + ch) * N + j] = bi;
 }
 
-__global__ void col_arg_combine_kernel(Stats st, int nch, int N, int BN) {
+__global__ void col_arg_combine_kernel(Stats st, int nch, int N, int BN, const int* Nb) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= BN) return;
   const int b = t / N, j = t - b * N;
+  if (Nb && j >= Nb[b]) return;
   float best = st.pv[(size_t)b * nch * N + j];
   int bi = st.pi[(size_t)b * nch * N + j];
   for (int c = 1; c < nch; ++c) {
@@ -184,10 +196,12 @@ __global__ void col_arg_combine_kernel(Stats st, int nch, int N, int BN) {
 }
 
 // filter_matches: mutual check, exp(max0), threshold, -1 for invalid.
-__global__ void filter_kernel(Stats st, int B, int M, int N, float th, int64_t* m0, int64_t* m1, float* s0, float* s1) {
+__global__ void filter_kernel(Stats st, int B, int M, int N, float th, int64_t* m0, int64_t* m1, float* s0, float* s1,
+                              const int* Mb, const int* Nb) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < B * M) {
     const int b = t / M, i = t - b * M;
+    if (Mb && i >= Mb[b]) return;
     const int j = st.arg0[t];
     const bool mutual = st.arg1[b * N + j] == i;
     const float sc = mutual ? expf(st.max0[t]) : 0.f;
@@ -197,6 +211,7 @@ __global__ void filter_kernel(Stats st, int B, int M, int N, float th, int64_t* 
   } else if (t < B * M + B * N) {
     const int u = t - B * M;
     const int b = u / N, j = u - b * N;
+    if (Nb && j >= Nb[b]) return;
     const int i = st.arg1[u];
     const bool mutual = st.arg0[b * M + i] == j;  // then row i is mutual too
     const float sc = mutual ? expf(st.max0[b * M + i]) : 0.f;
@@ -465,12 +480,15 @@ size_t filter_workspace_floats(int B, int M, int N) { return assign_workspace_fl
 
 template <bool FROM_LA>
 static hipError_t argmax_and_filter(const float* src, const Stats& s, const float* z0, float* la, int B, int M, int N,
-                                    float th, int64_t* m0, int64_t* m1, float* s0, float* s1, hipStream_t st) {
+                                    float th, int64_t* m0, int64_t* m1, float* s0, float* s1, hipStream_t st,
+                                    const int* Mb = nullptr, const int* Nb = nullptr) {
   const int nch = (M + CCH - 1) / CCH;
-  hipLaunchKernelGGL((row_pass_kernel<FROM_LA>), dim3((B * M + 3) / 4), dim3(256), 0, st, src, s, z0, la, B, M, N);
-  hipLaunchKernelGGL((col_arg_partial_kernel<FROM_LA>), dim3((N + 255) / 256, nch, B), dim3(256), 0, st, src, s, M, N);
-  hipLaunchKernelGGL(col_arg_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s, nch, N, B * N);
-  hipLaunchKernelGGL(filter_kernel, dim3((B * (M + N) + 255) / 256), dim3(256), 0, st, s, B, M, N, th, m0, m1, s0, s1);
+  hipLaunchKernelGGL((row_pass_kernel<FROM_LA>), dim3((B * M + 3) / 4), dim3(256), 0, st, src, s, z0, la, B, M, N, Mb, Nb);
+  hipLaunchKernelGGL((col_arg_partial_kernel<FROM_LA>), dim3((N + 255) / 256, nch, B), dim3(256), 0, st, src, s, M, N, Mb,
+                     Nb);
+  hipLaunchKernelGGL(col_arg_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s, nch, N, B * N, Nb);
+  hipLaunchKernelGGL(filter_kernel, dim3((B * (M + N) + 255) / 256), dim3(256), 0, st, s, B, M, N, th, m0, m1, s0, s1, Mb,
+                     Nb);
   return hipGetLastError();
 }
 
@@ -480,7 +498,8 @@ hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st) {
   const Stats s = carve(a.ws, B, M, N);
   const int nch = (M + CCH - 1) / CCH;
   float* psum = reinterpret_cast<float*>(s.pi);  // the argmax index partials are not live yet
-  const bool fused = LG_ASSIGN_FUSED && N % 4 == 0 && N <= kAsMaxN && !getenv("LG_ASSIGN_UNFUSED");
+  // per-pair counts (pruned batches) take the four-read kernels, which bound every loop by them
+  const bool fused = LG_ASSIGN_FUSED && !a.Mb && N % 4 == 0 && N <= kAsMaxN && !getenv("LG_ASSIGN_UNFUSED");
   if (fused) {
     const int k4 = (N + 255) / 256;
     if (k4 <= 1) launch_assign_fused<1>(a, s, nch, psum, st);
@@ -488,27 +507,30 @@ hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st) {
     else if (k4 <= 4) launch_assign_fused<4>(a, s, nch, psum, st);
     else launch_assign_fused<8>(a, s, nch, psum, st);
   } else {
-    hipLaunchKernelGGL(row_stats_kernel, dim3((B * M + 3) / 4), dim3(256), 0, st, a.sim, B * M, N, s.rmax, s.rlog);
+    hipLaunchKernelGGL(row_stats_kernel, dim3((B * M + 3) / 4), dim3(256), 0, st, a.sim, B, M, N, a.Mb, a.Nb, s.rmax,
+                       s.rlog);
     const dim3 cg((N + 255) / 256, nch, B);
-    hipLaunchKernelGGL(col_stats_partial_kernel, cg, dim3(256), 0, st, a.sim, M, N, s.pv, psum);
+    hipLaunchKernelGGL(col_stats_partial_kernel, cg, dim3(256), 0, st, a.sim, M, N, a.Mb, a.Nb, s.pv, psum);
   }
   hipLaunchKernelGGL(col_stats_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s.pv, psum, nch, N, B * N,
-                     s.cmax, s.clog);
+                     a.Nb, s.cmax, s.clog);
   hipLaunchKernelGGL(logsig_kernel, dim3((B * M + 255) / 256), dim3(256), 0, st, a.z0, s.ls0, B * M);
   hipLaunchKernelGGL(logsig_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, a.z1, s.ls1, B * N);
-  if (a.la) hipLaunchKernelGGL(la_last_row_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, a.z1, a.la, B, M, N);
+  if (a.la)
+    hipLaunchKernelGGL(la_last_row_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, a.z1, a.la, B, M, N, a.Mb,
+                       a.Nb);
   if (fused) {
     const int k4 = (N + 255) / 256;
     if (k4 <= 1) launch_la_fused<1>(a, s, nch, st);
     else if (k4 <= 2) launch_la_fused<2>(a, s, nch, st);
     else if (k4 <= 4) launch_la_fused<4>(a, s, nch, st);
     else launch_la_fused<8>(a, s, nch, st);
-    hipLaunchKernelGGL(col_arg_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s, nch, N, B * N);
+    hipLaunchKernelGGL(col_arg_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s, nch, N, B * N, nullptr);
     hipLaunchKernelGGL(filter_kernel, dim3((B * (M + N) + 255) / 256), dim3(256), 0, st, s, B, M, N, a.th, a.m0, a.m1,
-                       a.s0, a.s1);
+                       a.s0, a.s1, nullptr, nullptr);
     return hipGetLastError();
   }
-  return argmax_and_filter<false>(a.sim, s, a.z0, a.la, B, M, N, a.th, a.m0, a.m1, a.s0, a.s1, st);
+  return argmax_and_filter<false>(a.sim, s, a.z0, a.la, B, M, N, a.th, a.m0, a.m1, a.s0, a.s1, st, a.Mb, a.Nb);
 }
 
 hipError_t filter_from_scores(const float* scores, int B, int M, int N, float th, float* ws, int64_t* m0, int64_t* m1,

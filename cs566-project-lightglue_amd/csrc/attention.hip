@@ -68,11 +68,14 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
   const int set = sbh / (B * H), bh = sbh - set * (B * H);
   const AttnSet& S = set == 0 ? s0 : s1;
   const int q_blk = qb * QB;
-  if (q_blk >= S.Nq) return;
-  const int Nq = S.Nq, Nk = S.Nk;
-  const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
-  const __bf16* Kp = static_cast<const __bf16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
-  const __bf16* Vp = static_cast<const __bf16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
+  // S.Nq / S.Nk are the layout capacities; per-pair counts (batched pruning) bound the loops
+  const int NqS = S.Nq, NkS = S.Nk, pb = bh / H;
+  if (S.act && !S.act[pb]) return;
+  const int Nq = S.nq_cnt ? S.nq_cnt[pb] : NqS, Nk = S.nk_cnt ? S.nk_cnt[pb] : NkS;
+  if (q_blk >= Nq || Nk <= 0) return;
+  const float* Q = S.q + (size_t)bh * NqS * kHeadDim;
+  const __bf16* Kp = static_cast<const __bf16*>(S.kp) + (size_t)bh * NkS * kHeadDim;
+  const __bf16* Vp = static_cast<const __bf16*>(S.vp) + (size_t)bh * NkS * kHeadDim;
   const long long ps = S.pstride;
   const int head = bh % H;
   const int b = bh / H;
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
   const float inv = 1.f / l_tot;
   const int q = q_blk + wave * 32 + l32;
   if (q < Nq) {
-    float* orow = S.o + ((size_t)b * Nq + q) * kDim + head * kHeadDim;
+    float* orow = S.o + ((size_t)b * NqS + q) * kDim + head * kHeadDim;
     // register r holds dim row32(r, half) (+32 for o1): r = 4g + e -> dim 8g + 4*half + e
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -335,11 +338,14 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   const int set = sbh / (B * H), bh = sbh - set * (B * H);
   const AttnSet& S = set == 0 ? s0 : s1;
   const int q_blk = qb * QB;
-  if (q_blk >= S.Nq) return;
-  const int Nq = S.Nq, Nk = S.Nk;
-  const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
-  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
-  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
+  // S.Nq / S.Nk are the layout capacities; per-pair counts (batched pruning) bound the loops
+  const int NqS = S.Nq, NkS = S.Nk, pb = bh / H;
+  if (S.act && !S.act[pb]) return;
+  const int Nq = S.nq_cnt ? S.nq_cnt[pb] : NqS, Nk = S.nk_cnt ? S.nk_cnt[pb] : NkS;
+  if (q_blk >= Nq || Nk <= 0) return;
+  const float* Q = S.q + (size_t)bh * NqS * kHeadDim;
+  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * NkS * kHeadDim;
+  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * NkS * kHeadDim;
   const long long ps = S.pstride;
   const int head = bh % H;
   const int b = bh / H;
@@ -598,7 +604,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
     const float inv = 1.f / l_tot;
     const int q = q_blk + wave * 32 + qt * 16 + r16;
     if (q < Nq) {
-      const int orow = S.o_row0 + b * Nq + q;
+      const int orow = S.o_row0 + b * NqS + q;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         f16x4 h, l;
@@ -668,11 +674,14 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
   const int set = sbh / (B * H), bh = sbh - set * (B * H);
   const AttnSet& S = set == 0 ? s0 : s1;
   const int q_blk = qb * QB;
-  if (q_blk >= S.Nq) return;
-  const int Nq = S.Nq, Nk = S.Nk;
-  const float* Q = S.q + (size_t)bh * Nq * kHeadDim;
-  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * Nk * kHeadDim;
-  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * Nk * kHeadDim;
+  // S.Nq / S.Nk are the layout capacities; per-pair counts (batched pruning) bound the loops
+  const int NqS = S.Nq, NkS = S.Nk, pb = bh / H;
+  if (S.act && !S.act[pb]) return;
+  const int Nq = S.nq_cnt ? S.nq_cnt[pb] : NqS, Nk = S.nk_cnt ? S.nk_cnt[pb] : NkS;
+  if (q_blk >= Nq || Nk <= 0) return;
+  const float* Q = S.q + (size_t)bh * NqS * kHeadDim;
+  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * NkS * kHeadDim;
+  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * NkS * kHeadDim;
   const long long ps = S.pstride;
   const int head = bh % H;
   const int b = bh / H;
@@ -912,7 +921,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
   const float inv = 1.f / l_tot;
   const int q = q_blk + wave * 32 + l32;
   if (q < Nq) {
-    const int orow = S.o_row0 + b * Nq + q;
+    const int orow = S.o_row0 + b * NqS + q;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll

@@ -152,10 +152,10 @@ hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows
 // and TokenConfidence.token (:99,104-106).  One wave per row.
 // ----------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void gemv256_kernel(const float* x, const float* w, const float* b, float* y, int rows,
-                                                      int sigmoid) {
+                                                      int sigmoid, RowMask rm) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
+  if (row >= rows || !row_live(rm, row)) return;
   const f32x4 xv = *reinterpret_cast<const f32x4*>(x + (size_t)row * kDim + lane * 4);
   const f32x4 wv = *reinterpret_cast<const f32x4*>(w + lane * 4);
   float s = xv[0] * wv[0] + xv[1] * wv[1] + xv[2] * wv[2] + xv[3] * wv[3];
@@ -169,7 +169,14 @@ __global__ __launch_bounds__(256) void gemv256_kernel(const float* x, const floa
 
 hipError_t gemv_256(const float* x, const float* w, const float* b, float* y, int rows, int sigmoid, hipStream_t st) {
   if (rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(gemv256_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, y, rows, sigmoid);
+  hipLaunchKernelGGL(gemv256_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, y, rows, sigmoid, RowMask{});
+  return hipGetLastError();
+}
+
+hipError_t gemv_256_masked(const float* x, const float* w, const float* b, float* y, int rows, const RowMask& m,
+                           hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(gemv256_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, y, rows, 0, m);
   return hipGetLastError();
 }
 
@@ -265,56 +272,96 @@ hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, i
 
 // ----------------------------------------------------------------------------------------
 // Point pruning (lightglue.py:532-547, get_pruning_mask :586-593) and early stop
-// (check_if_stop :595-606), batch 1.
+// (check_if_stop :595-606) for any batch size: fixed per-(image, pair) segments, device counts
+// (kernels.h SegLayout).
 // ----------------------------------------------------------------------------------------
-__global__ void prune_flags_kernel(const float* zmatch, const float* token, float width_thr, float conf_thr, int n,
-                                   int* flags) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float prob = 1.f / (1.f + expf(-zmatch[i]));  // sigmoid(matchability)
-  bool keep = prob > width_thr;
-  if (token) keep = keep || (token[i] <= conf_thr);
-  flags[i] = keep ? 1 : 0;
+__global__ void prune_init_kernel(SegLayout L, int* cnt, int* act, int* stop, int n_layers, int* ind) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int R = L.B * (L.M0 + L.N0);
+  if (t < R) {
+    int local;
+    (void)seg_of_row(L, t, local);
+    ind[t] = local;
+  }
+  if (t < 2 * L.B) cnt[t] = seg_len(L, t);
+  if (t < L.B) {
+    act[t] = 1;
+    stop[t] = n_layers - 1;
+  }
 }
 
-hipError_t prune_flags(const float* zmatch, const float* token, float width_thr, float conf_thr, int n, int* flags,
-                       hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(prune_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, st, zmatch, token, width_thr, conf_thr, n,
-                     flags);
+hipError_t prune_init(const SegLayout& L, int* cnt, int* act, int* stop, int n_layers, int* ind, hipStream_t st) {
+  const int R = L.B * (L.M0 + L.N0);
+  hipLaunchKernelGGL(prune_init_kernel, dim3((R + 255) / 256), dim3(256), 0, st, L, cnt, act, stop, n_layers, ind);
   return hipGetLastError();
 }
 
-__global__ void count_below_kernel(const float* token, float thr, int n, int* counter) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool below = i < n && token[i] < thr;
-  const unsigned long long m = __ballot(below);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, (int)__popcll(m));
+// one workgroup per pair
+__global__ __launch_bounds__(256) void stop_decide_kernel(const float* token, const int* cnt, int* act, int* stop,
+                                                          SegLayout L, float thr, float depth_conf, int layer) {
+  __shared__ int red[4];
+  const int b = blockIdx.x;
+  if (!act[b]) return;
+  int below = 0;
+  for (int sgi = 0; sgi < 2; ++sgi) {
+    const int s = sgi == 0 ? b : L.B + b;
+    const int base = seg_base(L, s), n = cnt[s];
+    for (int i = threadIdx.x; i < n; i += 256) below += token[base + i] < thr ? 1 : 0;
+  }
+  for (int o = 32; o >= 1; o >>= 1) below += __shfl_xor(below, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = below;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int c = red[0] + red[1] + red[2] + red[3];
+    // 1.0 - (confidences < threshold).float().sum() / num_points, num_points = m + n (:602-605)
+    const float ratio = 1.0f - (float)c / (float)(L.M0 + L.N0);
+    if (ratio > depth_conf) {
+      act[b] = 0;
+      stop[b] = layer;
+    }
+  }
 }
 
-hipError_t count_below(const float* token, float thr, int n, int* counter, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(count_below_kernel, dim3((n + 255) / 256), dim3(256), 0, st, token, thr, n, counter);
+hipError_t stop_decide(const float* token, const int* cnt, int* act, int* stop, const SegLayout& L, float thr,
+                       float depth_conf, int layer, hipStream_t st) {
+  hipLaunchKernelGGL(stop_decide_kernel, dim3(L.B), dim3(256), 0, st, token, cnt, act, stop, L, thr, depth_conf, layer);
   return hipGetLastError();
 }
 
-// Exclusive scan of 0/1 flags in one workgroup (n is a keypoint count, <= a few 10^4).
-__global__ __launch_bounds__(1024) void compact_scan_kernel(const int* flags, int n, int* pos, int* count) {
+// one workgroup per segment: keep flags and their exclusive scan (chunks of 1024 with a carry)
+__global__ __launch_bounds__(1024) void prune_scan_kernel(const float* zmatch, const float* token, const int* cnt_in,
+                                                          int* cnt_out, const int* act, int* flags, int* pos, SegLayout L,
+                                                          float width_thr, float conf_thr) {
   __shared__ int wsum[16];
   __shared__ int carry;
+  const int s = blockIdx.x;
+  const int pair = s < L.B ? s : s - L.B;
+  const int base = seg_base(L, s), n = cnt_in[s];
+  const bool running = act[pair] != 0;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int base = 0; base < n; base += 1024) {
-    const int i = base + threadIdx.x;
-    const int f = i < n ? flags[i] : 0;
-    const unsigned long long m = __ballot(f != 0);
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    const int i = c0 + threadIdx.x;
+    bool keep = false;
+    if (i < n) {
+      keep = true;
+      if (running) {
+        const float prob = 1.f / (1.f + expf(-zmatch[base + i]));  // sigmoid(matchability)
+        keep = prob > width_thr;
+        if (token) keep = keep || (token[base + i] <= conf_thr);  // low confidence: never pruned
+      }
+    }
+    const unsigned long long m = __ballot(keep);
     const int before = __popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0) wsum[wave] = __popcll(m);
     __syncthreads();
     int off = carry;
     for (int w = 0; w < wave; ++w) off += wsum[w];
-    if (i < n) pos[i] = off + before;
+    if (i < n) {
+      flags[base + i] = keep ? 1 : 0;
+      pos[base + i] = off + before;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       int t = 0;
@@ -323,52 +370,62 @@ __global__ __launch_bounds__(1024) void compact_scan_kernel(const int* flags, in
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *count = carry;
+  if (threadIdx.x == 0) cnt_out[s] = carry;
 }
 
-hipError_t compact_scan(const int* flags, int n, int* pos, int* count, hipStream_t st) {
-  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, st, flags, n, pos, count);
+hipError_t prune_scan(const float* zmatch, const float* token, const int* cnt_in, int* cnt_out, const int* act,
+                      int* flags, int* pos, const SegLayout& L, float width_thr, float conf_thr, hipStream_t st) {
+  hipLaunchKernelGGL(prune_scan_kernel, dim3(2 * L.B), dim3(1024), 0, st, zmatch, token, cnt_in, cnt_out, act, flags, pos,
+                     L, width_thr, conf_thr);
   return hipGetLastError();
 }
 
-__global__ void compact_rows_kernel(const float* src, float* dst, const int* flags, const int* pos, int n, int cols) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (size_t)n * cols) return;
-  const int r = (int)(i / cols), c = (int)(i % cols);
-  if (flags[r]) dst[(size_t)pos[r] * cols + c] = src[i];
+// four floats per thread (cols % 4 == 0)
+__global__ void compact_seg_kernel(const float* src, float* dst, int cols, const int* flags, const int* pos,
+                                   const int* cnt_in, SegLayout L) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = cols / 4;
+  const int r = (int)(t / q), c = (int)(t % q) * 4;
+  if (r >= L.B * (L.M0 + L.N0)) return;
+  int local;
+  const int s = seg_of_row(L, r, local);
+  if (local >= cnt_in[s] || !flags[r]) return;
+  const int to = seg_base(L, s) + pos[r];
+  *reinterpret_cast<f32x4*>(dst + (size_t)to * cols + c) = *reinterpret_cast<const f32x4*>(src + (size_t)r * cols + c);
 }
 
-hipError_t compact_rows(const float* src, float* dst, const int* flags, const int* pos, int n, int cols, hipStream_t st) {
-  const size_t t = (size_t)n * cols;
-  if (t == 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_rows_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, src, dst, flags, pos, n,
-                     cols);
-  return hipGetLastError();
-}
-
-__global__ void compact_index_kernel(const int* ind, int* ind_out, int64_t* prune, const int* flags, const int* pos,
-                                     int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !flags[i]) return;
-  const int orig = ind[i];
-  ind_out[pos[i]] = orig;
-  prune[orig] += 1;  // prune0[:, ind0] += 1 after the selection (lightglue.py:540)
-}
-
-hipError_t compact_index(const int* ind, int* ind_out, int64_t* prune, const int* flags, const int* pos, int n,
-                         hipStream_t st) {
+hipError_t compact_seg(const float* src, float* dst, int cols, const int* flags, const int* pos, const int* cnt_in,
+                       const SegLayout& L, hipStream_t st) {
+  if (cols % 4) return hipErrorInvalidValue;
+  const size_t n = (size_t)L.B * (L.M0 + L.N0) * (cols / 4);
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_index_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ind, ind_out, prune, flags, pos, n);
+  hipLaunchKernelGGL(compact_seg_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, dst, cols, flags, pos,
+                     cnt_in, L);
   return hipGetLastError();
 }
 
-__global__ void iota_kernel(int* p, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = i;
+__global__ void compact_ind_seg_kernel(const int* ind, int* ind_out, int64_t* prune0, int64_t* prune1, const int* flags,
+                                       const int* pos, const int* cnt_in, const int* act, SegLayout L) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= L.B * (L.M0 + L.N0)) return;
+  int local;
+  const int s = seg_of_row(L, r, local);
+  if (local >= cnt_in[s] || !flags[r]) return;
+  const int base = seg_base(L, s), orig = ind[r];
+  ind_out[base + pos[r]] = orig;
+  const int pair = s < L.B ? s : s - L.B;
+  if (act[pair]) {  // prune0[:, ind0] += 1 after the selection (lightglue.py:540,546)
+    int64_t* pr = s < L.B ? prune0 + (size_t)pair * L.M0 : prune1 + (size_t)pair * L.N0;
+    if (pr) pr[orig] += 1;
+  }
 }
-hipError_t iota_fill(int* ind, int n, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ind, n);
+
+hipError_t compact_ind_seg(const int* ind, int* ind_out, int64_t* prune0, int64_t* prune1, const int* flags,
+                           const int* pos, const int* cnt_in, const int* act, const SegLayout& L, hipStream_t st) {
+  const int R = L.B * (L.M0 + L.N0);
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(compact_ind_seg_kernel, dim3((R + 255) / 256), dim3(256), 0, st, ind, ind_out, prune0, prune1, flags,
+                     pos, cnt_in, act, L);
   return hipGetLastError();
 }
 
@@ -382,34 +439,48 @@ hipError_t fill_i64(int64_t* p, int64_t v, size_t n, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Scatter compact matches back to full size (lightglue.py:553-562).
-__global__ void remap_kernel(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind0,
-                             const int* ind1, int kept0, int kept1, int64_t* m0, int64_t* m1, float* s0, float* s1) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < kept0) {
-    const int64_t j = m0c[i];
-    m0[ind0[i]] = j == -1 ? -1 : (int64_t)ind1[j];
-    s0[ind0[i]] = s0c[i];
-  } else if (i < kept0 + kept1) {
-    const int k = i - kept0;
-    const int64_t j = m1c[k];
-    m1[ind1[k]] = j == -1 ? -1 : (int64_t)ind0[j];
-    s1[ind1[k]] = s1c[k];
+// Scatter compact matches back to full size (lightglue.py:553-562): one thread per output slot
+// of the full [B][M0] / [B][N0] arrays is initialised (-1 / 0) by remap_init; then one thread per
+// kept point writes its match through the index arrays
+__global__ void remap_init_kernel(int64_t* m0, int64_t* m1, float* s0, float* s1, SegLayout L) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < L.B * L.M0) {
+    m0[t] = -1;
+    s0[t] = 0.f;
+  } else if (t < L.B * (L.M0 + L.N0)) {
+    m1[t - L.B * L.M0] = -1;
+    s1[t - L.B * L.M0] = 0.f;
+  }
+}
+__global__ void remap_seg_kernel(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind,
+                                 const int* cnt, SegLayout L, int64_t* m0, int64_t* m1, float* s0, float* s1) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= L.B * (L.M0 + L.N0)) return;
+  int local;
+  const int s = seg_of_row(L, r, local);
+  if (local >= cnt[s]) return;
+  if (s < L.B) {  // image 0, pair s: compact match -> image-1 original index
+    const int b = s;
+    const int64_t j = m0c[(size_t)b * L.M0 + local];
+    const int* ind1 = ind + seg_base(L, L.B + b);
+    m0[(size_t)b * L.M0 + ind[r]] = j == -1 ? -1 : (int64_t)ind1[j];
+    s0[(size_t)b * L.M0 + ind[r]] = s0c[(size_t)b * L.M0 + local];
+  } else {
+    const int b = s - L.B;
+    const int64_t j = m1c[(size_t)b * L.N0 + local];
+    const int* ind0 = ind + seg_base(L, b);
+    m1[(size_t)b * L.N0 + ind[r]] = j == -1 ? -1 : (int64_t)ind0[j];
+    s1[(size_t)b * L.N0 + ind[r]] = s1c[(size_t)b * L.N0 + local];
   }
 }
 
-hipError_t remap_matches(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind0,
-                         const int* ind1, int kept0, int kept1, int64_t* m0, int64_t* m1, float* s0, float* s1, int M,
-                         int N, hipStream_t st) {
-  hipError_t e;
-  if ((e = fill_i64(m0, -1, M, st)) != hipSuccess) return e;
-  if ((e = fill_i64(m1, -1, N, st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(s0, 0, sizeof(float) * M, st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(s1, 0, sizeof(float) * N, st)) != hipSuccess) return e;
-  const int n = kept0 + kept1;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(remap_kernel, dim3((n + 255) / 256), dim3(256), 0, st, m0c, m1c, s0c, s1c, ind0, ind1, kept0, kept1,
-                     m0, m1, s0, s1);
+hipError_t remap_seg(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind,
+                     const int* cnt, const SegLayout& L, int64_t* m0, int64_t* m1, float* s0, float* s1, hipStream_t st) {
+  const int R = L.B * (L.M0 + L.N0);
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(remap_init_kernel, dim3((R + 255) / 256), dim3(256), 0, st, m0, m1, s0, s1, L);
+  hipLaunchKernelGGL(remap_seg_kernel, dim3((R + 255) / 256), dim3(256), 0, st, m0c, m1c, s0c, s1c, ind, cnt, L, m0, m1,
+                     s0, s1);
   return hipGetLastError();
 }
 

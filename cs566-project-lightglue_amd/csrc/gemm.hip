@@ -230,7 +230,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm0 + i * 32 + row32(r, half);
-          if (row >= args.R) continue;
+          if (row >= args.R || (args.rm.cnt && !row_live(args.rm, row))) continue;
           float v = (acc[i][j][r] + bj) * args.out_scale;
           if (args.res) v = args.res[(size_t)row * args.ldr + col] + v;
           Y[(size_t)row * args.ldy + col] = v;
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(GemmAr
       for (int r = 0; r < 16; ++r) {
         const int lr = wm0 + i * 32 + row32(r, half);
         const int row = m0 + lr;
-        if (row >= args.R) continue;
+        if (row >= args.R || (args.rm.cnt && !row_live(args.rm, row))) continue;
         const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + 2 * l32;
         float xe = acc[i][0][r] + be;  // dim 2*l32   (even)
         float xo = acc[i][1][r] + bo;  // dim 2*l32+1 (odd)

@@ -111,6 +111,16 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   const int tm = tile / num_n, tn = tile - tm * num_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = g.K / BK, nk0 = g.K0 / BK;
+  if (g.rm.cnt) {  // batched pruning: a tile without a live row does nothing (flag in the idle LDS)
+    volatile int* fl = reinterpret_cast<volatile int*>(smem);
+    if (threadIdx.x == 0) *fl = 0;
+    __syncthreads();
+    if (threadIdx.x < BM && m0 + (int)threadIdx.x < g.R && row_live(g.rm, m0 + threadIdx.x)) *fl = 1;
+    __syncthreads();
+    const bool any = *fl != 0;
+    __syncthreads();  // read before the first LDS-DMA stage lands on it
+    if (!any) return;
+  }
 
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)smem);
 
@@ -353,7 +363,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
           const int sw = (rr & 1) << 2;
           const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
-          if (row < g.R) {
+          if (row < g.R && row_live(g.rm, row)) {
             f16x8 h, l;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -404,7 +414,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         const int sw = (rr & 1) << 2;
         f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
         f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
-        if (row < g.R) {
+        if (row < g.R && row_live(g.rm, row)) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             v0[e] = fmaf(v0[e], accs, b0[e]) * g.out_scale;
@@ -491,7 +501,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         const int sw = (rr & 1) << 2;
         const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (d0 ^ sw));
         const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((d0 + 4) ^ sw));
-        if (row >= g.R) continue;
+        if (row >= g.R || !row_live(g.rm, row)) continue;
         float x[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) x[e] = fmaf(e < 4 ? v0[e] : v1[e - 4], accs, bd[e]);
@@ -609,13 +619,14 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
 // (xc != nullptr: the fp32 rows are also copied to xc, row stride K -- the residual stream's
 // initial value taken in the same read)
 __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
-                                      RangeOut ro, float* xc) {
+                                      RangeOut ro, float* xc, RowMask rm) {
   const int nch = K / 8;
   const int eo = range_exponent(ro);
   const float so = ldexpf(1.f, -eo);
   float wmax = 0.f;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)R * nch; i += (size_t)gridDim.x * blockDim.x) {
     const int r = (int)(i / nch), c = (int)(i % nch);
+    if (!row_live(rm, row0 + r)) continue;  // dead rows of a pruned batch: stale data, not tracked
     const float* p = x + (size_t)r * ld + c * 8;
     const f32x4 v0 = *reinterpret_cast<const f32x4*>(p), v1 = *reinterpret_cast<const f32x4*>(p + 4);
     if (xc) {
@@ -641,12 +652,12 @@ __global__ void rows_to_planes_kernel(const float* x, int R, int K, int ld, _Flo
 }
 
 hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
-                          const RangeOut& ro, hipStream_t st, float* xcopy) {
+                          const RangeOut& ro, hipStream_t st, float* xcopy, const RowMask* rm) {
   if (R <= 0) return hipSuccess;
   if (K % kKB || rows_pad < row0 + R) return hipErrorInvalidValue;
   const size_t n = (size_t)R * (K / 8);
   hipLaunchKernelGGL(rows_to_planes_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 2048)), dim3(256), 0, st, x, R, K, ld, planes,
-                     rows_pad, row0, ro, xcopy);
+                     rows_pad, row0, ro, xcopy, rm ? *rm : RowMask{});
   return hipGetLastError();
 }
 

@@ -20,6 +20,41 @@ enum EpiKind {
 //   PREC_X6  bf16x6 -- 6 bf16 MFMAs per product; full fp32 range
 enum Prec { PREC_H3 = 0, PREC_X6 = 1 };
 
+// ---- Point pruning and early stop for any batch size (lightglue.py:527-562,586-606) --------
+// The row space keeps a fixed slot per (image, pair): segment s < B is image 0 of pair s (rows
+// s*M0 ..), segment s >= B is image 1 of pair s-B (rows B*M0 + (s-B)*N0 ..).  A segment's kept
+// points are a prefix of its slot (cnt[s] of them), compacted in place layer by layer; a pair that
+// stopped early is frozen (act[pair] = 0).  Every count lives on the device: no host sync.
+struct SegLayout {
+  int B, M0, N0;
+};
+__host__ __device__ inline int seg_base(const SegLayout& L, int s) { return s < L.B ? s * L.M0 : L.B * L.M0 + (s - L.B) * L.N0; }
+__host__ __device__ inline int seg_len(const SegLayout& L, int s) { return s < L.B ? L.M0 : L.N0; }
+__host__ __device__ inline int seg_of_row(const SegLayout& L, int r, int& local) {
+  if (r < L.B * L.M0) {
+    const int s = r / L.M0;
+    local = r - s * L.M0;
+    return s;
+  }
+  const int r2 = r - L.B * L.M0, p = r2 / L.N0;
+  local = r2 - p * L.N0;
+  return L.B + p;
+}
+// Which rows of a GEMM are live: local < cnt[segment] and (sel == null or sel[pair] == sel_eq).
+// cnt == null: every row.  Dead rows are neither stored nor tracked; a tile of dead rows exits.
+struct RowMask {
+  const int* cnt;
+  const int* sel;
+  int sel_eq;
+  SegLayout L;
+};
+__host__ __device__ inline bool row_live(const RowMask& m, int r) {
+  if (!m.cnt) return true;
+  int local;
+  const int s = seg_of_row(m.L, r, local);
+  if (local >= m.cnt[s]) return false;
+  return !m.sel || m.sel[s < m.L.B ? s : s - m.L.B] == m.sel_eq;
+}
 // Run-time range scaling of fp16x3 plane images.  A forward keeps a small table
 // in its workspace, zeroed at the start; slot s holds (common.h: sharded layout)
 //   M[s]: max |x| over the values written (float bits; atomicMax of non-negative floats), kept
@@ -74,6 +109,7 @@ struct GemmArgs {
   int R, Nout;
   long long sA, sA1, sW, sY;  // per-blockIdx.z strides (floats)
   HeadLayout hl;
+  RowMask rm;                 // live rows (batched pruning; cnt == null: all)
 };
 
 // bf16x6 GEMM on fp32 operands (gemm.hip): the PREC_X6 linears and the similarity GEMM.
@@ -106,6 +142,7 @@ struct GemmH3Args {
   int a0_slot, a1_slot;  // their slots (-1: exponent 0)
   RangeOut ro;        // Yp / EPI_LN_GELU planes (EPI_QKV_*: the key planes)
   RangeOut ro_v;      // EPI_QKV_*: the value planes
+  RowMask rm;         // live rows (batched pruning; cnt == null: all)
   const float* ln_g;  // EPI_LN_GELU: LayerNorm weight / bias [Nout]
   const float* ln_b;
   HeadLayout hl;      // EPI_QKV_ROT / EPI_CROSS_QKV
@@ -114,7 +151,7 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st);
 // fp32 rows [R][K] (row stride ld) -> rows row0 .. row0+R-1 of a plane image (rows_pad), with
 // the fp16-range guard; xcopy (optional) also receives the fp32 rows, row stride K
 hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
-                          const RangeOut& ro, hipStream_t st, float* xcopy = nullptr);
+                          const RangeOut& ro, hipStream_t st, float* xcopy = nullptr, const RowMask* rm = nullptr);
 // max |x| over n floats, atomicMax'ed into slot `slot` of a range table (M only)
 hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipStream_t st);
 
@@ -135,6 +172,11 @@ struct AttnSet {
   // ctx * 2^-E[v_slot] and their consumer reads v_slot.  Null rtab: exponents 0.
   const unsigned* rtab;
   int k_slot;
+  // batched pruning (nullable): per-pair query / key counts (Nq, Nk above are then the layout
+  // capacities) and the pairs still running (0 = stopped early: nothing computed or written)
+  const int* nq_cnt;
+  const int* nk_cnt;
+  const int* act;
 };
 hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st);
 
@@ -169,9 +211,11 @@ struct AssignArgs {
   const float* z1;   // [B*N]
   float* la;         // [B][M+1][N+1] or null
   float* ws;         // scratch
-  int B, M, N;
+  int B, M, N;       // M, N: the layout capacities when Mb / Nb are given
   float th;
   int64_t* m0; int64_t* m1; float* s0; float* s1;
+  const int* Mb;      // per-pair kept counts (batched pruning; null: M, N for every pair); la
+  const int* Nb;      // then holds pair b's [Mb+1][Nb+1] block with the capacity strides
 };
 size_t assign_workspace_floats(int B, int M, int N);
 hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st);
@@ -203,19 +247,31 @@ hipError_t layernorm_bound(const float* g, const float* b, int n, float* out, hi
 // Weight repacking: dst[r,:] = src[idx[r],:] (row length `cols`).
 hipError_t gather_rows(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st);
 
-// Pruning support (B == 1).
-hipError_t prune_flags(const float* zmatch, const float* token, float width_thr, float conf_thr, int n, int* flags,
-                       hipStream_t st);
-hipError_t count_below(const float* token, float thr, int n, int* counter, hipStream_t st);
-hipError_t compact_scan(const int* flags, int n, int* pos, int* count, hipStream_t st);
-hipError_t compact_rows(const float* src, float* dst, const int* flags, const int* pos, int n, int cols, hipStream_t st);
-hipError_t compact_index(const int* ind, int* ind_out, int64_t* prune, const int* flags, const int* pos, int n,
-                         hipStream_t st);
-hipError_t iota_fill(int* ind, int n, hipStream_t st);
+// ---- Point pruning and early stop for any batch size: layout and masks above (RowMask) -----
+// initial state: cnt = slot sizes, act = 1, stop = L-1, ind = 0, 1, 2, .. per segment
+hipError_t prune_init(const SegLayout& L, int* cnt, int* act, int* stop, int n_layers, int* ind, hipStream_t st);
+// early stop (check_if_stop :595-606, thresholds :581-584): per running pair, ratio =
+// 1 - #(token < thr over its kept points) / (M0 + N0); ratio > depth_conf stops it at `layer`
+hipError_t stop_decide(const float* token, const int* cnt, int* act, int* stop, const SegLayout& L, float thr,
+                       float depth_conf, int layer, hipStream_t st);
+// keep flags + in-segment exclusive scan (get_pruning_mask :586-593): running pairs keep
+// sigmoid(z) > width_thr or (token && token <= conf_thr); frozen pairs keep every point
+hipError_t prune_scan(const float* zmatch, const float* token, const int* cnt_in, int* cnt_out, const int* act,
+                      int* flags, int* pos, const SegLayout& L, float width_thr, float conf_thr, hipStream_t st);
+// move kept rows (cols floats each) to their compacted position of the same segment
+hipError_t compact_seg(const float* src, float* dst, int cols, const int* flags, const int* pos, const int* cnt_in,
+                       const SegLayout& L, hipStream_t st);
+// compacted original indices; prune[ind] += 1 for the kept points of running pairs (:540,546)
+hipError_t compact_ind_seg(const int* ind, int* ind_out, int64_t* prune0, int64_t* prune1, const int* flags,
+                           const int* pos, const int* cnt_in, const int* act, const SegLayout& L, hipStream_t st);
 hipError_t fill_i64(int64_t* p, int64_t v, size_t n, hipStream_t st);
-hipError_t remap_matches(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind0,
-                         const int* ind1, int kept0, int kept1, int64_t* m0, int64_t* m1, float* s0, float* s1, int M,
-                         int N, hipStream_t st);
+// scatter the per-pair compact matches back to full size (lightglue.py:553-562); m0c.. have the
+// capacity strides (M0 per pair), the outputs are [B][M0] / [B][N0]
+hipError_t remap_seg(const int64_t* m0c, const int64_t* m1c, const float* s0c, const float* s1c, const int* ind,
+                     const int* cnt, const SegLayout& L, int64_t* m0, int64_t* m1, float* s0, float* s1, hipStream_t st);
+// y[r] = dot(x[r], w) + b for the live rows of a mask (the per-pair assignment heads)
+hipError_t gemv_256_masked(const float* x, const float* w, const float* b, float* y, int rows, const RowMask& m,
+                           hipStream_t st);
 
 // Sinkhorn (superglue.py:173-201).
 size_t sinkhorn_workspace_floats(int B, int M, int N);

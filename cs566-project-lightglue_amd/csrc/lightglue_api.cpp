@@ -299,7 +299,7 @@ struct Work {
   float* Dst;
   int rows_pad;
   size_t R;
-  int *flags, *pos, *ind0, *ind1, *ind0b, *ind1b, *counts;
+  int *flags, *pos, *ind, *indb, *cnt, *cntb, *act, *stop;  // pruning / early stop (SegLayout)
   unsigned* rtab;  // PREC_H3 range table (kernels.h RangeOut), kRangeSlots slots
   int64_t *m0c, *m1c;
   float *s0c, *s1c;
@@ -349,15 +349,16 @@ Work carve(char* base, int B, int M, int N, bool prune, int din) {
     w.sin2 = tf(R * 32);
     w.flags = ti(R);
     w.pos = ti(R);
-    w.ind0 = ti(M);
-    w.ind1 = ti(N);
-    w.ind0b = ti(M);
-    w.ind1b = ti(N);
-    w.counts = ti(64);
-    w.m0c = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * M));
-    w.m1c = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * N));
-    w.s0c = tf(M);
-    w.s1c = tf(N);
+    w.ind = ti(R);
+    w.indb = ti(R);
+    w.cnt = ti(2 * (size_t)B);
+    w.cntb = ti(2 * (size_t)B);
+    w.act = ti(B);
+    w.stop = ti(B);
+    w.m0c = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * B * M));
+    w.m1c = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * B * N));
+    w.s0c = tf((size_t)B * M);
+    w.s1c = tf((size_t)B * N);
   }
   w.bytes = off;
   return w;
@@ -604,7 +605,6 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   // training-mode gating (lightglue.py:502-503): no early stop, no pruning
   const bool gated = (in->flags & LG_FWD_TRAINING_GATE) != 0;
   const bool do_stop = !gated && c.depth_confidence > 0.f, do_prune = !gated && c.width_confidence > 0.f;
-  if ((do_stop || do_prune) && B != 1) return fail(LG_E_INVALID, "pruning / early stop require batch size 1");
   if ((out->layer_descriptors0 || out->layer_descriptors1) && (do_stop || do_prune))
     return fail(LG_E_INVALID, "layer_descriptors need early stop and pruning off (training-mode outputs)");
   if (do_prune && (!out->prune0 || !out->prune1)) return fail(LG_E_INVALID, "prune0/prune1 outputs required with pruning");
@@ -737,18 +737,27 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     LG_HIP(positional_encoding(p, st));
   }
 
-  if (do_prune) {
-    LG_HIP(iota_fill(w.ind0, M, st));
-    LG_HIP(iota_fill(w.ind1, N, st));
+  // ---- early stop / point pruning for any batch size, counts on the device (kernels.h
+  // SegLayout): each (image, pair) keeps a fixed slot whose kept points are a compacted prefix;
+  // GEMMs skip dead rows, the attention reads per-pair counts, a stopped pair is frozen
+  const bool seg = do_stop || do_prune;
+  const SegLayout SL{B, M0, N0};
+  int* cnt = w.cnt;
+  int* cntb = w.cntb;
+  int* ind = w.ind;
+  int* indb = w.indb;
+  RowMask live{};  // cnt == null outside pruning: every row live
+  if (seg) {
+    LG_HIP(prune_init(SL, cnt, w.act, w.stop, L, ind, st));
+    live = RowMask{cnt, w.act, 1, SL};
   }
   if (out->prune0) LG_HIP(fill_i64(out->prune0, do_prune ? 1 : L, (size_t)B * M0, st));
   if (out->prune1) LG_HIP(fill_i64(out->prune1, do_prune ? 1 : L, (size_t)B * N0, st));
 
   const float thr_w = (float)(1.0 - c.width_confidence);  // python-float arithmetic, then fp32 compare
-  int stop = L - 1;
+  const int R = B * (M + N);
   for (int i = 0; i < L; ++i) {
     const LayerW& lw = h->layers[i];
-    const int R = B * (M + N);
     for (int blk = 0; blk < 2; ++blk) {
       const BlockW& bw = blk == 0 ? lw.self : lw.cross;
       // QKV projection with fused rotary (self) / scale (cross) and head-major scatter
@@ -762,7 +771,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       if (prec == PREC_H3) {
         GemmH3Args g = gemm_h3_base();
         g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, bw.Wqkv); g.bias = Wb + bw.bqkv;
-        g.rtab = rt; g.a0_slot = s_x;
+        g.rtab = rt; g.a0_slot = s_x; g.rm = live;
         g.ro = ro(s_x, gn.gK, -1, 0.f, gn.bK, s_k, 1);  // M[k]: the attention's exact-softmax test
         g.ro_v = ro(s_x, gn.gV, -1, 0.f, gn.bV, s_v, h->fold ? 0 : 1);
         g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D; g.hl = hl;
@@ -770,7 +779,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       } else {
         GemmArgs g = gemm_base();
         g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wqkv; g.ldw = D; g.bias = Wb + bw.bqkv;
-        g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D; g.hl = hl;
+        g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D; g.hl = hl; g.rm = live;
         LG_HIP(gemm(g, epi_qkv, 1));
       }
       const size_t img1 = (size_t)B * H * M * 64;
@@ -780,12 +789,16 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       const void* kp1 = static_cast<const char*>(w.KP) + 2 * img1;
       const void* vp1 = static_cast<const char*>(w.VP) + 2 * img1;
       float* ctx1 = w.ctx + (size_t)B * M * D;
+      // per-pair counts of a pruned batch: image 0 = cnt[0..B), image 1 = cnt[B..2B)
+      const int* c0 = seg ? cnt : nullptr;
+      const int* c1 = seg ? cnt + B : nullptr;
+      const int* act = seg ? w.act : nullptr;
       if (blk == 0) {  // self: q/k/v of the same image, scale 1/sqrt(64) (SDPA default)
-        a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M, w.Cp, (long long)RP * D, RP, 0, rt, s_k};
-        a1 = {w.Q + img1, kp1, vp1, ps, ctx1, N, N, w.Cp, (long long)RP * D, RP, B * M, rt, s_k};
+        a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M, w.Cp, (long long)RP * D, RP, 0, rt, s_k, c0, c0, act};
+        a1 = {w.Q + img1, kp1, vp1, ps, ctx1, N, N, w.Cp, (long long)RP * D, RP, B * M, rt, s_k, c1, c1, act};
       } else {  // cross: qk fp32 in w.Q and as planes in w.KP, v planes in w.VP
-        a0 = {w.Q, kp1, vp1, ps, w.ctx, M, N, w.Cp, (long long)RP * D, RP, 0, rt, s_k};
-        a1 = {w.Q + img1, w.KP, w.VP, ps, ctx1, N, M, w.Cp, (long long)RP * D, RP, B * M, rt, s_k};
+        a0 = {w.Q, kp1, vp1, ps, w.ctx, M, N, w.Cp, (long long)RP * D, RP, 0, rt, s_k, c0, c1, act};
+        a1 = {w.Q + img1, w.KP, w.VP, ps, ctx1, N, M, w.Cp, (long long)RP * D, RP, B * M, rt, s_k, c1, c0, act};
       }
       LG_HIP(attn(a0, a1, blk == 0 ? 0.125f : 1.0f, blk == 1));
       if (prec == PREC_H3) {
@@ -796,7 +809,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
           s_msg = slot();
           GemmH3Args g = gemm_h3_base();
           g.A0 = image(w.Cp, D); g.K0 = D; g.K = D; wplanes(g, bw.Wo); g.bias = Wb + bw.bo;
-          g.rtab = rt; g.a0_slot = s_v; g.ro = ro(s_v, gn.go, -1, 0.f, gn.bo, s_msg);
+          g.rtab = rt; g.a0_slot = s_v; g.ro = ro(s_v, gn.go, -1, 0.f, gn.bo, s_msg); g.rm = live;
           g.R = R; g.Nout = D; g.Yp = w.Mp; g.yps = (long long)RP * D; g.yrows_pad = RP;
           LG_HIP(gemmh(g, EPI_STORE));
         }
@@ -805,7 +818,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         GemmH3Args g = gemm_h3_base();
         g.A0 = image(w.Xp, D); g.K0 = D; g.A1 = image(h->fold ? w.Cp : w.Mp, D); g.K = 2 * D;
         wplanes(g, bw.W1); g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D;
-        g.rtab = rt; g.a0_slot = s_x; g.a1_slot = s_msg;
+        g.rtab = rt; g.a0_slot = s_x; g.a1_slot = s_msg; g.rm = live;
         const int s_h = slot();
         const RangeOut ro_h = ro(-1, 0.f, -1, 0.f, gn.hb, s_h);
         if (gemm_h3_ln_split(R)) {  // small R: 64x64-tile GEMM into H1, then the LN + GELU row kernel
@@ -820,7 +833,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         const int s_xn = slot();
         g = gemm_h3_base();
         g.A0 = image(w.Hp, 2 * D); g.K0 = 2 * D; g.K = 2 * D; wplanes(g, bw.W2); g.bias = Wb + bw.b2;
-        g.rtab = rt; g.a0_slot = s_h;
+        g.rtab = rt; g.a0_slot = s_h; g.rm = live;  // frozen / dead rows keep their residual stream
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
         g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP;
         g.ro = ro(s_x, 1.f, -1, 0.f, gn.g2 * gn.hb + gn.b2, s_xn, 1);  // |x + ffn(..)| <= M_x + |W2|_1 hb + |b2|
@@ -830,17 +843,18 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         if (!h->fold) {
           GemmArgs g = gemm_base();
           g.A0 = w.ctx; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + bw.Wo; g.ldw = D; g.bias = Wb + bw.bo;
-          g.R = R; g.Nout = D; g.Y = w.msg; g.ldy = D;
+          g.R = R; g.Nout = D; g.Y = w.msg; g.ldy = D; g.rm = live;
           LG_HIP(gemm(g, EPI_STORE, 1));
         }
         GemmArgs g = gemm_base();
         g.A0 = w.X; g.lda0 = D; g.K0 = D; g.A1 = h->fold ? w.ctx : w.msg; g.lda1 = D; g.K = 2 * D;
         g.W = Wb + bw.W1; g.ldw = 2 * D; g.bias = Wb + bw.b1; g.R = R; g.Nout = 2 * D; g.Y = w.H1; g.ldy = 2 * D;
+        g.rm = live;
         LG_HIP(gemm(g, EPI_STORE, 1));
         LG_HIP(layernorm_gelu_512(w.H1, Wb + bw.g, Wb + bw.be, R, nullptr, 0, range_none(), st));
         g = gemm_base();
         g.A0 = w.H1; g.lda0 = 2 * D; g.K0 = 2 * D; g.K = 2 * D; g.W = Wb + bw.W2; g.ldw = 2 * D; g.bias = Wb + bw.b2;
-        g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
+        g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D; g.rm = live;
         LG_HIP(gemm(g, EPI_STORE, 1));
       }
     }
@@ -855,79 +869,70 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     }
     if (i == L - 1) break;
 
-    // ---- early stop (lightglue.py:527-531, check_if_stop :595-606; thresholds per :581-584)
+    // ---- early stop (lightglue.py:527-531, check_if_stop :595-606; thresholds per :581-584),
+    // decided per pair on the device
     const float thr_c = confidence_threshold(i, L);
     if (do_stop) {
       LG_HIP(gemv_256(w.X, Wb + lw.wt, Wb + lw.bt, w.tok, R, 1, st));
-      LG_HIP(hipMemsetAsync(w.counts, 0, sizeof(int), st));
-      LG_HIP(count_below(w.tok, thr_c, R, w.counts, st));
-      int below = 0;
-      LG_HIP(hipMemcpyAsync(&below, w.counts, sizeof(int), hipMemcpyDeviceToHost, st));
-      LG_HIP(hipStreamSynchronize(st));
-      const float ratio = 1.0f - (float)below / (float)(M0 + N0);
-      if (ratio > (float)c.depth_confidence) {
-        stop = i;
-        break;
-      }
+      LG_HIP(stop_decide(w.tok, cnt, w.act, w.stop, SL, thr_c, (float)c.depth_confidence, i, st));
     }
-    // ---- width pruning (lightglue.py:532-547, get_pruning_mask :586-593)
+    // ---- width pruning (lightglue.py:532-547, get_pruning_mask :586-593), compaction inside each
+    // pair's slot; a pair that stopped at this layer keeps every point (the reference breaks first)
     if (do_prune) {
       LG_HIP(gemv_256(w.X, Wb + lw.wm, Wb + lw.bm, w.z, R, 0, st));
-      LG_HIP(prune_flags(w.z, do_stop ? w.tok : nullptr, thr_w, thr_c, R, w.flags, st));
-      LG_HIP(compact_scan(w.flags, M, w.pos, w.counts + 1, st));
-      LG_HIP(compact_scan(w.flags + M, N, w.pos + M, w.counts + 2, st));
-      LG_HIP(compact_rows(w.X, w.X2, w.flags, w.pos, M, D, st));
-      LG_HIP(compact_rows(w.cosb, w.cos2, w.flags, w.pos, M, 32, st));
-      LG_HIP(compact_rows(w.sinb, w.sin2, w.flags, w.pos, M, 32, st));
-      LG_HIP(compact_index(w.ind0, w.ind0b, out->prune0 ? out->prune0 : nullptr, w.flags, w.pos, M, st));
-      int cnt[2] = {0, 0};
-      LG_HIP(hipMemcpyAsync(cnt, w.counts + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-      LG_HIP(hipStreamSynchronize(st));
-      const int M2 = cnt[0], N2 = cnt[1];
-      // image-1 rows land right after the M2 kept image-0 rows
-      LG_HIP(compact_rows(w.X + (size_t)M * D, w.X2 + (size_t)M2 * D, w.flags + M, w.pos + M, N, D, st));
-      LG_HIP(compact_rows(w.cosb + (size_t)M * 32, w.cos2 + (size_t)M2 * 32, w.flags + M, w.pos + M, N, 32, st));
-      LG_HIP(compact_rows(w.sinb + (size_t)M * 32, w.sin2 + (size_t)M2 * 32, w.flags + M, w.pos + M, N, 32, st));
-      LG_HIP(compact_index(w.ind1, w.ind1b, out->prune1 ? out->prune1 : nullptr, w.flags + M, w.pos + M, N, st));
+      LG_HIP(prune_scan(w.z, do_stop ? w.tok : nullptr, cnt, cntb, w.act, w.flags, w.pos, SL, thr_w, thr_c, st));
+      LG_HIP(compact_seg(w.X, w.X2, D, w.flags, w.pos, cnt, SL, st));
+      LG_HIP(compact_seg(w.cosb, w.cos2, 32, w.flags, w.pos, cnt, SL, st));
+      LG_HIP(compact_seg(w.sinb, w.sin2, 32, w.flags, w.pos, cnt, SL, st));
+      LG_HIP(compact_ind_seg(ind, indb, out->prune0, out->prune1, w.flags, w.pos, cnt, w.act, SL, st));
       std::swap(w.X, w.X2);
       std::swap(w.cosb, w.cos2);
       std::swap(w.sinb, w.sin2);
-      std::swap(w.ind0, w.ind0b);
-      std::swap(w.ind1, w.ind1b);
-      M = M2;
-      N = N2;
-      if (M == 0 || N == 0)
-        return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size (all keypoints pruned)");
+      std::swap(ind, indb);
+      std::swap(cnt, cntb);
+      live = RowMask{cnt, w.act, 1, SL};
       if (prec == PREC_H3) {
         const int s_c = slot();
-        LG_HIP(rows_to_planes(w.X, M + N, D, D, w.Xp, RP, 0, ro(s_x, 1.f, -1, 0.f, 0.f, s_c, 1), st));
+        const RowMask kept{cnt, nullptr, 0, SL};  // every kept row (frozen pairs too)
+        LG_HIP(rows_to_planes(w.X, R, D, D, w.Xp, RP, 0, ro(s_x, 1.f, -1, 0.f, 0.f, s_c, 1), st, nullptr, &kept));
         s_x = s_c;
       }
     }
   }
-  out->stop_layer = stop;
-  out->kept0 = M;
-  out->kept1 = N;
   out->precision_used = prec;
 
-  // ---- assignment head of the last executed layer (lightglue.py:549-551, MatchAssignment :306-315)
-  const LayerW& la = h->layers[stop];
-  const int R = B * (M + N);
-  {
+  // ---- assignment head of each pair's last executed layer (lightglue.py:549-551,
+  // MatchAssignment :306-315): one final_proj / matchability launch per layer a pair may have
+  // stopped at (rows of the other pairs are masked out)
+  auto head = [&](int li, const RowMask& m) -> int {
+    const LayerW& la = h->layers[li];
     if (prec == PREC_H3) {
       GemmH3Args g = gemm_h3_base();
       g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, la.Wf); g.bias = Wb + la.bf;
-      g.rtab = rt; g.a0_slot = s_x;
+      g.rtab = rt; g.a0_slot = s_x; g.rm = m;
       g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
       LG_HIP(gemmh(g, EPI_STORE));
     } else {
       GemmArgs g = gemm_base();
       g.A0 = w.X; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + la.Wf; g.ldw = D; g.bias = Wb + la.bf;
-      g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
+      g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f; g.rm = m;  // / d**0.25
       LG_HIP(gemm(g, EPI_STORE, 1));
     }
-    LG_HIP(gemv_256(w.X, Wb + la.wm, Wb + la.bm, w.z, R, 0, st));
-    // similarity: both operands are run-time values -> bf16x6 (full fp32 range)
+    LG_HIP(gemv_256_masked(w.X, Wb + la.wm, Wb + la.bm, w.z, R, m, st));
+    return LG_OK;
+  };
+  if (do_stop) {
+    for (int li = 0; li < L; ++li) {
+      const int rc = head(li, RowMask{cnt, w.stop, li, SL});
+      if (rc != LG_OK) return rc;
+    }
+  } else {
+    const int rc = head(L - 1, seg ? RowMask{cnt, nullptr, 0, SL} : RowMask{});
+    if (rc != LG_OK) return rc;
+  }
+  {
+    // similarity: both operands are run-time values -> bf16x6 (full fp32 range); per pair over
+    // the slot capacities (the assignment bounds everything by the kept counts)
     GemmArgs g = gemm_base();
     g.A0 = w.md; g.lda0 = D; g.K0 = D; g.K = D; g.sA = (long long)M * D;
     g.W = w.md + (size_t)B * M * D; g.ldw = D; g.sW = (long long)N * D;
@@ -949,13 +954,18 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     }
   }
   AssignArgs aa;
+  memset(&aa, 0, sizeof(aa));
   aa.sim = w.sim; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = out->log_assignment; aa.ws = w.aws;
   aa.B = B; aa.M = M; aa.N = N; aa.th = (float)c.filter_threshold;
+  if (seg) {  // per-pair kept counts; la holds pair b's [M_b+1][N_b+1] block at the capacity strides
+    aa.Mb = cnt;
+    aa.Nb = cnt + B;
+  }
   if (do_prune) {
     aa.m0 = w.m0c; aa.m1 = w.m1c; aa.s0 = w.s0c; aa.s1 = w.s1c;
     LG_HIP(assign(aa));
-    LG_HIP(remap_matches(w.m0c, w.m1c, w.s0c, w.s1c, w.ind0, w.ind1, M, N, out->matches0, out->matches1,
-                         out->matching_scores0, out->matching_scores1, M0, N0, st));
+    LG_HIP(remap_seg(w.m0c, w.m1c, w.s0c, w.s1c, ind, cnt, SL, out->matches0, out->matches1, out->matching_scores0,
+                     out->matching_scores1, st));
   } else {
     aa.m0 = out->matches0; aa.m1 = out->matches1; aa.s0 = out->matching_scores0; aa.s1 = out->matching_scores1;
     LG_HIP(assign(aa));
@@ -965,6 +975,25 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   if (out->ref_descriptors1)
     LG_HIP(hipMemcpyAsync(out->ref_descriptors1, w.X + (size_t)B * M * D, sizeof(float) * B * N * D,
                           hipMemcpyDeviceToDevice, st));
+  // kept counts and stop layers: on the device for the caller, and (one read-back, the only
+  // synchronisation of a pruning forward) as host outs
+  out->stop_layer = L - 1;
+  out->kept0 = M;
+  out->kept1 = N;
+  if (seg) {
+    if (out->kept) LG_HIP(hipMemcpyAsync(out->kept, cnt, 2 * B * sizeof(int), hipMemcpyDeviceToDevice, st));
+    if (out->stop) LG_HIP(hipMemcpyAsync(out->stop, w.stop, B * sizeof(int), hipMemcpyDeviceToDevice, st));
+    std::vector<int> hc(3 * (size_t)B);
+    LG_HIP(hipMemcpyAsync(hc.data(), cnt, 2 * B * sizeof(int), hipMemcpyDeviceToHost, st));
+    LG_HIP(hipMemcpyAsync(hc.data() + 2 * B, w.stop, B * sizeof(int), hipMemcpyDeviceToHost, st));
+    LG_HIP(hipStreamSynchronize(st));
+    out->kept0 = hc[0];
+    out->kept1 = hc[B];
+    out->stop_layer = hc[2 * B];
+    for (int k = 0; k < 2 * B; ++k)
+      if (hc[k] == 0)  // the reference's filter_matches fails on the empty set the same way
+        return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size (all keypoints pruned)");
+  }
   return LG_OK;
 }
 

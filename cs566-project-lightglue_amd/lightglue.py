@@ -308,10 +308,9 @@ class LightGlue(nn.Module):
                 "Use torch.no_grad() or .eval()"
             )
         lib = self._ensure_handle(device)
-        # early stop / pruning only in eval mode (lightglue.py:502-503)
+        # early stop / pruning only in eval mode (lightglue.py:502-503).  The reference asserts
+        # b == 1 (:528,533); here each pair of a batch prunes and stops on its own.
         pruning = (c.width_confidence > 0 or c.depth_confidence > 0) and not self.training
-        if pruning and b != 1:
-            raise AssertionError("pruning / early stop require batch size 1")  # :528,533
         L, dd = int(c.n_layers), int(c.descriptor_dim)
         m0 = torch.empty((b, m), dtype=torch.int64, device=device)
         m1 = torch.empty((b, n), dtype=torch.int64, device=device)
@@ -335,34 +334,51 @@ class LightGlue(nn.Module):
         inp = _lib.LGInputs(b, m, n, *[_ptr(t) for t in (k0, k1, d0, d1, s0, s1, sc0, o0, sc1, o1)], flags)
         final, layers = (None, rd0) if self.training else (rd0, None)
         final1, layers1 = (None, rd1) if self.training else (rd1, None)
-        out = _lib.LGOutputs(*[_ptr(t) for t in (m0, m1, ms0, ms1, la, final, final1, p0, p1, layers, layers1)], 0, 0, 0, 0)
+        kept = torch.empty((2, b), dtype=torch.int32, device=device) if pruning else None
+        stop = torch.empty((b,), dtype=torch.int32, device=device) if pruning else None
+        out = _lib.LGOutputs(*[_ptr(t) for t in (m0, m1, ms0, ms1, la, final, final1, p0, p1, layers, layers1, kept, stop)],
+                             0, 0, 0, 0)
         stream = torch.cuda.current_stream(device).cuda_stream
         _lib.check(
             lib.lg_forward(self._handle, ctypes.byref(inp), ctypes.byref(out), _ptr(self._ws), ws_bytes.value, ctypes.c_void_p(stream)),
             "lg_forward",
         )
         self.last_precision_used = "fp16x3" if out.precision_used == 0 else "bf16x6"
-        kept0, kept1 = out.kept0, out.kept1
-        if kept0 != m or kept1 != n:  # log_assignment was written for the kept points
-            la = la.view(-1)[: b * (kept0 + 1) * (kept1 + 1)].view(b, kept0 + 1, kept1 + 1)
         if c.width_confidence > 0 and not self.training:
             prune0, prune1 = p0, p1
         else:
             prune0 = torch.full((b, m), float(L), device=device)
             prune1 = torch.full((b, n), float(L), device=device)
-        return {
+        pred = {
             "matches0": m0,
             "matches1": m1,
             "matching_scores0": ms0,
             "matching_scores1": ms1,
-            "ref_descriptors0": rd0 if self.training else rd0[:, None, :kept0],
-            "ref_descriptors1": rd1 if self.training else rd1[:, None, :kept1],
+            "ref_descriptors0": rd0 if self.training else rd0[:, None],
+            "ref_descriptors1": rd1 if self.training else rd1[:, None],
             "log_assignment": la,
             "prune0": prune0,
             "prune1": prune1,
             # extension key (no reference counterpart): index of the last executed layer, per pair
             "stop_layer": torch.full((b,), out.stop_layer, dtype=torch.int64),
         }
+        if pruning:
+            # kept points per pair (the library synchronised once to return them): the
+            # reference's outputs cover the kept points only -- its log_assignment is
+            # [1, M'+1, N'+1] -- so they are sliced per pair; B > 1 gives per-pair lists
+            k0, k1 = out.kept0, out.kept1
+            pred["stop_layer"] = stop.to(torch.int64)
+            pred["kept0"], pred["kept1"] = kept[0].to(torch.int64), kept[1].to(torch.int64)
+            if b == 1:
+                pred["log_assignment"] = la[:, : k0 + 1, : k1 + 1]
+                pred["ref_descriptors0"] = rd0[:, None, :k0]
+                pred["ref_descriptors1"] = rd1[:, None, :k1]
+            else:
+                ks = kept.tolist()
+                pred["log_assignment"] = [la[i, : ks[0][i] + 1, : ks[1][i] + 1] for i in range(b)]
+                pred["ref_descriptors0"] = [rd0[i, None, : ks[0][i]] for i in range(b)]
+                pred["ref_descriptors1"] = [rd1[i, None, : ks[1][i]] for i in range(b)]
+        return pred
 
     # ------------------------------------------------------------ profiling (bench.py)
     def profile_enable(self, enable=True, only=None):

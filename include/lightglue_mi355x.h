@@ -14,9 +14,9 @@
  *   - Every pointer argument marked "device" is caller-allocated HIP device memory on the
  *     handle's device (torch CUDA tensors on ROCm); the library never frees caller memory.
  *   - All device work is stream-ordered on `stream` (a hipStream_t; NULL = default stream).
- *     lg_forward is fully asynchronous without pruning / early stop; with them it synchronises
- *     the stream where the kept point counts decide launch sizes (as the reference's torch.where
- *     does).
+ *     lg_forward is fully asynchronous without pruning / early stop; with them every decision
+ *     stays on the device and the stream is synchronised once, at the end, to return the kept
+ *     counts as host outs.
  *   - Functions return 0 on success and a negative LG_E* code on failure; lg_last_error()
  *     returns a thread-local message for the last failure on the calling thread.
  *   - A handle belongs to one device; it is not re-entrant (one forward at a time), separate
@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define LG_ABI_VERSION 3
+#define LG_ABI_VERSION 4
 
 enum {
   LG_OK = 0,
@@ -92,7 +92,7 @@ typedef struct {
   int64_t* matches1;            /* device [B,N]  (required) */
   float* matching_scores0;      /* device [B,M]  (required) */
   float* matching_scores1;      /* device [B,N]  (required) */
-  float* log_assignment;        /* device [B,M'+1,N'+1] or NULL (M',N' = kept counts) */
+  float* log_assignment;        /* device [B,M+1,N+1] or NULL (with pruning: pair b's kept block, see kept) */
   float* ref_descriptors0;      /* device [B,M,256] or NULL: final descriptors (first M' rows valid) */
   float* ref_descriptors1;      /* device [B,N,256] or NULL */
   int64_t* prune0;              /* device [B,M] or NULL: layer count per point (lightglue.py:511,540,564) */
@@ -101,8 +101,13 @@ typedef struct {
                                  * reference's training-mode ref_descriptors, lightglue.py:521-524,
                                  * torch.stack(all_desc0, 1) at :572); needs pruning / early stop off */
   float* layer_descriptors1;    /* device [B,L,N,256] or NULL */
-  int32_t stop_layer;           /* host out: index of the last executed layer */
-  int32_t kept0, kept1;         /* host out: M', N' after width pruning (= M, N without) */
+  int32_t* kept;                /* device [2,B] or NULL: kept points per pair after width pruning
+                                 * (row 0 image 0, row 1 image 1); pair b's outputs are the first
+                                 * kept[.,b] rows of ref_descriptors*, and log_assignment holds its
+                                 * [kept[0,b]+1, kept[1,b]+1] block at the [M+1, N+1] strides */
+  int32_t* stop;                /* device [B] or NULL: last executed layer per pair (early stop) */
+  int32_t stop_layer;           /* host out: last executed layer (of pair 0) */
+  int32_t kept0, kept1;         /* host out: M', N' of pair 0 after width pruning (= M, N without) */
   int32_t precision_used;       /* host out: 0 = fp16x3, 1 = bf16x6 (LG_PREC_X6) */
 } lg_outputs_t;
 
@@ -128,8 +133,9 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
 /* Device scratch needed by lg_forward for this shape (bytes, 256-B aligned pieces). */
 int lg_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
 
-/* LightGlue.forward (lightglue.py:444-579), eval mode.  Pruning / early stop need B == 1
- * (lightglue.py:528,533). */
+/* LightGlue.forward (lightglue.py:444-579), eval mode.  Pruning / early stop work for any B
+ * (the reference asserts B == 1, lightglue.py:528,533; here every pair prunes and stops on its
+ * own, with the counts kept on the device) and synchronise the stream once at the end. */
 int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* workspace,
                size_t workspace_bytes, void* stream);
 

@@ -531,3 +531,72 @@ def test_values_beyond_fp16_range_with_pruning():
         a = auto(_gpu_data(data))
         b = x6(_gpu_data(data))
     _assert_same_result(a, b)
+
+
+def _stack_pairs(datas):
+    return {k: np.concatenate([d[k] for d in datas], 0) for k in datas[0]}
+
+
+@pytest.mark.parametrize("precision", ["auto", "bf16x6"])
+@pytest.mark.parametrize("name,seeds", [("prune_depth_width_n512", (22, 5, 9)), ("prune_width_n512", (21, 3)),
+                                        ("early_stop_n256", (23, 4, 6, 8))])
+def test_batched_pruning_equals_per_pair(name, seeds, precision):
+    """Pruning / early stop for B > 1 (the reference asserts B == 1, lightglue.py:528,533): every
+    pair prunes and stops on its own with device-side counts, so a batch gives exactly what each
+    pair gives alone -- matches, prune counts, stop layers, its log-assignment block and its kept
+    descriptors."""
+    from lightglue_amd.weights import synthetic_pair
+
+    g = load(name)
+    conf, sd, data = case_inputs(g["meta"])
+    pkw = dict(g["meta"]["pair"])
+    pairs = []
+    for sd_ in seeds:
+        pkw["seed"] = sd_
+        pairs.append(synthetic_pair(**pkw))
+    model = _model(conf, sd, precision)
+    with torch.no_grad():
+        full = model(_gpu_data(_stack_pairs(pairs)))
+        singles = [model(_gpu_data(p)) for p in pairs]
+    for i, one in enumerate(singles):
+        for k in ("matches0", "matches1", "prune0", "prune1"):
+            assert torch.equal(one[k][0], full[k][i]), (i, k)
+        assert int(one["stop_layer"][0]) == int(full["stop_layer"][i])
+        assert torch.allclose(one["matching_scores0"][0], full["matching_scores0"][i], atol=1e-6)
+        la1, laB = one["log_assignment"][0], full["log_assignment"][i]
+        assert la1.shape == laB.shape, (i, la1.shape, laB.shape)
+        assert torch.allclose(la1, laB, atol=1e-5)
+        assert torch.allclose(one["ref_descriptors0"][0, 0], full["ref_descriptors0"][i][0], atol=1e-6)
+    # the batch really exercises ragged sets: the pairs keep different numbers of points
+    if "width" in conf and conf.get("width_confidence", -1) > 0:
+        assert len({int(k) for k in full["kept0"].tolist()}) > 1
+
+
+def test_configs3_batched_pruning_equals_golden():
+    """configs[3] shape (N = 2048, width = depth = 0.95) batched: the reference golden pair (prunes
+    ~10 % per layer, stops after layer 5) four times in one forward, with image 1 permuted in two of
+    them; every pair must give the golden matches and prune counts exactly."""
+    g = load("prune_depth_width_n2048")
+    conf, sd, data = case_inputs(g["meta"])
+    N = data["keypoints1"].shape[1]
+    rng = np.random.default_rng(1)
+    batch = {k: np.repeat(v, 4, axis=0) for k, v in data.items()}
+    perms = []
+    for b in range(4):
+        perm = rng.permutation(N) if b % 2 else np.arange(N)
+        batch["keypoints1"][b] = data["keypoints1"][0][perm]
+        batch["descriptors1"][b] = data["descriptors1"][0][perm]
+        perms.append(perm)
+    model = _model(conf, sd)
+    with torch.no_grad():
+        pred = model(_gpu_data(batch))
+    assert [int(s) + 1 for s in pred["stop_layer"].tolist()] == [int(g["n_layers_run"])] * 4
+    m0, m1 = pred["matches0"].cpu().numpy(), pred["matches1"].cpu().numpy()
+    p0, p1 = pred["prune0"].cpu().numpy(), pred["prune1"].cpu().numpy()
+    for b, perm in enumerate(perms):
+        inv = np.argsort(perm)
+        e0 = np.where(g["matches0"][0] > -1, inv[np.maximum(g["matches0"][0], 0)], -1)
+        np.testing.assert_array_equal(m0[b], e0, err_msg=f"pair {b}")
+        np.testing.assert_array_equal(m1[b], g["matches1"][0][perm], err_msg=f"pair {b}")
+        np.testing.assert_array_equal(p0[b], g["prune0"][0], err_msg=f"pair {b}")
+        np.testing.assert_array_equal(p1[b], g["prune1"][0][perm], err_msg=f"pair {b}")

@@ -5,9 +5,10 @@
 
 One JSON line per config:
   configs[1]  N=1024, 9 layers, B=1 (latency-shaped: one pair per forward)
-  configs[3]  N=2048, width/depth pruning on (0.95 / 0.95), B=1 per forward (the reference's pruning
-              is B == 1 only, lightglue.py:528,533); MegaDepth-like 1600x1200 keypoints; the
-              per-GPU share of the 8-GPU work-queue run (parallel.match_dynamic pulls single pairs)
+  configs[3]  N=2048, width/depth pruning on (0.95 / 0.95) with weights that really prune and stop
+              early, 32 pairs per forward (each pair prunes / stops on its own; the reference asserts
+              B == 1, lightglue.py:528,533); MegaDepth-like 1600x1200 keypoints; also the same
+              batch unpruned and one pair per forward
   configs[4]  N=4096, 8 pairs per GPU (64 over 8 GPUs): the LightGlue forward at N=4096 and the
               SuperGlue log-domain Sinkhorn (superglue.py:173-201, 50 iterations) on the
               [8, 4096, 4096] similarity, each timed on its own; Sinkhorn against the HBM roofline
@@ -58,28 +59,44 @@ def cfg1(dev, reps):
             "matches": int((pred["matches0"] > -1).sum())}
 
 
-def cfg3(dev, reps):
+def prune_recipe_model(conf, dev):
+    """Weights that really prune and stop (tests/golden/make_golden.py, configs[3] case: layers 0..4
+    prune ~10 % of the points, layer 5 fires the early stop)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import PRUNE2K_MATCH_BIAS, PRUNE2K_TOKEN_BIAS  # noqa: E402
+
+    sd = synthetic_state_dict(conf, seed=8)
+    for i, (tb, mb) in enumerate(zip(PRUNE2K_TOKEN_BIAS, PRUNE2K_MATCH_BIAS)):
+        if tb is not None:
+            sd[f"token_confidence.{i}.token.0.bias"][:] = tb
+        if mb is not None:
+            sd[f"log_assignment.{i}.matchability.bias"][:] = mb
+    m = LightGlue(conf).eval().to(dev)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    return m
+
+
+def cfg3(dev, reps, B=32):
+    """configs[3]: N = 2048 with width + depth pruning 0.95, B pairs per forward (every pair prunes
+    and stops on its own, device-side counts, one sync per forward), against the same batch
+    unpruned and against one pair per forward (the reference's B == 1 regime)."""
     conf = {"filter_threshold": 0.1, "width_confidence": 0.95, "depth_confidence": 0.95}
-    m = model_for(conf, dev)
-    P = 16
-    data = gpu_pairs(P, 2048, 256, seed=3, device=dev, size=(1600.0, 1200.0))
-    pairs = [{k: (v[i:i + 1] if torch.is_tensor(v) else {"image_size": v["image_size"][i:i + 1]})
-              for k, v in data.items()} for i in range(P)]
-    layers = []
-
-    def run():
-        layers.clear()
-        for d in pairs:
-            with torch.no_grad():
-                p = m(d)
-            layers.append(int(p["stop_layer"][0]))
-        return p
-
-    s, _ = timed(run, max(1, reps // 4), warm=1)
-    return {"config": "configs[3]: N=2048 (1600x1200 keypoints), width+depth pruning 0.95, B=1 per forward, "
-                      "per-GPU share of the pair-sharded work queue",
-            "value": round(P / s, 2), "unit": "image-pairs/s per GPU", "ms_per_pair": round(1e3 * s / P, 3),
-            "pairs_in_sample": P, "layers_executed": layers}
+    m = prune_recipe_model(conf, dev)
+    m_full = prune_recipe_model({"filter_threshold": 0.1}, dev)
+    data = gpu_pairs(B, 2048, 256, seed=3, device=dev, size=(1600.0, 1200.0))
+    with torch.no_grad():
+        s, pred = timed(lambda: m(data), reps)
+        s_full, _ = timed(lambda: m_full(data), max(1, reps // 2), warm=1)
+        ones = [{k: (v[i:i + 1] if torch.is_tensor(v) else {"image_size": v["image_size"][i:i + 1]})
+                 for k, v in data.items()} for i in range(8)]
+        s1, _ = timed(lambda: [m(d) for d in ones], max(1, reps // 4), warm=1)
+    kept = (pred["kept0"].float() / 2048).tolist()
+    return {"config": f"configs[3]: N=2048 (1600x1200 keypoints), width+depth pruning 0.95, batch={B} per forward",
+            "value": round(B / s, 2), "unit": "image-pairs/s per GPU", "ms_per_pair": round(1e3 * s / B, 3),
+            "unpruned_same_batch_pairs_per_s": round(B / s_full, 2),
+            "one_pair_per_forward_pairs_per_s": round(8 / s1, 2),
+            "layers_executed": sorted({int(x) + 1 for x in pred["stop_layer"].tolist()}),
+            "kept_fraction_image0_mean": round(sum(kept) / len(kept), 3)}
 
 
 def cfg4(dev, reps):

@@ -16,6 +16,10 @@ def __getattr__(name):
         from .lightglue import LightGlue
 
         return LightGlue
+    if name == "SuperPoint":
+        from .superpoint import SuperPoint
+
+        return SuperPoint
     if name in ("log_optimal_transport", "filter_matches"):
         from . import assignment
 

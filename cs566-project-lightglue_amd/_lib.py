@@ -32,6 +32,16 @@ EXPORTED_SYMBOLS = [
     "lg_profile_read",
     "lg_attention_workspace_bytes",
     "lg_attention",
+    # SuperPoint extractor (include/superpoint_mi355x.h)
+    "sp_create",
+    "sp_destroy",
+    "sp_weight_count",
+    "sp_weight_name",
+    "sp_weight_numel",
+    "sp_load_weights",
+    "sp_workspace_bytes",
+    "sp_forward",
+    "sp_sample_descriptors",
 ]
 KERNEL_IDS = {"attention": 0, "gemm": 1, "assign": 2}
 # lg_config_t.precision (include/lightglue_mi355x.h): "auto" = fp16x3 (device-side range scaling)
@@ -99,6 +109,45 @@ class LGOutputs(ctypes.Structure):
     ]
 
 
+class SPConfig(ctypes.Structure):  # sp_config_t
+    _fields_ = [
+        ("has_detector", ctypes.c_int32),
+        ("has_descriptor", ctypes.c_int32),
+        ("descriptor_dim", ctypes.c_int32),
+        ("nms_radius", ctypes.c_int32),
+        ("refinement_radius", ctypes.c_int32),
+        ("remove_borders", ctypes.c_int32),
+        ("legacy_sampling", ctypes.c_int32),
+        ("detection_threshold", ctypes.c_float),
+    ]
+
+
+class SPInputs(ctypes.Structure):  # sp_inputs_t
+    _fields_ = [
+        ("B", ctypes.c_int32),
+        ("C", ctypes.c_int32),
+        ("H", ctypes.c_int32),
+        ("W", ctypes.c_int32),
+        ("image", _P),
+        ("image_size", _P),
+        ("max_keypoints", ctypes.c_int32),
+        ("sparse", ctypes.c_int32),
+    ]
+
+
+class SPOutputs(ctypes.Structure):  # sp_outputs_t
+    _fields_ = [
+        ("dense_scores", _P),
+        ("dense_descriptors", _P),
+        ("capacity", ctypes.c_int32),
+        ("keypoints", _P),
+        ("keypoint_scores", _P),
+        ("descriptors", _P),
+        ("counts", _P),
+        ("host_counts", _P),
+    ]
+
+
 class LightGlueLibError(RuntimeError):
     pass
 
@@ -143,6 +192,18 @@ def load():
             ctypes.c_int,
             [_P, _P, _P, i32, i32, i32, i32, ctypes.c_float, i32, _P, _P, sz, _P],
         ),
+        "sp_create": (ctypes.c_int, [ctypes.POINTER(SPConfig), ctypes.c_int, ctypes.POINTER(_P)]),
+        "sp_destroy": (ctypes.c_int, [_P]),
+        "sp_weight_count": (ctypes.c_int, [_P]),
+        "sp_weight_name": (ctypes.c_char_p, [_P, ctypes.c_int]),
+        "sp_weight_numel": (ctypes.c_int64, [_P, ctypes.c_int]),
+        "sp_load_weights": (
+            ctypes.c_int,
+            [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64), _P],
+        ),
+        "sp_workspace_bytes": (ctypes.c_int, [_P, i32, i32, i32, i32, i32, ctypes.POINTER(sz)]),
+        "sp_forward": (ctypes.c_int, [_P, ctypes.POINTER(SPInputs), ctypes.POINTER(SPOutputs), _P, sz, _P]),
+        "sp_sample_descriptors": (ctypes.c_int, [_P, _P, _P, i32, i32, _P, _P, sz, _P]),
         "lg_profile_read": (
             ctypes.c_int,
             [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),

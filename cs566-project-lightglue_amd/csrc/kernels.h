@@ -278,4 +278,61 @@ size_t sinkhorn_workspace_floats(int B, int M, int N);
 hipError_t log_optimal_transport(const float* scores, float alpha, int B, int M, int N, int iters, float* Z, float* ws,
                                  hipStream_t st);
 
+// ---- SuperPoint extractor (gluefactory_nonfree/superpoint.py, superpoint.hip) --------------
+// Feature maps are NHWC plane images: rows = pixels (n, y, x) in row-major order, K = channels.
+// An image that feeds a 3x3 convolution keeps rows [R, rows_pad) zero (sp_zero_rows): the
+// implicit GEMM reads its last row for every tap that falls outside the image.
+//
+// gray (RGB: 0.299 r + 0.587 g + 0.114 b) + conv1a (1 -> 64, 3x3, pad 1) + bias + ReLU -> planes
+hipError_t sp_conv1a(const float* image, int B, int C, int H, int W, const float* w, const float* bias, _Float16* Y,
+                     int yrows_pad, const RangeOut& ro, hipStream_t st);
+// 3x3 convolution (pad 1) as an implicit fp16x3 GEMM + bias + ReLU (+ 2x2 max-pool, floor):
+//   Y = planes of relu(conv(X) + bias) [B*H*W rows] or of its pool [B*(H/2)*(W/2) rows]
+struct ConvH3Args {
+  PlaneRef X;            // input image, rows B*H*W, K = Cin, rows_pad > B*H*W (zero tail)
+  int B, H, W, Cin, Cout;
+  PlaneRef Wt;           // [Cout][9*Cin] weight planes, k = (3*ky + kx)*Cin + ci (rows_pad = Cout)
+  float acc_scale;       // 2^-(11+sw)
+  const float* bias;     // [Cout]
+  _Float16* Y;           // output planes (K = Cout)
+  long long yps;
+  int yrows_pad;
+  const unsigned* rtab;  // range table: X holds x * 2^-E[x_slot]
+  int x_slot;
+  RangeOut ro;           // Y
+  int pool;
+};
+hipError_t sp_conv3x3(const ConvH3Args& a, hipStream_t st);
+hipError_t sp_zero_rows(_Float16* planes, long long ps, int rows_pad, int K, int R, hipStream_t st);
+// conv weight [Cout][Cin][k][k] -> dst [Cout][k*k*Cin] (column (k*ky + kx)*Cin + ci)
+hipError_t sp_repack_conv(const float* w, int Cout, int Cin, int ksize, float* dst, hipStream_t st);
+// detector head: 65 logits per cell (row stride ld) -> softmax without the dustbin, unfolded:
+// scores[b][8y + dy][8x + dx] = p[8 dy + dx] (superpoint.py:224-230)
+hipError_t sp_detector_scores(const float* logits, int ld, int B, int Hc, int Wc, float* scores, hipStream_t st);
+// dense descriptors: rows of 256 -> x / max(|x|, 1e-12) (in place allowed)
+hipError_t sp_desc_normalize(const float* x, int rows, float* y, hipStream_t st);
+// simple_nms (superpoint.py:60-80) on [B][Hs][Ws]; mask / sup bytes, ss floats (scratch)
+hipError_t sp_nms(const float* scores, int B, int Hs, int Ws, int radius, unsigned char* mask, unsigned char* sup,
+                  float* ss, hipStream_t st);
+// candidates: nms(scores) with borders at -1 (superpoint.py:244-254) > threshold, per image in
+// row-major order -> key (orderable score bits) / pixel index; cnt[b] = their number.
+// image_size: [B][2] (w, h) or null.  blk: scratch ints, B * sp_cand_blocks(Hs)
+int sp_cand_blocks(int Hs);
+hipError_t sp_candidates(const float* scores, const unsigned char* mask, int B, int Hs, int Ws, int border,
+                         const float* image_size, float thr, unsigned* key, int* idx, int* blk, int* cnt, hipStream_t st);
+// per image: the k best candidates by score, sorted (torch.topk, superpoint.py:83-87; ties -> lower
+// pixel index first), or all of them in row-major order when k <= 0 or there are not more than k.
+// Writes sel_idx [B][cap] (pixel index), sel_score [B][cap], n[b]; k <= kSpSelectMax
+constexpr int kSpSelectMax = 16384;
+hipError_t sp_select(const unsigned* key, const int* idx, const int* cnt, int B, int cand_cap, int k, int* sel_idx,
+                     float* sel_score, int cap, int* n, hipStream_t st);
+// keypoints (x, y) [B][cap][2] from pixel indices; radius > 0: soft-argmax refinement on the dense
+// scores (superpoint.py:97-113)
+hipError_t sp_keypoints(const int* sel_idx, const int* n, int B, int cap, int Hs, int Ws, const float* dense,
+                        int radius, float* kpts, hipStream_t st);
+// bilinear descriptor sampling at (x, y) keypoints + L2 normalisation (superpoint.py:117-149);
+// desc NHWC [B][Hc][Wc][256]; out [B][cap][256]; kpts_out (nullable) = kpts + 0.5
+hipError_t sp_sample(const float* kpts, const int* n, int B, int cap, const float* desc, int Hc, int Wc, int legacy,
+                     float* out, float* kpts_out, hipStream_t st);
+
 }  // namespace lg

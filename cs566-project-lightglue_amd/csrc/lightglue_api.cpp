@@ -109,6 +109,14 @@ size_t align64(size_t n) { return (n + 63) & ~size_t(63); }
 
 }  // namespace
 
+namespace lg {
+// the other C-ABI families of this library (superpoint_api.cpp) report through lg_last_error()
+int api_fail(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+}  // namespace lg
+
 struct lg_handle {
   lg_config_t cfg;
   int device;

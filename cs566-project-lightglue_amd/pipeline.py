@@ -121,12 +121,22 @@ class TwoViewPipeline(BaseModel):
         return pred
 
 
+def _superpoint():
+    from .superpoint import SuperPoint
+
+    return SuperPoint
+
+
 _REGISTRY = {
     "lightglue": LightGlue,
     "matchers.lightglue": LightGlue,
     "lightglue_pretrained_MINE": LightGluePreTrainedMINE,
     "matchers.lightglue_pretrained_MINE": LightGluePreTrainedMINE,
     "two_view_pipeline": TwoViewPipeline,
+    # the extractor (gluefactory_nonfree/superpoint.py), resolved lazily
+    "gluefactory_nonfree.superpoint": _superpoint,
+    "extractors.superpoint": _superpoint,
+    "superpoint": _superpoint,
 }
 
 
@@ -140,7 +150,8 @@ def get_model(name):
     prefix the reference also tries (backward compatibility)."""
     for path in (name, f"matchers.{name}", f"extractors.{name}"):
         if path in _REGISTRY:
-            return _REGISTRY[path]
+            obj = _REGISTRY[path]
+            return obj() if obj is _superpoint else obj
     paths = [name, f"gluefactory.models.{name}", f"gluefactory.models.extractors.{name}",
              f"gluefactory.models.matchers.{name}"]
     raise RuntimeError(f'Model {name} not found in any of [{" ".join(paths)}]')

@@ -21,7 +21,7 @@ def declared_symbols():
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        syms |= set(re.findall(r"\b(lg_[a-z_0-9]+)\s*\(", src))
+        syms |= set(re.findall(r"\b((?:lg|sp)_[a-z_0-9]+)\s*\(", src))
     return syms
 
 
@@ -40,9 +40,10 @@ def test_ctypes_structs_match_header_layout(tmp_path):
     include/lightglue_mi355x.h (gcc on a generated offsetof table)."""
     import subprocess
 
-    structs = {"lg_config_t": _lib.LGConfig, "lg_inputs_t": _lib.LGInputs, "lg_outputs_t": _lib.LGOutputs}
+    structs = {"lg_config_t": _lib.LGConfig, "lg_inputs_t": _lib.LGInputs, "lg_outputs_t": _lib.LGOutputs,
+               "sp_config_t": _lib.SPConfig, "sp_inputs_t": _lib.SPInputs, "sp_outputs_t": _lib.SPOutputs}
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{os.path.join(ROOT, "include", "lightglue_mi355x.h")}"',
-             "int main(void) {"]
+             f'#include "{os.path.join(ROOT, "include", "superpoint_mi355x.h")}"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
         for f, _ in py._fields_:
@@ -136,3 +137,37 @@ def test_synthetic_recipes_are_deterministic():
     assert all(np.array_equal(p[k], q[k]) for k in p)
     assert p["keypoints1"].shape == (2, 30, 2)
     np.testing.assert_allclose(np.linalg.norm(p["descriptors1"], axis=-1), 1.0, atol=1e-5)
+
+
+def test_superpoint_module_schema_matches_reference_schema():
+    """lightglue_amd.SuperPoint registers the reference's conv modules (superpoint.py:174-196), so
+    its state dict has the recipe schema's keys, order and shapes for every head combination."""
+    from lightglue_amd.sp_weights import SP_DEFAULT_CONF, superpoint_schema
+    from lightglue_amd.superpoint import SuperPoint
+
+    for conf in ({}, {"has_detector": False, "sparse_outputs": False}, {"has_descriptor": False, "sparse_outputs": False}):
+        sd = SuperPoint(conf).state_dict()
+        schema = superpoint_schema(conf)
+        assert list(sd.keys()) == [n for n, _ in schema]
+        for n, shape in schema:
+            assert tuple(sd[n].shape) == tuple(shape), n
+    assert set(SP_DEFAULT_CONF) == {  # superpoint.py:153-169 + base_model.py:54-59
+        "name", "trainable", "freeze_batch_normalization", "timeit", "has_detector", "has_descriptor",
+        "descriptor_dim", "sparse_outputs", "dense_outputs", "nms_radius", "refinement_radius",
+        "detection_threshold", "max_num_keypoints", "max_num_keypoints_val", "force_num_keypoints",
+        "randomize_keypoints_training", "remove_borders", "legacy_sampling"}
+
+
+def test_superpoint_registered_in_pipeline():
+    from lightglue_amd import pipeline
+    from lightglue_amd.superpoint import SuperPoint
+
+    for name in ("gluefactory_nonfree.superpoint", "extractors.superpoint", "superpoint"):
+        assert pipeline.get_model(name) is SuperPoint
+
+
+def test_superpoint_cpu_input_raises():
+    from lightglue_amd.superpoint import SuperPoint
+
+    with pytest.raises(RuntimeError, match="HIP device"):
+        SuperPoint({})({"image": torch.zeros(1, 1, 64, 64)})

@@ -9,6 +9,7 @@ One JSON line per config:
               early, 32 pairs per forward (each pair prunes / stops on its own; the reference asserts
               B == 1, lightglue.py:528,533); MegaDepth-like 1600x1200 keypoints; also the same
               batch unpruned and one pair per forward
+  sp          SuperPoint (§8f row 3): 16 gray 640x480 images per forward, top-2048 keypoints
   configs[4]  N=4096, 8 pairs per GPU (64 over 8 GPUs): the LightGlue forward at N=4096 and the
               SuperGlue log-domain Sinkhorn (superglue.py:173-201, 50 iterations) on the
               [8, 4096, 4096] similarity, each timed on its own; Sinkhorn against the HBM roofline
@@ -124,13 +125,39 @@ def cfg4(dev, reps):
             "Z_finite": bool(torch.isfinite(Z).all())}
 
 
+def sp_flops(H, W):
+    """Algorithmic flops of one SuperPoint dense forward (2 per MAC, superpoint.py:208-235)."""
+    f, h, w = 0, H, W
+    for i, (ci, co) in enumerate([(1, 64), (64, 64), (64, 64), (64, 64), (64, 128), (128, 128), (128, 128), (128, 128)]):
+        f += 2 * h * w * ci * co * 9
+        if i in (1, 3, 5):
+            h, w = h // 2, w // 2
+    return f + 2 * h * w * (2 * 128 * 256 * 9 + 256 * 65 + 256 * 256)
+
+
+def cfg_sp(dev, reps, B=16, H=480, W=640, k=2048):
+    """SuperPoint extractor (§8f row 3): B gray 640x480 images per forward, top-2048 keypoints."""
+    from lightglue_amd import SuperPoint
+    from lightglue_amd.sp_weights import superpoint_state_dict, synthetic_images
+
+    m = SuperPoint({"max_num_keypoints": k}).eval().to(dev)
+    m.load_state_dict({n: torch.from_numpy(v) for n, v in superpoint_state_dict({}, seed=0).items()})
+    img = torch.from_numpy(synthetic_images(B, 1, H, W, seed=1)).to(dev)
+    with torch.no_grad():
+        s, pred = timed(lambda: m({"image": img}), reps)
+    fl = sp_flops(H, W) * B
+    return {"config": f"SuperPoint {W}x{H} gray, batch={B}, max_num_keypoints={k}", "value": round(B / s, 2),
+            "unit": "images/s", "ms_per_image": round(1e3 * s / B, 3), "dense_tflops_wall": round(fl / s / 1e12, 1),
+            "keypoints": list(pred["keypoints"].shape)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="1,3,4")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    fns = {"1": cfg1, "3": cfg3, "4": cfg4}
+    fns = {"1": cfg1, "3": cfg3, "4": cfg4, "sp": cfg_sp}
     for k in a.only.split(","):
         print(json.dumps(fns[k](dev, a.reps)), flush=True)
 

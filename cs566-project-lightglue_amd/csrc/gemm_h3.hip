@@ -385,20 +385,25 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem));
   } else if constexpr (EPI == EPI_STORE) {
     static_assert(WN == 64, "EPI_STORE tile");
-    // Transposed through LDS (free after the k-loop; 8 KiB per wave per 32-row pass) so that every
-    // lane owns 8 consecutive columns of a row: fp32 stores, residual loads and plane-image
-    // stores are then 16 bytes per lane.  LDS element (r, c) of a pass at r*64 + (c ^ 4*(r&1))
-    // (conflict-free ds_write_b32 rows and ds_read_b128 groups).
+    // Transposed through LDS (free after the k-loop; 8 KiB per wave per 32-row pass), LDS element
+    // (r, c) of a pass at r*64 + (c ^ 4*(r&1)) (conflict-free ds_write_b32 rows, ds_read_b128 groups).
+    // fp32 rows (Y, residual) are read and written as full 128-byte lines per 8 lanes: a lane owns
+    // columns 4(lane&7) .. +3 and 32 + 4(lane&7) .. +3 (a 16-byte access at a 32-byte stride would
+    // write half lines, which measured 2x the cost per byte); the finished values go back into the
+    // LDS slots they came from and the plane pass re-reads them as 8 consecutive columns (one
+    // 16-byte fp16 chunk per plane: consecutive rows of a k-block are contiguous).
     static_assert(NW * 32 * 64 * 4 <= NSTAGE * STAGE_BYTES, "epilogue scratch");
     float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
-    const int cq = (lane & 7) * 8;                     // first of the lane's 8 columns (in the wave tile)
-    const int col0 = n0 + wn0 + cq;
+    const int cq = (lane & 7) * 8;  // plane pass: the lane's 8 columns (in the wave tile)
+    const int c4 = (lane & 7) * 4;  // fp32 pass: columns c4 .. c4+3 and 32 + c4 ..
     const int eo = g.Yp ? eo_main : 0;
     const float so = ldexpf(1.f, -eo);
+    const bool fp32_pass = g.Y || g.res || !g.Yp;
     f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
     if (g.bias) {
-      b0 = *reinterpret_cast<const f32x4*>(g.bias + col0);
-      b1 = *reinterpret_cast<const f32x4*>(g.bias + col0 + 4);
+      const int ca = fp32_pass ? c4 : cq, cb = fp32_pass ? 32 + c4 : cq + 4;
+      b0 = *reinterpret_cast<const f32x4*>(g.bias + n0 + wn0 + ca);
+      b1 = *reinterpret_cast<const f32x4*>(g.bias + n0 + wn0 + cb);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -407,34 +412,60 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         return v;
       });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (fp32_pass) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int rr = (lane >> 3) + 8 * k;
-        const int row = m0 + wm0 + i * 32 + rr;
-        const int sw = (rr & 1) << 2;
-        f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
-        f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
-        if (row < g.R && row_live(g.rm, row)) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v0[e] = fmaf(v0[e], accs, b0[e]) * g.out_scale;
-            v1[e] = fmaf(v1[e], accs, b1[e]) * g.out_scale;
-          }
-          if (g.res) {
-            const float* rp = g.res + (size_t)row * g.ldr + col0;
-            const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp), r1 = *reinterpret_cast<const f32x4*>(rp + 4);
+        for (int k = 0; k < 4; ++k) {
+          const int rr = (lane >> 3) + 8 * k;
+          const int row = m0 + wm0 + i * 32 + rr;
+          const int sw = (rr & 1) << 2;
+          float* pa = ep + rr * 64 + (c4 ^ sw);
+          float* pb = ep + rr * 64 + ((32 + c4) ^ sw);
+          f32x4 v0 = *reinterpret_cast<const f32x4*>(pa);
+          f32x4 v1 = *reinterpret_cast<const f32x4*>(pb);
+          if (row < g.R && row_live(g.rm, row)) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              v0[e] = r0[e] + v0[e];
-              v1[e] = r1[e] + v1[e];
+              v0[e] = fmaf(v0[e], accs, b0[e]) * g.out_scale;
+              v1[e] = fmaf(v1[e], accs, b1[e]) * g.out_scale;
+            }
+            if (g.res) {
+              const float* rp = g.res + (size_t)row * g.ldr + n0 + wn0 + c4;
+              const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp), r1 = *reinterpret_cast<const f32x4*>(rp + 32);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v0[e] = r0[e] + v0[e];
+                v1[e] = r1[e] + v1[e];
+              }
+            }
+            if (g.Y) {
+              float* yp = g.Y + (size_t)row * g.ldy + n0 + wn0 + c4;
+              *reinterpret_cast<f32x4*>(yp) = v0;
+              *reinterpret_cast<f32x4*>(yp + 32) = v1;
+            }
+            if (g.Yp) {
+              *reinterpret_cast<f32x4*>(pa) = v0;
+              *reinterpret_cast<f32x4*>(pb) = v1;
             }
           }
-          if (g.Y) {
-            float* yp = g.Y + (size_t)row * g.ldy + col0;
-            *reinterpret_cast<f32x4*>(yp) = v0;
-            *reinterpret_cast<f32x4*>(yp + 4) = v1;
-          }
-          if (g.Yp) {
+        }
+        if (g.Yp) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      if (g.Yp) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int rr = (lane >> 3) + 8 * k;
+          const int row = m0 + wm0 + i * 32 + rr;
+          const int sw = (rr & 1) << 2;
+          f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
+          f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
+          if (row < g.R && row_live(g.rm, row)) {
+            if (!fp32_pass) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v0[e] = fmaf(v0[e], accs, b0[e]) * g.out_scale;
+                v1[e] = fmaf(v1[e], accs, b1[e]) * g.out_scale;
+              }
+            }
             f16x8 h, l;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -445,7 +476,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
               h[e] = a;
               l[e] = c;
             }
-            const size_t off = plane_off(row, col0, g.yrows_pad);
+            const size_t off = plane_off(row, n0 + wn0 + cq, g.yrows_pad);
             *reinterpret_cast<f16x8*>(g.Yp + off) = h;
             *reinterpret_cast<f16x8*>(g.Yp + g.yps + off) = l;
           }
@@ -459,8 +490,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     // Head-major scatter through the same LDS transpose as EPI_STORE.  The wave's 64 columns are
     // one (type t, head) block; GEMM column c holds dim 2c (c < 32) or 2(c - 32) + 1 (c >= 32) (the
     // load-time Wqkv row order puts rotary partners in one lane of the MFMA tile).  Written into
-    // LDS at their natural dim, each lane then owns 8 consecutive dims (4 rotary pairs) of one row:
-    // 16-byte bias / cos / sin loads and 16-byte q and plane stores.
+    // LDS at their natural dim, each lane then owns whole rotary pairs of one row.
     //   self  (EPI_QKV_ROT):   t0 -> q fp32 (rotary), t1 -> k planes (rotary), t2 -> v planes
     //   cross (EPI_CROSS_QKV): t0 -> qk fp32 * scale^0.5 and qk planes,        t1 -> v planes
     const HeadLayout& hl = g.hl;
@@ -481,10 +511,28 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     const int eo = to_kp ? eo_main : to_vp ? eo_v : 0;
     const float so = ldexpf(1.f, -eo);
     float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
-    const int d0 = (lane & 7) * 8;  // the lane's first dim
-    float bd[8];                    // bias in dim order: dim d <- GEMM column (d & 1) * 32 + d / 2
+    // fp32 rows (q, qk) go out as full 128-byte lines per 8 lanes (lane dims c4 .. c4+3 and
+    // 32 + c4 ..: two rotary pairs each); plane rows as one 16-byte chunk per lane (dims d0 ..
+    // d0+7).  qk (cross) needs both: the fp32 pass puts its finished values back into LDS and the
+    // plane pass re-reads them.
+    const bool qpass = to_q, ppass = to_kp || to_vp;
+    const int d0 = (lane & 7) * 8, c4 = (lane & 7) * 4;
+    auto dimA = [&](int e) { return e < 4 ? c4 + e : 32 + c4 + (e - 4); };
+    float bA[8], bB[8];  // bias in dim order: dim d <- GEMM column (d & 1) * 32 + d / 2
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bd[e] = g.bias[cbase + ((d0 + e) & 1) * 32 + ((d0 + e) >> 1)];
+    for (int e = 0; e < 8; ++e) {
+      bA[e] = qpass ? g.bias[cbase + (dimA(e) & 1) * 32 + (dimA(e) >> 1)] : 0.f;
+      bB[e] = ppass && !qpass ? g.bias[cbase + ((d0 + e) & 1) * 32 + ((d0 + e) >> 1)] : 0.f;
+    }
+    // t*cos + rotate_half(t)*sin, rotate_half(x)[2p] = -x[2p+1], [2p+1] = x[2p]; freq p = dim / 2
+    auto rotate = [&](float* x, const float* cs, const float* sn) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float xe = x[2 * p], xo = x[2 * p + 1];
+        x[2 * p] = add_rn(mul_rn(xe, cs[p]), mul_rn(-xo, sn[p]));
+        x[2 * p + 1] = add_rn(mul_rn(xo, cs[p]), mul_rn(xe, sn[p]));
+      }
+    };
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       visit(i, [&](int rr, int c, float v) {
@@ -493,37 +541,67 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         return v;
       });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (qpass) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int rr = (lane >> 3) + 8 * k;
-        const int lr = wm0 + i * 32 + rr;
-        const int row = m0 + lr;
-        const int sw = (rr & 1) << 2;
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (d0 ^ sw));
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((d0 + 4) ^ sw));
-        if (row >= g.R || !row_live(g.rm, row)) continue;
-        float x[8];
+        for (int k = 0; k < 4; ++k) {
+          const int rr = (lane >> 3) + 8 * k;
+          const int lr = wm0 + i * 32 + rr;
+          const int row = m0 + lr;
+          const int sw = (rr & 1) << 2;
+          float* pa = ep + rr * 64 + (c4 ^ sw);
+          float* pb = ep + rr * 64 + ((32 + c4) ^ sw);
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(pa);
+          const f32x4 v1 = *reinterpret_cast<const f32x4*>(pb);
+          if (row >= g.R || !row_live(g.rm, row)) continue;
+          float x[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = fmaf(e < 4 ? v0[e] : v1[e - 4], accs, bd[e]);
-        if (rot) {
-          // t*cos + rotate_half(t)*sin, rotate_half(x)[2p] = -x[2p+1], [2p+1] = x[2p]; freq p = dim / 2
-          const f32x4 c4 = *reinterpret_cast<const f32x4*>(hl.cosb + (size_t)row * kFreq + d0 / 2);
-          const f32x4 s4 = *reinterpret_cast<const f32x4*>(hl.sinb + (size_t)row * kFreq + d0 / 2);
+          for (int e = 0; e < 8; ++e) x[e] = fmaf(e < 4 ? v0[e] : v1[e - 4], accs, bA[e]);
+          if (rot) {
+            const float* cr = hl.cosb + (size_t)row * kFreq;
+            const float* sr = hl.sinb + (size_t)row * kFreq;
+            const f32x2 ca = *reinterpret_cast<const f32x2*>(cr + c4 / 2), cb = *reinterpret_cast<const f32x2*>(cr + 16 + c4 / 2);
+            const f32x2 sa = *reinterpret_cast<const f32x2*>(sr + c4 / 2), sb = *reinterpret_cast<const f32x2*>(sr + 16 + c4 / 2);
+            const float cs[4] = {ca[0], ca[1], cb[0], cb[1]}, sn[4] = {sa[0], sa[1], sb[0], sb[1]};
+            rotate(x, cs, sn);
+          }
 #pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            const float xe = x[2 * p], xo = x[2 * p + 1];
-            x[2 * p] = add_rn(mul_rn(xe, c4[p]), mul_rn(-xo, s4[p]));
-            x[2 * p + 1] = add_rn(mul_rn(xo, c4[p]), mul_rn(xe, s4[p]));
+          for (int e = 0; e < 8; ++e) x[e] *= sc;
+          const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + c4;
+          *reinterpret_cast<f32x4*>(hl.q + off) = f32x4{x[0], x[1], x[2], x[3]};
+          *reinterpret_cast<f32x4*>(hl.q + off + 32) = f32x4{x[4], x[5], x[6], x[7]};
+          if (ppass) {
+            *reinterpret_cast<f32x4*>(pa) = f32x4{x[0], x[1], x[2], x[3]};
+            *reinterpret_cast<f32x4*>(pb) = f32x4{x[4], x[5], x[6], x[7]};
           }
         }
+        if (ppass) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      if (ppass) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] *= sc;
-        const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + d0;
-        if (to_q) {
-          *reinterpret_cast<f32x4*>(hl.q + off) = f32x4{x[0], x[1], x[2], x[3]};
-          *reinterpret_cast<f32x4*>(hl.q + off + 4) = f32x4{x[4], x[5], x[6], x[7]};
-        }
-        if (to_kp || to_vp) {
+        for (int k = 0; k < 4; ++k) {
+          const int rr = (lane >> 3) + 8 * k;
+          const int lr = wm0 + i * 32 + rr;
+          const int row = m0 + lr;
+          const int sw = (rr & 1) << 2;
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (d0 ^ sw));
+          const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((d0 + 4) ^ sw));
+          if (row >= g.R || !row_live(g.rm, row)) continue;
+          float x[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = e < 4 ? v0[e] : v1[e - 4];
+          if (!qpass) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = fmaf(x[e], accs, bB[e]);
+            if (rot) {
+              const f32x4 c4v = *reinterpret_cast<const f32x4*>(hl.cosb + (size_t)row * kFreq + d0 / 2);
+              const f32x4 s4v = *reinterpret_cast<const f32x4*>(hl.sinb + (size_t)row * kFreq + d0 / 2);
+              const float cs[4] = {c4v[0], c4v[1], c4v[2], c4v[3]}, sn[4] = {s4v[0], s4v[1], s4v[2], s4v[3]};
+              rotate(x, cs, sn);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] *= sc;
+          }
+          const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + d0;
           _Float16* base = static_cast<_Float16*>(to_kp ? hl.kp : hl.vp);
           f16x8 h, l;
 #pragma unroll

@@ -14,6 +14,7 @@
 //   filter      one thread per keypoint
 // Ties resolve to the smallest index, as torch-CPU max(dim) does.
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "kernels.h"
@@ -531,6 +532,53 @@ hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st) {
     return hipGetLastError();
   }
   return argmax_and_filter<false>(a.sim, s, a.z0, a.la, B, M, N, a.th, a.m0, a.m1, a.s0, a.s1, st, a.Mb, a.Nb);
+}
+
+// similarity recomputed in two fp16x3 GEMM passes (assign_h3.hip) instead of materialised
+hipError_t assign_and_filter_h3(const AssignArgs& a, const PlaneRef& md, const unsigned* rtab, int slot, hipStream_t st) {
+  const int B = a.B, M = a.M, N = a.N;
+  if (B * M == 0 || B * N == 0 || a.Mb || !sim_h3_supported(M, N)) return hipErrorInvalidValue;
+  const Stats s = carve(a.ws, B, M, N);
+  const int ntm = (M + 255) / 256;
+  float* extra = a.ws + ((assign_workspace_floats(B, M, N) + 63) & ~size_t(63));
+  SimH3Args g;
+  memset(&g, 0, sizeof(g));
+  g.P = md;
+  g.rtab = rtab;
+  g.slot = slot;
+  g.B = B;
+  g.M = M;
+  g.N = N;
+  g.rowp = reinterpret_cast<float2*>(extra);
+  g.pmax = s.pv;
+  g.psum = reinterpret_cast<float*>(s.pi);  // the argmax index partials are not live yet
+  hipError_t e = sim_h3_pass(g, 0, st);
+  if (e != hipSuccess) return e;
+  g.rmax = s.rmax;
+  g.rlog = s.rlog;
+  if ((e = sim_row_stats(g, st)) != hipSuccess) return e;
+  hipLaunchKernelGGL(col_stats_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s.pv, g.psum, ntm, N, B * N,
+                     nullptr, s.cmax, s.clog);
+  hipLaunchKernelGGL(logsig_kernel, dim3((B * M + 255) / 256), dim3(256), 0, st, a.z0, s.ls0, B * M);
+  hipLaunchKernelGGL(logsig_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, a.z1, s.ls1, B * N);
+  if (a.la)
+    hipLaunchKernelGGL(la_last_row_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, a.z1, a.la, B, M, N, nullptr,
+                       nullptr);
+  g.ls0 = s.ls0;
+  g.cmax = s.cmax;
+  g.clog = s.clog;
+  g.ls1 = s.ls1;
+  g.la = a.la;
+  g.rbest = extra;
+  g.rbi = reinterpret_cast<int*>(extra + (size_t)B * M * ((N + 255) / 256));
+  g.pv = s.pv;
+  g.pi = s.pi;
+  if ((e = sim_h3_pass(g, 1, st)) != hipSuccess) return e;
+  if ((e = sim_row_arg(g, a.z0, s.max0, s.arg0, st)) != hipSuccess) return e;
+  hipLaunchKernelGGL(col_arg_combine_kernel, dim3((B * N + 255) / 256), dim3(256), 0, st, s, ntm, N, B * N, nullptr);
+  hipLaunchKernelGGL(filter_kernel, dim3((B * (M + N) + 255) / 256), dim3(256), 0, st, s, B, M, N, a.th, a.m0, a.m1, a.s0,
+                     a.s1, nullptr, nullptr);
+  return hipGetLastError();
 }
 
 hipError_t filter_from_scores(const float* scores, int B, int M, int N, float th, float* ws, int64_t* m0, int64_t* m1,

@@ -1,0 +1,414 @@
+// Dual-softmax assignment with the similarity never materialised (gfx950, fp16x3).
+//
+//   sim = md0 . md1^T                                   lightglue.py:306-315 (MatchAssignment)
+//   la  = log_softmax_j(sim) + log_softmax_i(sim) + logsig(z0_i) + logsig(z1_j)   :284-296
+//   row / column argmax of la, mutual filter            :321-337
+//
+// The [B,M,N] similarity is the product of two 256-wide plane images (the final_proj epilogue
+// writes md as planes, range-scaled so |md| <= 16: the "y" operand of the fp16x3 product).  It is
+// computed twice by the same GEMM tile code -- bit-identical values both times -- instead of being
+// written once and read twice:
+//   pass 1 (stats): per 256x256 tile, each row's (max, sum exp) over the tile's columns and each
+//                   column's over the tile's rows, reduced in registers (DPP / permlane) and LDS
+//   pass 2 (la):    the la value (assign.hip's formula, same operations, same order), written
+//                   once; each row's (max, first argmax) over the tile's columns, each column's
+//                   over the tile's rows
+// Small combine kernels merge the tile partials in tile order (ties keep the first index, as
+// torch-CPU's max), and assign.hip's filter finishes.  HBM traffic per forward: the la write plus
+// the md planes and partials (~0.6 GB at B = 32, N = 2048, against 2.1 GB for sim write + two
+// reads + la write).
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace lg {
+
+namespace {
+constexpr int kSimTile = 256;
+__device__ __forceinline__ int sim_xcd_remap(int id, int n) {
+  const int xcd = id & 7, local = id >> 3;
+  const int base = n >> 3, extra = n & 7;
+  return xcd * base + (xcd < extra ? xcd : extra) + local;
+}
+template <int N>
+__device__ __forceinline__ void sim_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// reductions over the 16 lanes of a DPP row (lanes sharing lane >> 4)
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  return fmaxf(v, dppf<0x140>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  return v + dppf<0x140>(v);
+}
+__device__ __forceinline__ void row16_argmax(float& best, int& bi) {
+  argmax_merge(best, bi, dppf<0xB1>(best), dppi<0xB1>(bi));
+  argmax_merge(best, bi, dppf<0x4E>(best), dppi<0x4E>(bi));
+  argmax_merge(best, bi, dppf<0x141>(best), dppi<0x141>(bi));
+  argmax_merge(best, bi, dppf<0x140>(best), dppi<0x140>(bi));
+}
+// e^x for x <= 0 in the statistics sums: one v_exp_f32 (results below 2^-126 of the max, which
+// cannot move an fp32 sum, flush to zero); expf's denormal / range handling costs ~7x the VALU
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+// (max, sum exp(x - max)) pairs: merge (commutative: both orders round identically)
+template <bool FAST = true>
+__device__ __forceinline__ void lse_merge(float& am, float& as, float bm, float bs) {
+  const float m = fmaxf(am, bm);
+  if (m == -INFINITY) return;
+  const float ea = am == m ? 1.f : (FAST ? fast_exp(am - m) : expf(am - m));
+  const float eb = bm == m ? 1.f : (FAST ? fast_exp(bm - m) : expf(bm - m));
+  as = as * ea + bs * eb;
+  am = m;
+}
+// the same merge with the lanes 16 and 32 apart (the four 16-lane rows of the wave)
+__device__ __forceinline__ void lse_merge_rows(float& m, float& s) {
+  {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    float m0 = __uint_as_float(a[0]), s0 = __uint_as_float(b[0]);
+    lse_merge(m0, s0, __uint_as_float(a[1]), __uint_as_float(b[1]));
+    m = m0;
+    s = s0;
+  }
+  {
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    float m0 = __uint_as_float(a[0]), s0 = __uint_as_float(b[0]);
+    lse_merge(m0, s0, __uint_as_float(a[1]), __uint_as_float(b[1]));
+    m = m0;
+    s = s0;
+  }
+}
+__device__ __forceinline__ void argmax_rows(float& best, int& bi) {
+  {
+    const auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+    const auto i = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
+    float b0 = __uint_as_float(v[0]);
+    int i0 = (int)i[0];
+    argmax_merge(b0, i0, __uint_as_float(v[1]), (int)i[1]);
+    best = b0;
+    bi = i0;
+  }
+  {
+    const auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+    const auto i = __builtin_amdgcn_permlane32_swap((unsigned)bi, (unsigned)bi, false, false);
+    float b0 = __uint_as_float(v[0]);
+    int i0 = (int)i[0];
+    argmax_merge(b0, i0, __uint_as_float(v[1]), (int)i[1]);
+    best = b0;
+    bi = i0;
+  }
+}
+}  // namespace
+
+// 256 x 256 similarity tile, 16 waves of 64 x 64 (16x16x32 f16 MFMAs, three
+// per product), two 64 KiB LDS-DMA stages; MODE 0 = stats pass, 1 = la pass.
+template <int MODE>
+__global__ __launch_bounds__(1024) void sim_h3_kernel(SimH3Args g) {
+  constexpr int BM = kSimTile, BN = kSimTile, BK = kKB, NSTAGE = 2, NW = 16, WGN = 4;
+  constexpr int APT = BM * BK * 2, WPT = BN * BK * 2;
+  constexpr int STAGE_BYTES = 2 * APT + 2 * WPT, PPW = STAGE_BYTES / 1024 / NW;
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm0 = (wave / WGN) * 64, wn0 = (wave % WGN) * 64;
+  const int M = g.M, N = g.N;
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN, T = ntm * ntn;
+  // whole pairs per XCD (workgroups go to XCDs round-robin by linear id): a pair's md rows are
+  // fetched into one L2, not eight; tiles of one pair in row-panel order
+  int b, tile;
+  if (g.B % 8 == 0) {
+    const int id = blockIdx.x, local = id >> 3;
+    b = (id & 7) + 8 * (local / T);
+    tile = local % T;
+  } else {
+    b = blockIdx.x / T;
+    tile = sim_xcd_remap(blockIdx.x % T, T);
+  }
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int arow = b * M + tm * BM, wrow = g.B * M + b * N + tn * BN;  // plane-image rows
+  const float scale = ldexpf(1.f / kLoScale, 2 * range_slot_exp(g.rtab, g.slot));
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)smem);
+  const uint32_t voff = lane * 16;
+  auto issue = [&](int kt, int stage) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;  // [A h | A l | W h | W l], 16 pieces each
+      const int pl = (q >> 4) & 1, pc = q & 15;
+      const int r0 = q < 32 ? arow : wrow;
+      const char* src = reinterpret_cast<const char*>(g.P.p + pl * g.P.ps + ((size_t)kt * g.P.rows_pad + r0) * BK) + pc * 1024;
+      dma16(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto frag = [&](const char* st, int t0, int r, int c) {
+    return *reinterpret_cast<const f16x8*>(st + t0 + r * (BK * 2) + ((c ^ plane_swz(r)) << 4));
+  };
+  const int nk = 256 / BK;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    sim_wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    const char* st = smem + (kt & 1) * STAGE_BYTES;
+    const int c = lane >> 4, r16 = lane & 15;
+    f16x8 ah[4], al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = frag(st, 0, wm0 + i * 16 + r16, c);
+      al[i] = frag(st, APT, wm0 + i * 16 + r16, c);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = wn0 + j * 16 + r16;
+      const f16x8 wh = frag(st, 2 * APT, r, c);
+      const f16x8 wl = frag(st, 2 * APT + WPT, r, c);
+      const f16x8 whs = wh * (_Float16)kLoScale;  // exact: |md_h| <= 16
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] = mfma_h3_16(ah[i], al[i], whs, wl, wh, acc[i][j]);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // lane element (ti, tj, r): pair-local row i0 + 16 ti + 4 (lane >> 4) + r, column j0 + 16 tj + (lane & 15)
+  const int i0 = tm * BM + wm0 + 4 * (lane >> 4), j0 = tn * BN + wn0 + (lane & 15);
+  auto row_of = [&](int ti, int r) { return i0 + 16 * ti + r; };
+  auto col_of = [&](int tj) { return j0 + 16 * tj; };
+  float2* red = reinterpret_cast<float2*>(smem);  // [256 rows][4] row partials, then [4][256] column partials
+  int* redi = reinterpret_cast<int*>(smem + 16384);
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[ti][tj][r] = (row_of(ti, r) < M && col_of(tj) < N) ? acc[ti][tj][r] * scale : -INFINITY;
+    // rows: the wave's 64 columns (lane-local over tj, then the 16 lanes of the row)
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float m = fmaxf(fmaxf(acc[ti][0][r], acc[ti][1][r]), fmaxf(acc[ti][2][r], acc[ti][3][r]));
+        m = row16_max(m);
+        float s = 0.f;
+        if (m != -INFINITY)
+#pragma unroll
+          for (int tj = 0; tj < 4; ++tj) s += fast_exp(acc[ti][tj][r] - m);
+        s = row16_sum(s);
+        if ((lane & 15) == 0) red[(wm0 + 16 * ti + 4 * (lane >> 4) + r) * 4 + (wave % WGN)] = make_float2(m, s);
+      }
+    // columns: the wave's 64 rows (lane-local over ti, r, then the four 16-lane rows); the column
+    // table lies beside the row table, so no barrier in between
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m = fmaxf(m, acc[ti][tj][r]);
+      float s = 0.f;
+      if (m != -INFINITY)
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s += fast_exp(acc[ti][tj][r] - m);
+      lse_merge_rows(m, s);
+      if (lane < 16) red[1024 + (wave / WGN) * 256 + wn0 + 16 * tj + lane] = make_float2(m, s);
+    }
+    __syncthreads();
+    if (tid < 256) {
+      const int i = tm * BM + tid;
+      float m = red[tid * 4].x, s = red[tid * 4].y;
+      for (int w = 1; w < 4; ++w) lse_merge(m, s, red[tid * 4 + w].x, red[tid * 4 + w].y);
+      if (i < M) g.rowp[((size_t)b * M + i) * ntn + tn] = make_float2(m, s);
+    } else if (tid < 512) {
+      const int cl = tid - 256, j = tn * BN + cl;
+      float m = red[1024 + cl].x, s = red[1024 + cl].y;
+      for (int w = 1; w < 4; ++w) lse_merge(m, s, red[1024 + w * 256 + cl].x, red[1024 + w * 256 + cl].y);
+      if (j < N) {
+        g.pmax[((size_t)b * ntm + tm) * N + j] = m;
+        g.psum[((size_t)b * ntm + tm) * N + j] = s;
+      }
+    }
+  } else {
+    // la value: assign.hip score_at<false> (same operations, same order); the row statistics are
+    // loaded per 16-row block, just before use (register pressure)
+    float cm[4], cl[4], l1[4];
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) {
+      const int j = min(col_of(tj), N - 1);
+      cm[tj] = g.cmax[(size_t)b * N + j];
+      cl[tj] = g.clog[(size_t)b * N + j];
+      l1[tj] = g.ls1[(size_t)b * N + j];
+    }
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = min(row_of(ti, r), M - 1);
+        const float rm = g.rmax[(size_t)b * M + i], rl = g.rlog[(size_t)b * M + i], l0 = g.ls0[(size_t)b * M + i];
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj) {
+          const float x = acc[ti][tj][r] * scale;
+          const float s0 = (x - rm) - rl;
+          const float s1 = (x - cm[tj]) - cl[tj];
+          const float v = (s0 + s1) + (l0 + l1[tj]);
+          acc[ti][tj][r] = (row_of(ti, r) < M && col_of(tj) < N) ? v : -INFINITY;
+        }
+      }
+    // la write: 32-row passes through a per-wave LDS transpose, one 256-byte row run per store
+    if (g.la) {
+      float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int rr = a * 16 + 4 * (lane >> 4) + r, c = 16 * tj + (lane & 15);
+              ep[rr * 64 + (c ^ ((rr & 1) << 2))] = acc[2 * p + a][tj][r];
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int j = tn * BN + wn0 + lane;
+#pragma unroll 4
+        for (int rr = 0; rr < 32; ++rr) {
+          const int i = tm * BM + wm0 + 32 * p + rr;
+          const float v = ep[rr * 64 + (lane ^ ((rr & 1) << 2))];
+          if (i < M && j < N) g.la[((size_t)b * (M + 1) + i) * (N + 1) + j] = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();  // the transpose buffers become the argmax tables
+    float* redf = reinterpret_cast<float*>(smem);
+    // row argmax over the wave's columns (first index on ties) -> table [256 rows][4]
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float best = acc[ti][0][r];
+        int bi = col_of(0);
+#pragma unroll
+        for (int tj = 1; tj < 4; ++tj) argmax_merge(best, bi, acc[ti][tj][r], col_of(tj));
+        row16_argmax(best, bi);
+        if ((lane & 15) == 0) {
+          const int lr = wm0 + 16 * ti + 4 * (lane >> 4) + r;
+          redf[lr * 4 + (wave % WGN)] = best;
+          redi[lr * 4 + (wave % WGN)] = bi;
+        }
+      }
+    // column argmax over the wave's rows -> table [4][256 columns]
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) {
+      float best = acc[0][tj][0];
+      int bi = row_of(0, 0);
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) argmax_merge(best, bi, acc[ti][tj][r], row_of(ti, r));
+      argmax_rows(best, bi);
+      if (lane < 16) {
+        const int lc = wn0 + 16 * tj + lane;
+        redf[1024 + (wave / WGN) * 256 + lc] = best;
+        redi[1024 + (wave / WGN) * 256 + lc] = bi;
+      }
+    }
+    __syncthreads();
+    if (tid < 256) {
+      const int i = tm * BM + tid;
+      float best = redf[tid * 4];
+      int bi = redi[tid * 4];
+      for (int w = 1; w < 4; ++w) argmax_merge(best, bi, redf[tid * 4 + w], redi[tid * 4 + w]);
+      if (i < M) {
+        g.rbest[((size_t)b * M + i) * ntn + tn] = best;
+        g.rbi[((size_t)b * M + i) * ntn + tn] = bi;
+      }
+    } else if (tid < 512) {
+      const int lc = tid - 256, j = tn * BN + lc;
+      float best = redf[1024 + lc];
+      int bi = redi[1024 + lc];
+      for (int w = 1; w < 4; ++w) argmax_merge(best, bi, redf[1024 + w * 256 + lc], redi[1024 + w * 256 + lc]);
+      if (j < N) {
+        g.pv[((size_t)b * ntm + tm) * N + j] = best;
+        g.pi[((size_t)b * ntm + tm) * N + j] = bi;
+      }
+    }
+  }
+}
+
+// rows: merge the ntn tile partials in column order
+__global__ void sim_row_stats_kernel(const float2* rowp, int BM, int ntn, float* rmax, float* rlog) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= BM) return;
+  float m = rowp[(size_t)t * ntn].x, s = rowp[(size_t)t * ntn].y;
+  for (int k = 1; k < ntn; ++k) lse_merge<false>(m, s, rowp[(size_t)t * ntn + k].x, rowp[(size_t)t * ntn + k].y);
+  rmax[t] = m;
+  rlog[t] = logf(s);
+}
+// rows: first argmax over the tile partials in column order (strictly greater wins); la dustbin
+__global__ void sim_row_arg_kernel(const float* rbest, const int* rbi, int B, int M, int N, int ntn, const float* z0,
+                                   float* max0, int* arg0, float* la) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * M) return;
+  float best = rbest[(size_t)t * ntn];
+  int bi = rbi[(size_t)t * ntn];
+  for (int k = 1; k < ntn; ++k) {
+    const float v = rbest[(size_t)t * ntn + k];
+    if (v > best) {
+      best = v;
+      bi = rbi[(size_t)t * ntn + k];
+    }
+  }
+  max0[t] = best;
+  arg0[t] = bi;
+  if (la) {
+    const int b = t / M, i = t - b * M;
+    la[((size_t)b * (M + 1) + i) * (N + 1) + N] = log_sigmoid(-z0[t]);
+  }
+}
+
+bool sim_h3_supported(int M, int N) { return M % 16 == 0 && N % 16 == 0 && !getenv("LG_ASSIGN_SIM_X6"); }
+size_t sim_h3_workspace_floats(int B, int M, int N) { return 2 * (size_t)B * M * ((N + kSimTile - 1) / kSimTile) + 64; }
+
+hipError_t sim_h3_pass(const SimH3Args& a, int mode, hipStream_t st) {
+  const int ntm = (a.M + kSimTile - 1) / kSimTile, ntn = (a.N + kSimTile - 1) / kSimTile;
+  if (a.M % 16 || a.N % 16 || a.P.rows_pad < a.B * (a.M + a.N) + kSimTile) return hipErrorInvalidValue;
+  const dim3 grid(ntm * ntn * a.B), block(1024);
+  if (mode == 0) hipLaunchKernelGGL(sim_h3_kernel<0>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(sim_h3_kernel<1>, grid, block, 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t sim_row_stats(const SimH3Args& a, hipStream_t st) {
+  const int ntn = (a.N + kSimTile - 1) / kSimTile, BM = a.B * a.M;
+  hipLaunchKernelGGL(sim_row_stats_kernel, dim3((BM + 255) / 256), dim3(256), 0, st, a.rowp, BM, ntn,
+                     const_cast<float*>(a.rmax), const_cast<float*>(a.rlog));
+  return hipGetLastError();
+}
+
+hipError_t sim_row_arg(const SimH3Args& a, const float* z0, float* max0, int* arg0, hipStream_t st) {
+  const int ntn = (a.N + kSimTile - 1) / kSimTile, BM = a.B * a.M;
+  hipLaunchKernelGGL(sim_row_arg_kernel, dim3((BM + 255) / 256), dim3(256), 0, st, a.rbest, a.rbi, a.B, a.M, a.N, ntn, z0,
+                     max0, arg0, a.la);
+  return hipGetLastError();
+}
+
+}  // namespace lg

@@ -218,9 +218,10 @@ __device__ __forceinline__ int range_exponent(const RO& r) {
   float b = r.add;
   if (r.in0 >= 0) b += r.g0 * range_max(r.tab, r.in0);
   if (r.in1 >= 0) b += r.g1 * range_max(r.tab, r.in1);
-  if (!(b > kRangeLimit) || !(b <= 3.0e38f)) return 0;  // in range, or non-finite data
+  const float lim = ldexpf(kRangeLimit, -r.lshift);
+  if (!(b > lim) || !(b <= 3.0e38f)) return 0;  // in range, or non-finite data
   int E;
-  (void)frexpf(b * (1.f / kRangeLimit), &E);  // b / 2^15 = m 2^E, m in [0.5, 1)  ->  2^E >= it
+  (void)frexpf(b / lim, &E);  // b / lim = m 2^E, m in [0.5, 1)  ->  2^E >= it
   return E;
 }
 __device__ __forceinline__ int range_slot_exp(const unsigned* tab, int slot) {

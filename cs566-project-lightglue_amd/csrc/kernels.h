@@ -73,6 +73,8 @@ struct RangeOut {
   float g0, g1, add;
   int out;
   int track;          // 1: record M[out] (only the residual stream's images need it; E is always kept)
+  int lshift;         // the bound is held to 2^(15 - lshift): 11 for images used as the "y" operand
+                      // of an fp16x3 product (|y| <= 16, so y_h * 2^11 stays finite)
 };
 inline RangeOut range_none() { return RangeOut{nullptr, -1, -1, 0.f, 0.f, 0.f, 0, 0}; }
 
@@ -219,6 +221,30 @@ struct AssignArgs {
 };
 size_t assign_workspace_floats(int B, int M, int N);
 hipError_t assign_and_filter(const AssignArgs& a, hipStream_t st);
+// The same with the similarity recomputed inside two fp16x3 GEMM passes instead of materialised
+// (assign_h3.hip): P = plane image of md (rows: image 0 rows of pair b at b*M, image 1 rows at
+// B*M + b*N; |md| <= 16 after its range exponent E[slot]), rows_pad >= B*(M+N) + 256, M and N
+// multiples of 16, no per-pair counts.  a.sim is not read; a.ws needs assign_workspace_floats +
+// sim_h3_workspace_floats.
+struct SimH3Args {
+  PlaneRef P;
+  const unsigned* rtab;
+  int slot;
+  int B, M, N;
+  float2* rowp;                       // stats pass: [B][M][ntn] (max, sum) per column tile
+  float* pmax; float* psum;           //             [B][ntm][N] per row tile
+  const float* rmax; const float* rlog; const float* ls0;  // la pass inputs [B*M]
+  const float* cmax; const float* clog; const float* ls1;  //               [B*N]
+  float* la;                          // [B][M+1][N+1] or null
+  float* rbest; int* rbi;             // la pass: [B][M][ntn] row argmax per column tile
+  float* pv; int* pi;                 //          [B][ntm][N] column argmax per row tile
+};
+bool sim_h3_supported(int M, int N);
+size_t sim_h3_workspace_floats(int B, int M, int N);
+hipError_t sim_h3_pass(const SimH3Args& a, int mode, hipStream_t st);
+hipError_t sim_row_stats(const SimH3Args& a, hipStream_t st);
+hipError_t sim_row_arg(const SimH3Args& a, const float* z0, float* max0, int* arg0, hipStream_t st);
+hipError_t assign_and_filter_h3(const AssignArgs& a, const PlaneRef& md, const unsigned* rtab, int slot, hipStream_t st);
 // filter_matches on an existing [B][M+1][N+1] log-assignment.
 hipError_t filter_from_scores(const float* scores, int B, int M, int N, float th, float* ws, int64_t* m0, int64_t* m1,
                               float* s0, float* s1, hipStream_t st);

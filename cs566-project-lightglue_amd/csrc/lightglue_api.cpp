@@ -149,6 +149,7 @@ struct lg_handle {
   };
   std::vector<BlockGain> gains;  // [layer * 2 + block]
   float gi = 0.f, bi_max = 0.f;  // input_proj
+  std::vector<float> gf, bf_max;  // per layer: final_proj row-L1 max / |bias| max (md range bound)
   bool loaded = false;
   bool pass_started = false;  // forward_pass got past argument checks (work was enqueued)
   // fold out_proj / to_out into ffn.0 at load time (env LG_FOLD_OUT_PROJ=0 disables)
@@ -304,6 +305,7 @@ struct Work {
   // PREC_H3 plane images (common.h), rows_pad rows: x, context, message (unfolded out_proj),
   // FFN hidden, input descriptors (input_dim != 256)
   _Float16 *Xp, *Cp, *Mp, *Hp, *Dp;
+  _Float16* mdp;  // md = final_proj(x) / 4 as a plane image (rows_pad + 256 rows) for the fused assignment
   float* Dst;
   int rows_pad;
   size_t R;
@@ -346,10 +348,11 @@ Work carve(char* base, int B, int M, int N, bool prune, int din) {
   w.Dp = din != D ? th(2 * RP * din) : nullptr;
   w.Dst = din != D ? tf(R * din) : nullptr;  // staging for 16-byte-unaligned input descriptors
   w.md = tf(R * D);
+  w.mdp = th(2 * (RP + 256) * D);
   w.z = tf(R);
   w.tok = tf(R);
   w.sim = tf((size_t)B * M * N);
-  w.aws = tf(lg::assign_workspace_floats(B, M, N));
+  w.aws = tf(lg::assign_workspace_floats(B, M, N) + 64 + lg::sim_h3_workspace_floats(B, M, N));
   w.rtab = reinterpret_cast<unsigned*>(ti(kRangeSlots * lg::kRangeStride));
   if (prune) {
     w.X2 = tf(R * D);
@@ -581,6 +584,21 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
     }
     h->gi = hs[nf - 2];
     h->bi_max = hs[nf - 1];
+    // final_proj of every layer (the md plane image of the fused assignment)
+    float* fst = nullptr;
+    LG_HIP(hipMallocAsync((void**)&fst, 2 * L * sizeof(float), st));
+    for (int i = 0; i < L; ++i)
+      LG_HIP(lg::weight_range_stats(W + h->layers[i].Wf, D, D, W + h->layers[i].bf, fst + 2 * i, st));
+    std::vector<float> fs(2 * L);
+    LG_HIP(hipMemcpyAsync(fs.data(), fst, 2 * L * sizeof(float), hipMemcpyDeviceToHost, st));
+    LG_HIP(hipStreamSynchronize(st));
+    LG_HIP(hipFreeAsync(fst, st));
+    h->gf.resize(L);
+    h->bf_max.resize(L);
+    for (int i = 0; i < L; ++i) {
+      h->gf[i] = fs[2 * i];
+      h->bf_max[i] = fs[2 * i + 1];
+    }
   }
   h->loaded = true;
   return LG_OK;
@@ -912,6 +930,11 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   // ---- assignment head of each pair's last executed layer (lightglue.py:549-551,
   // MatchAssignment :306-315): one final_proj / matchability launch per layer a pair may have
   // stopped at (rows of the other pairs are masked out)
+  // fused assignment (assign_h3.hip): the similarity is recomputed from md's plane image, held
+  // to |md| <= 16 (the "y" side of the fp16x3 product), instead of a bf16x6 GEMM into w.sim
+  const bool fused_sim = prec == PREC_H3 && !seg && sim_h3_supported(M, N);
+  const int md_rows_pad = RP + 256;
+  const int s_md = fused_sim ? slot() : -1;
   auto head = [&](int li, const RowMask& m) -> int {
     const LayerW& la = h->layers[li];
     if (prec == PREC_H3) {
@@ -919,6 +942,11 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, la.Wf); g.bias = Wb + la.bf;
       g.rtab = rt; g.a0_slot = s_x; g.rm = m;
       g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f;  // / d**0.25
+      if (fused_sim) {
+        g.Y = nullptr;
+        g.Yp = w.mdp; g.yps = (long long)md_rows_pad * D; g.yrows_pad = md_rows_pad;
+        g.ro = RangeOut{rt, s_x, -1, 0.25f * h->gf[li], 0.f, 0.25f * h->bf_max[li], s_md, 0, 11};
+      }
       LG_HIP(gemmh(g, EPI_STORE));
     } else {
       GemmArgs g = gemm_base();
@@ -938,7 +966,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     const int rc = head(L - 1, seg ? RowMask{cnt, nullptr, 0, SL} : RowMask{});
     if (rc != LG_OK) return rc;
   }
-  {
+  if (!fused_sim) {
     // similarity: both operands are run-time values -> bf16x6 (full fp32 range); per pair over
     // the slot capacities (the assignment bounds everything by the kept counts)
     GemmArgs g = gemm_base();
@@ -976,7 +1004,14 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
                      out->matching_scores1, st));
   } else {
     aa.m0 = out->matches0; aa.m1 = out->matches1; aa.s0 = out->matching_scores0; aa.s1 = out->matching_scores1;
-    LG_HIP(assign(aa));
+    if (fused_sim) {
+      const int p = h->prof_begin(LG_KERNEL_ASSIGN, st);
+      LG_HIP(assign_and_filter_h3(aa, PlaneRef{w.mdp, (long long)md_rows_pad * D, md_rows_pad}, rt, s_md, st));
+      // two similarity GEMMs; HBM: the la write (the similarity is never stored)
+      h->prof_end(p, 2.0 * 2.0 * B * M * N * D, aa.la ? 4.0 * B * (M + 1) * (N + 1) : 0.0, st);
+    } else {
+      LG_HIP(assign(aa));
+    }
   }
   if (out->ref_descriptors0)
     LG_HIP(hipMemcpyAsync(out->ref_descriptors0, w.X, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));

@@ -118,19 +118,23 @@ def test_forward_matches_reference_golden(name, precision):
     check_against_golden(pred, g, f"{name}/{precision}")
 
 
-@pytest.mark.parametrize("tile,waves,assign,kernel", [("big", "8", "fused", "h3g"), ("small", "4", "fused", "h3m"),
-                                                       ("small", "2", "unfused", "h3g"), ("big", "2", "fused", "h3m")])
+@pytest.mark.parametrize("tile,waves,assign,kernel", [("big", "8", "sim_h3", "h3g"), ("small", "4", "x6_fused", "h3m"),
+                                                       ("small", "2", "x6_unfused", "h3g"), ("big", "2", "sim_h3", "h3m")])
 @pytest.mark.parametrize("name", case_names())
 def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, monkeypatch):
     """The fp16x3 GEMM picks 256x256 tiles (throughput) or 64x64 tiles (fewer big tiles than CUs,
     e.g. B = 1) by row count, and the attention 8, 4 or 2 waves (256/128/64 queries) per
-    workgroup, and the assignment its two-read fused passes (N % 4 == 0, N <= 2048) or the
-    four-read ones; LG_GEMM_TILE / LG_ATTN_WAVES / LG_ASSIGN_UNFUSED force each so that every
-    launch shape is checked against the reference on every golden case."""
+    workgroup, and the assignment either recomputes the similarity inside two fp16x3 GEMM passes
+    (M, N multiples of 16, no pruning: sim_h3) or materialises it with the bf16x6 GEMM and runs
+    the two-read fused passes (N % 4 == 0, N <= 2048) or the four-read ones; LG_GEMM_TILE /
+    LG_ATTN_WAVES / LG_ASSIGN_SIM_X6 / LG_ASSIGN_UNFUSED force each so that every launch shape is
+    checked against the reference on every golden case."""
     monkeypatch.setenv("LG_GEMM_TILE", tile)
     monkeypatch.setenv("LG_ATTN_WAVES", waves)
     monkeypatch.setenv("LG_ATTN_KERNEL", kernel)  # fp16x3 attention: 16x16x32 (h3g) / 32x32x16 (h3m) MFMAs
-    if assign == "unfused":  # the four-read assignment path (N % 4 != 0 or N > 2048)
+    if assign != "sim_h3":  # the materialised bf16x6 similarity
+        monkeypatch.setenv("LG_ASSIGN_SIM_X6", "1")
+    if assign == "x6_unfused":  # its four-read assignment passes (N % 4 != 0 or N > 2048)
         monkeypatch.setenv("LG_ASSIGN_UNFUSED", "1")
     g = load(name)
     conf, sd, data = case_inputs(g["meta"])

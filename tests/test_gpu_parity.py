@@ -604,3 +604,23 @@ def test_configs3_batched_pruning_equals_golden():
         np.testing.assert_array_equal(m1[b], g["matches1"][0][perm], err_msg=f"pair {b}")
         np.testing.assert_array_equal(p0[b], g["prune0"][0], err_msg=f"pair {b}")
         np.testing.assert_array_equal(p1[b], g["prune1"][0][perm], err_msg=f"pair {b}")
+
+
+def test_compile_replays_hip_graphs():
+    """compile(): the first forward of a signature is captured into a hipGraph, later ones replay
+    it on fresh inputs -- identical to eager forwards; a new shape captures a new graph."""
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1}
+    sd = synthetic_state_dict(conf, seed=0)
+    eager = _model(conf, sd, "auto")
+    graphed = _model(conf, sd, "auto").compile()
+    for M, N, seed in ((256, 230, 1), (256, 230, 2), (256, 230, 3), (192, 200, 4)):
+        data = _gpu_data(synthetic_pair(B=2, M=M, N=N, seed=seed))
+        with torch.no_grad():
+            ref = eager(data)
+            got = graphed(data)
+        torch.cuda.synchronize()
+        for k in ("matches0", "matches1", "matching_scores0", "matching_scores1", "log_assignment"):
+            assert torch.equal(got[k], ref[k]), (k, M, N, seed)
+    assert len(graphed._graphs) == 2

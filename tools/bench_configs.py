@@ -55,8 +55,12 @@ def cfg1(dev, reps):
     data = gpu_pairs(1, 1024, 256, seed=1, device=dev)
     with torch.no_grad():
         s, pred = timed(lambda: m(data), reps)
+        mg = model_for({"filter_threshold": 0.1}, dev).compile()  # HIP-graph replay
+        sg, pg = timed(lambda: mg(data), reps)
+    assert torch.equal(pg["matches0"], pred["matches0"])
     return {"config": "configs[1]: synthetic N=1024 d=256, 9 layers, batch=1, 1 GPU", "value": round(1 / s, 2),
             "unit": "image-pairs/s", "ms_per_pair": round(1e3 * s, 3),
+            "graph_replay_pairs_per_s": round(1 / sg, 2), "graph_replay_ms_per_pair": round(1e3 * sg, 3),
             "matches": int((pred["matches0"] > -1).sum())}
 
 

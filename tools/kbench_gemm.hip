@@ -103,7 +103,8 @@ __global__ void ref64(const float* A, const float* W, const float* bias, double*
 }
 
 int main() {
-  const Shape shapes[] = {{131072, 256, 768, "qkv"}, {131072, 512, 512, "ffn1"}, {131072, 512, 256, "ffn2"}, {131072, 256, 256, "outp"}};
+  const Shape shapes[] = {{131072, 32, 768, "k32"}, {131072, 256, 768, "qkv"}, {131072, 512, 512, "ffn1"},
+                          {131072, 512, 256, "ffn2"}, {131072, 256, 256, "outp"}};
   const int RR = 512;  // rows checked against fp64
   for (const Shape& s : shapes) {
     float *A, *W, *bias, *Y;

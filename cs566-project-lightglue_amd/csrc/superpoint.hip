@@ -17,6 +17,8 @@
 // only the pooled map is written.
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "kernels.h"
@@ -47,8 +49,11 @@ unsigned grid_for(long long n, int block, int cap = 8192) {
 }  // namespace
 
 // ---- gray + conv1a -------------------------------------------------------------------------
-// superpoint.py:204-209.  One thread per pixel: the 3x3 gray neighbourhood (zero padded) in
-// registers, 64 output channels in 8 chunks of 8 -> ReLU -> fp16x3 planes (16-byte stores).
+// superpoint.py:204-209.  Four threads per pixel (thread c of a pixel owns the 16-byte chunk c of
+// both 32-channel blocks, channels 8c..8c+7 and 32+8c..32+8c+7): the 3x3 gray neighbourhood
+// (zero padded) in registers -> ReLU -> fp16x3 planes.  A wave's store covers 16 consecutive
+// 64-byte rows = 1 KiB contiguous (one thread per pixel with 16-byte stores at a 64-byte stride
+// wrote each line in four partial pieces and ran at half the store rate).
 __global__ __launch_bounds__(256) void sp_conv1a_kernel(const float* __restrict__ img, int B, int C, int H, int W,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         _Float16* Y, int yrows_pad, RangeOut ro) {
@@ -59,15 +64,17 @@ __global__ __launch_bounds__(256) void sp_conv1a_kernel(const float* __restrict_
   const float so = ldexpf(1.f, -eo);
   const long long yps = (long long)yrows_pad * 64;
   float wmax = 0.f;
-  const long long HW = (long long)H * W, total = (long long)B * HW;
-  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (long long)gridDim.x * blockDim.x) {
+  const long long HW = (long long)H * W, total = (long long)B * HW * 4;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const long long p = t >> 2;
+    const int c = (int)(t & 3);
     const int n = (int)(p / HW);
     const int rem = (int)(p - (long long)n * HW);
     const int y = rem / W, x = rem - y * W;
     float g[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+    for (int k = 0; k < 9; ++k) {
+      const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
       float v = 0.f;
       if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
         const size_t o = (size_t)yy * W + xx;
@@ -78,17 +85,17 @@ __global__ __launch_bounds__(256) void sp_conv1a_kernel(const float* __restrict_
           v = img[(size_t)n * HW + o];
         }
       }
-      g[t] = v;
+      g[k] = v;
     }
-#pragma unroll 1
-    for (int c8 = 0; c8 < 8; ++c8) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
       f16x8 h, l;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int co = c8 * 8 + e;
+        const int co = kb * 32 + c * 8 + e;
         float a = 0.f;
 #pragma unroll
-        for (int t = 0; t < 9; ++t) a = fmaf(wsh[co * 9 + t], g[t], a);
+        for (int k = 0; k < 9; ++k) a = fmaf(wsh[co * 9 + k], g[k], a);
         const float v = fmaxf(a + wsh[64 * 9 + co], 0.f);
         wmax = fmaxf(wmax, v);
         _Float16 hh, ll;
@@ -96,7 +103,7 @@ __global__ __launch_bounds__(256) void sp_conv1a_kernel(const float* __restrict_
         h[e] = hh;
         l[e] = ll;
       }
-      const size_t off = plane_off((int)p, c8 * 8, yrows_pad);
+      const size_t off = plane_off((int)p, kb * 32 + c * 8, yrows_pad);
       *reinterpret_cast<f16x8*>(Y + off) = h;
       *reinterpret_cast<f16x8*>(Y + yps + off) = l;
     }
@@ -108,7 +115,7 @@ hipError_t sp_conv1a(const float* image, int B, int C, int H, int W, const float
                      int yrows_pad, const RangeOut& ro, hipStream_t st) {
   if (B <= 0 || H <= 0 || W <= 0) return hipSuccess;
   if ((C != 1 && C != 3) || (long long)yrows_pad < (long long)B * H * W) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sp_conv1a_kernel, dim3(grid_for((long long)B * H * W, 256, 4096)), dim3(256), 0, st, image, B, C,
+  hipLaunchKernelGGL(sp_conv1a_kernel, dim3(grid_for(4LL * B * H * W, 256, 8192)), dim3(256), 0, st, image, B, C,
                      H, W, w, bias, Y, yrows_pad, ro);
   return hipGetLastError();
 }
@@ -316,6 +323,312 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64) void sp_conv3x3_kernel(ConvH3Ar
   range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem));
 }
 
+// ---- 3x3 convolution with a halo tile per channel block (the production form) -------------
+// Output tile = 16 x 16 pixels of one image (GEMM rows in quad order, as above) x BN channels.
+// Per 32-channel block the (16+2) x (16+2) input halo is gathered ONCE into LDS by LDS-DMA
+// (384 rows x 64 B per plane; rows past 324 and taps outside the image read the zero row) and
+// the nine taps read their A fragments from it at a shifted row (halo row (py + ky) * 18 + px + kx):
+// per k-step the CU loads the BN x 32 weight tile plus 1/9 of a halo, ~3x less than re-gathering
+// 256 shifted rows per tap.
+// Persistent: one workgroup per CU walks its tiles (each XCD a contiguous range, so the tiles in
+// flight on one L2 are neighbours), and the step sequence (tile, channel block, tap) runs through
+// one pipeline: weights two steps ahead (ring of 3), the next halo -- next channel block or the
+// next tile's first -- issued at tap 0 into the other of two halo buffers (nine steps of lead),
+// so neither a tile's start nor a block boundary waits on HBM.  Waves of 32 x 64 (8 per 64
+// channels: two or four waves per SIMD hide each other's LDS reads).  Measured and not kept:
+// fragments read a step ahead into a second register set (4-deep weight ring) -- the compiler
+// copies the set every step and conv1b ran 10 % slower.  The epilogue transposes through
+// the halo buffer just consumed.  vmcnt waits count only the loads issued after the one needed
+// (the LDS-DMA loads return in order; epilogue stores can only make a wait longer).
+constexpr int kHT = 16, kHH = kHT + 2, kHRows = 384;
+// Halo layout in LDS: pixel (y, x) of the 18 x 18 halo at layout row halo_row(y, x) (< 360), its
+// 16-byte chunk c at slot halo_pos(x, c) of that row.  Chosen so the A-fragment reads are
+// conflict-free for every tap: a ds_read_b128 lane group reads 8 consecutive pixels of two
+// adjacent halo rows with two chunk values, and bank slot 4 * (row mod 4) + pos = (2x + (c & 1)
+// + 8 (y & 1)) mod 16 (up to a per-group constant) is distinct over those 16 -- the linear
+// layout (row 18 y + x) hit 3-way conflicts.  Rows: 20 per halo row, (x >> 1) + 2 (y & 1) fixes
+// the row residue; x = 16, 17 use the spare slots of rows y and y +- 1.
+__device__ __forceinline__ int halo_row(int y, int x) {
+  const int a = x >> 1, b = x & 1, p = y & 1;
+  if (x < 16) return 20 * y + 4 * (2 * (a >> 2) + b) + ((a + 2 * p) & 3);
+  return 20 * (y + (b ? (p ? -1 : 1) : 0)) + 16 + 2 * p;
+}
+__device__ __forceinline__ int halo_pos(int x, int c) { return (2 * (x & 1) + (c & 1)) ^ (c & 2); }
+// inverse: the pixel and chunk stored at (layout row lr, slot s); false for unused slots
+__device__ __forceinline__ bool halo_inv(int lr, int s, int& y, int& x, int& c) {
+  if (lr >= 20 * kHH) return false;
+  const int y0 = lr / 20, off = lr - 20 * y0, k = off >> 2, r = off & 3, p = y0 & 1;
+  if (k < 4) {
+    y = y0;
+    x = 2 * (4 * (k >> 1) + ((r - 2 * p) & 3)) + (k & 1);
+  } else if (r == 2 * p) {
+    y = y0;
+    x = 16;
+  } else if (r == 2 - 2 * p) {  // x = 17 of the neighbouring row
+    y = p ? y0 - 1 : y0 + 1;
+    x = 17;
+  } else {
+    return false;
+  }
+  c = 2 * (((s >> 1) ^ x) & 1) + (s & 1);
+  return true;
+}
+template <int BN, bool POOL>
+__global__ __launch_bounds__(8 * (BN / 64) * 64) void sp_conv3x3_halo_kernel(ConvH3Args g) {
+  constexpr int BK = kKB, WGN = BN / 64, NW = 8 * WGN, WM = 32, WMT = WM / 16;
+  constexpr int HALO_PLANE = kHRows * BK * 2, HALO_BYTES = 2 * HALO_PLANE;
+  constexpr int WPT = BN * BK * 2, WSTAGE = 2 * WPT, NSW = 3;
+  constexpr int PH = HALO_BYTES / 1024 / NW, PW = WSTAGE / 1024 / NW;
+  constexpr int EPR = NW == 8 ? 16 : 8;  // epilogue rows per pass (per-wave scratch EPR x 64 fp32)
+  static_assert((HALO_BYTES / 1024) % NW == 0 && (WSTAGE / 1024) % NW == 0, "pieces per wave");
+  static_assert(NW * EPR * 64 * 4 <= HALO_BYTES, "epilogue scratch");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * HALO_BYTES + NSW * WSTAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm0 = (wave / WGN) * WM, wn0 = (wave % WGN) * 64;
+  const int H = g.H, W = g.W, Hp = H >> 1, Wp = W >> 1;
+  const int tiles_x = (W + kHT - 1) / kHT, tiles_y = (H + kHT - 1) / kHT;
+  const int num_n = g.Cout / BN, ntiles = g.B * tiles_y * tiles_x * num_n;
+  // this workgroup's tiles: t_begin + local + k * nx (workgroups go to XCDs round-robin)
+  const int G = min(8, (int)gridDim.x);  // tile ranges (XCDs in use)
+  const int xcd = blockIdx.x % G, local = blockIdx.x / G, nx = ((int)gridDim.x - xcd + G - 1) / G;
+  const int t_begin = (int)((long long)ntiles * xcd / G), t_end = (int)((long long)ntiles * (xcd + 1) / G);
+  const int T = local < t_end - t_begin ? (t_end - t_begin - local + nx - 1) / nx : 0;
+  if (T == 0) return;  // workgroup-uniform
+  const int CB = g.Cin / BK, nsteps = 9 * CB, S = T * nsteps, GCB = T * CB;
+  const float accs = ldexpf(g.acc_scale, range_slot_exp(g.rtab, g.x_slot));
+  const int eo = range_exponent(g.ro);
+  const int zrow = g.X.rows_pad - 1;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)smem);
+
+  struct Tile {
+    int n, y0, x0, n0;
+  };
+  auto decode = [&](int k) {
+    const int tile = t_begin + local + k * nx;
+    const int tm = tile / num_n, tn = tile - tm * num_n;
+    const int n = tm / (tiles_y * tiles_x), trem = tm - n * tiles_y * tiles_x;
+    return Tile{n, (trem / tiles_x) * kHT, (trem % tiles_x) * kHT, tn * BN};
+  };
+  auto issue_halo = [&](const Tile& t, int cb, int buf) {
+#pragma unroll
+    for (int i = 0; i < PH; ++i) {
+      const int q = wave * PH + i;  // wave-uniform piece: 16 layout rows of one plane
+      const int pl = q / (kHRows / 16);
+      const int lr = (q % (kHRows / 16)) * 16 + (lane >> 2);
+      int hy = 0, hx = 0, c = 0;
+      const bool used = halo_inv(lr, lane & 3, hy, hx, c);
+      const int yy = t.y0 - 1 + hy, xx = t.x0 - 1 + hx;
+      const bool ok = used && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const int rs = ok ? (t.n * H + yy) * W + xx : zrow;
+      const uint32_t voff = (uint32_t)rs * 64u + (uint32_t)((c ^ plane_swz(rs)) << 4);
+      const char* base = reinterpret_cast<const char*>(g.X.p + pl * g.X.ps + (size_t)cb * g.X.rows_pad * BK);
+      dma16(base, voff, lds0 + buf * HALO_BYTES + q * 1024);
+    }
+  };
+  auto issue_w = [&](int n0, int ls, int slot) {
+    const int kt = (ls % 9) * CB + ls / 9;  // local step ls = (channel block ls / 9, tap ls % 9)
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int q = wave * PW + i;
+      const int pl = q / (WPT / 1024), pc = q % (WPT / 1024);
+      const char* src = reinterpret_cast<const char*>(g.Wt.p + pl * g.Wt.ps + ((size_t)kt * g.Wt.rows_pad + n0) * BK) + pc * 1024;
+      dma16(src, lane * 16, lds0 + 2 * HALO_BYTES + slot * WSTAGE + q * 1024);
+    }
+  };
+  // W(u) for global step u: tile k + (ls >= nsteps), local step ls
+  auto issue_w_step = [&](const Tile& cur, const Tile& nxt, int ls, int u) {
+    if (ls < nsteps) issue_w(cur.n0, ls, u % NSW);
+    else issue_w(nxt.n0, ls - nsteps, u % NSW);
+  };
+  // GEMM row p of the tile (quad order) -> pixel (py, px)
+  auto pix = [&](int p, int& py, int& px) {
+    const int q4 = p >> 2, sub = p & 3;
+    py = 2 * (q4 >> 3) + (sub >> 1);
+    px = 2 * (q4 & 7) + (sub & 1);
+  };
+  int hpy[WMT], hpx[WMT];  // halo pixel of this lane's A rows at tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < WMT; ++i) pix(wm0 + i * 16 + (lane & 15), hpy[i], hpx[i]);
+
+  // one step's fragments: all twelve reads in flight, then the MFMAs (left to itself the
+  // scheduler recycles fragment registers and serialises each read behind the last MFMAs)
+  struct Frag {
+    f16x8 ah[WMT], al[WMT], wh[4], wl[4];
+  };
+  auto load = [&](Frag& f, int hbuf, int tap, int wslot) {
+    const char* hb = smem + hbuf * HALO_BYTES;
+    const char* wb = smem + 2 * HALO_BYTES + wslot * WSTAGE;
+    const int c = lane >> 4, r16 = lane & 15;
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) {
+      const int x = hpx[i] + tap % 3;
+      const int o = halo_row(hpy[i] + tap / 3, x) * (BK * 2) + (halo_pos(x, c) << 4);
+      f.ah[i] = *reinterpret_cast<const f16x8*>(hb + o);
+      f.al[i] = *reinterpret_cast<const f16x8*>(hb + HALO_PLANE + o);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = wn0 + j * 16 + r16;
+      const int o = r * (BK * 2) + ((c ^ plane_swz(r)) << 4);
+      f.wh[j] = *reinterpret_cast<const f16x8*>(wb + o);
+      f.wl[j] = *reinterpret_cast<const f16x8*>(wb + WPT + o);
+    }
+  };
+  f32x4 acc[WMT][4];
+  auto mma = [&](const Frag& f) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f16x8 whs = f.wh[j] * (_Float16)kLoScale;  // exact: |W_h| < 16
+#pragma unroll
+      for (int i = 0; i < WMT; ++i) acc[i][j] = mfma_h3_16(f.ah[i], f.al[i], whs, f.wl[j], f.wh[j], acc[i][j]);
+    }
+  };
+  auto barrier = [&] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  const int cq = (lane & 7) * 8;
+  const float so = ldexpf(1.f, -eo);
+  float wmax = 0.f;
+  auto store8 = [&](int row, int col0, f32x4 v0, f32x4 v1) {
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.bias + col0);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.bias + col0 + 4);
+    f16x8 h, l;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = fmaxf(fmaf(e < 4 ? v0[e] : v1[e - 4], accs, e < 4 ? b0[e] : b1[e - 4]), 0.f);
+      wmax = fmaxf(wmax, v);
+      _Float16 a, c;
+      split2h(v * so, a, c);
+      h[e] = a;
+      l[e] = c;
+    }
+    const size_t off = plane_off(row, col0, g.yrows_pad);
+    *reinterpret_cast<f16x8*>(g.Y + off) = h;
+    *reinterpret_cast<f16x8*>(g.Y + g.yps + off) = l;
+  };
+
+  // prologue: halo 0, weights of steps 0 and 1
+  Tile cur = decode(0);
+  Tile nxt = T > 1 ? decode(1) : cur;
+  issue_halo(cur, 0, 0);
+  issue_w(cur.n0, 0, 0);
+  issue_w_step(cur, nxt, 1, 1);
+
+  int gs = 0;
+  for (int k = 0; k < T; ++k) {
+#pragma unroll
+    for (int i = 0; i < WMT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int cb = 0; cb < CB; ++cb) {
+      const int gcb = k * CB + cb;
+      const bool hnext = gcb + 1 < GCB;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap, ++gs) {
+        // W(gs) complete (and with it the halo of this block, issued before it); issued after
+        // it: W(gs + 1) and, at taps 1-2, the next halo (issued at tap 0)
+        if ((tap == 1 || tap == 2) && hnext) sp_wait_vm<PW + PH>();
+        else if (gs + 1 < S) sp_wait_vm<PW>();
+        else sp_wait_vm<0>();
+        barrier();
+        if (gs + 2 < S) issue_w_step(cur, nxt, cb * 9 + tap + 2, gs + 2);
+        if (tap == 0 && hnext) {
+          if (cb + 1 < CB) issue_halo(cur, cb + 1, (gcb + 1) & 1);
+          else issue_halo(nxt, 0, (gcb + 1) & 1);
+        }
+        Frag f;
+        load(f, gcb & 1, tap, gs % NSW);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(f);
+      }
+    }
+    // epilogue: bias + ReLU (+ pool) -> planes through a per-wave transpose in the halo buffer
+    // just consumed (every wave past its last read of it: the barrier)
+    barrier();
+    float* ep = reinterpret_cast<float*>(smem + ((k * CB + CB - 1) & 1) * HALO_BYTES) + wave * (EPR * 64);
+    const int col0 = cur.n0 + wn0 + cq;
+    if constexpr (!POOL) {
+#pragma unroll
+      for (int a = 0; a < WMT; ++a)
+#pragma unroll
+        for (int h = 0; h < 16 / EPR; ++h) {
+          if ((lane >> 4) / (EPR / 4) == h)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int rr = ((lane >> 4) % (EPR / 4)) * 4 + r, c = j * 16 + (lane & 15);
+                ep[rr * 64 + (c ^ ((rr & 1) << 2))] = acc[a][j][r];
+              }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int kk = 0; kk < EPR / 8; ++kk) {
+            const int rr = (lane >> 3) + 8 * kk;
+            int py, px;
+            pix(wm0 + a * 16 + h * EPR + rr, py, px);
+            const int sw = (rr & 1) << 2;
+            const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
+            const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
+            if (cur.y0 + py < H && cur.x0 + px < W) store8((cur.n * H + cur.y0 + py) * W + cur.x0 + px, col0, v0, v1);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
+        }
+    } else {
+      // the 4 registers of a lane are the 4 pixels of one pooling window: relu(max + b) ==
+      // max(relu(. + b)) (monotone, and rounding is monotone); 16 quads per pass
+#pragma unroll
+      for (int a2 = 0; a2 < WMT / 4 + (WMT < 4); ++a2) {
+#pragma unroll
+        for (int a = 0; a < (WMT < 4 ? WMT : 4); ++a)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 v = acc[a2 * 4 + a][j];
+            const int pr_ = a * 4 + (lane >> 4), c = j * 16 + (lane & 15);
+            ep[pr_ * 64 + (c ^ ((pr_ & 1) << 2))] = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int kk = 0; kk < (WMT < 4 ? WMT : 4) / 2; ++kk) {
+          const int rr = (lane >> 3) + 8 * kk;
+          const int q4 = (wm0 + a2 * 64) / 4 + rr;  // quad of the tile
+          const int qy = cur.y0 / 2 + (q4 >> 3), qx = cur.x0 / 2 + (q4 & 7);
+          const int sw = (rr & 1) << 2;
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
+          const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
+          if (qy < Hp && qx < Wp) store8((cur.n * Hp + qy) * Wp + qx, col0, v0, v1);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+    cur = nxt;
+    if (k + 2 < T) nxt = decode(k + 2);
+  }
+  range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem + 2 * HALO_BYTES));
+}
+
+static int sp_num_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return 256;
+    return cus;
+  }();
+  return n;
+}
+
+template <int BN, bool POOL>
+static hipError_t sp_conv3x3_halo_launch(const ConvH3Args& a, hipStream_t st) {
+  const int tiles = a.B * ((a.H + kHT - 1) / kHT) * ((a.W + kHT - 1) / kHT) * (a.Cout / BN);
+  const int grid = std::min(tiles, sp_num_cus());  // one workgroup per CU (LDS-limited)
+  hipLaunchKernelGGL((sp_conv3x3_halo_kernel<BN, POOL>), dim3(grid), dim3(8 * (BN / 64) * 64), 0, st, a);
+  return hipGetLastError();
+}
+
 template <int BN, int NS, bool POOL>
 static hipError_t sp_conv3x3_launch(const ConvH3Args& a, int R, hipStream_t st) {
   const int tiles = ((R + 255) / 256) * (a.Cout / BN);
@@ -331,6 +644,11 @@ hipError_t sp_conv3x3(const ConvH3Args& a, hipStream_t st) {
       a.Wt.rows_pad != a.Cout || a.yrows_pad < rout || a.X.rows_pad > (1 << 26))  // 32-bit DMA byte offsets
     return hipErrorInvalidValue;
   if (a.pool && (a.H < 2 || a.W < 2)) return hipErrorInvalidValue;
+  static const bool gather = getenv("LG_SP_CONV") && !strcmp(getenv("LG_SP_CONV"), "gather");
+  if (!gather) {  // halo tiles (default); LG_SP_CONV=gather: the per-tap row gather above
+    if (a.Cout % 128 == 0) return a.pool ? sp_conv3x3_halo_launch<128, true>(a, st) : sp_conv3x3_halo_launch<128, false>(a, st);
+    return a.pool ? sp_conv3x3_halo_launch<64, true>(a, st) : sp_conv3x3_halo_launch<64, false>(a, st);
+  }
   const int R = (int)(a.pool ? 4 * rout : rin);
   if (a.Cout % 128 == 0) return a.pool ? sp_conv3x3_launch<128, 3, true>(a, R, st) : sp_conv3x3_launch<128, 3, false>(a, R, st);
   return a.pool ? sp_conv3x3_launch<64, 3, true>(a, R, st) : sp_conv3x3_launch<64, 3, false>(a, R, st);

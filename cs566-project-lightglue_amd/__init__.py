@@ -20,6 +20,10 @@ def __getattr__(name):
         from .superpoint import SuperPoint
 
         return SuperPoint
+    if name in ("SuperGlue", "NLLLoss"):
+        from . import superglue
+
+        return getattr(superglue, name)
     if name in ("log_optimal_transport", "filter_matches"):
         from . import assignment
 

@@ -42,6 +42,15 @@ EXPORTED_SYMBOLS = [
     "sp_workspace_bytes",
     "sp_forward",
     "sp_sample_descriptors",
+    "sg_create",
+    "sg_destroy",
+    "sg_weight_count",
+    "sg_weight_name",
+    "sg_weight_numel",
+    "sg_load_weights",
+    "sg_workspace_bytes",
+    "sg_forward",
+    "sg_nll_loss",
 ]
 KERNEL_IDS = {"attention": 0, "gemm": 1, "assign": 2}
 # lg_config_t.precision (include/lightglue_mi355x.h): "auto" = fp16x3 (device-side range scaling)
@@ -148,6 +157,56 @@ class SPOutputs(ctypes.Structure):  # sp_outputs_t
     ]
 
 
+SG_MAX_LAYERS = 64
+SG_MAX_KENC = 7
+
+
+class SGConfig(ctypes.Structure):  # sg_config_t
+    _fields_ = [
+        ("descriptor_dim", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("layer_types", ctypes.c_int32 * SG_MAX_LAYERS),
+        ("n_kenc", ctypes.c_int32),
+        ("keypoint_encoder", ctypes.c_int32 * SG_MAX_KENC),
+        ("use_scores", ctypes.c_int32),
+        ("sinkhorn_iterations", ctypes.c_int32),
+        ("filter_threshold", ctypes.c_float),
+    ]
+
+
+class SGInputs(ctypes.Structure):  # sg_inputs_t
+    _fields_ = [
+        ("B", ctypes.c_int32),
+        ("M", ctypes.c_int32),
+        ("N", ctypes.c_int32),
+        ("keypoints0", _P),
+        ("keypoints1", _P),
+        ("descriptors0", _P),
+        ("descriptors1", _P),
+        ("scores0", _P),
+        ("scores1", _P),
+        ("image_size0", _P),
+        ("image_size1", _P),
+        ("image_w0", ctypes.c_int32),
+        ("image_h0", ctypes.c_int32),
+        ("image_w1", ctypes.c_int32),
+        ("image_h1", ctypes.c_int32),
+    ]
+
+
+class SGOutputs(ctypes.Structure):  # sg_outputs_t
+    _fields_ = [
+        ("matches0", _P),
+        ("matches1", _P),
+        ("matching_scores0", _P),
+        ("matching_scores1", _P),
+        ("sinkhorn_cost", _P),
+        ("log_assignment", _P),
+        ("descriptors0", _P),
+        ("descriptors1", _P),
+    ]
+
+
 class LightGlueLibError(RuntimeError):
     pass
 
@@ -204,6 +263,18 @@ def load():
         "sp_workspace_bytes": (ctypes.c_int, [_P, i32, i32, i32, i32, i32, ctypes.POINTER(sz)]),
         "sp_forward": (ctypes.c_int, [_P, ctypes.POINTER(SPInputs), ctypes.POINTER(SPOutputs), _P, sz, _P]),
         "sp_sample_descriptors": (ctypes.c_int, [_P, _P, _P, i32, i32, _P, _P, sz, _P]),
+        "sg_create": (ctypes.c_int, [ctypes.POINTER(SGConfig), ctypes.c_int, ctypes.POINTER(_P)]),
+        "sg_destroy": (ctypes.c_int, [_P]),
+        "sg_weight_count": (ctypes.c_int, [_P]),
+        "sg_weight_name": (ctypes.c_char_p, [_P, ctypes.c_int]),
+        "sg_weight_numel": (ctypes.c_int64, [_P, ctypes.c_int]),
+        "sg_load_weights": (
+            ctypes.c_int,
+            [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64), _P],
+        ),
+        "sg_workspace_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
+        "sg_forward": (ctypes.c_int, [_P, ctypes.POINTER(SGInputs), ctypes.POINTER(SGOutputs), _P, sz, _P]),
+        "sg_nll_loss": (ctypes.c_int, [_P, i32, i32, i32, _P, _P, _P, i32, ctypes.c_float, _P, _P]),
         "lg_profile_read": (
             ctypes.c_int,
             [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),

@@ -437,6 +437,12 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
                 v1[e] = r1[e] + v1[e];
               }
             }
+            if (g.relu)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v0[e] = fmaxf(v0[e], 0.f);
+                v1[e] = fmaxf(v1[e], 0.f);
+              }
             if (g.Y) {
               float* yp = g.Y + (size_t)row * g.ldy + n0 + wn0 + c4;
               *reinterpret_cast<f32x4*>(yp) = v0;
@@ -464,6 +470,10 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
               for (int e = 0; e < 4; ++e) {
                 v0[e] = fmaf(v0[e], accs, b0[e]) * g.out_scale;
                 v1[e] = fmaf(v1[e], accs, b1[e]) * g.out_scale;
+                if (g.relu) {
+                  v0[e] = fmaxf(v0[e], 0.f);
+                  v1[e] = fmaxf(v1[e], 0.f);
+                }
               }
             }
             f16x8 h, l;
@@ -503,7 +513,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     __syncthreads();
     const int cbase = n0 + wn0;
     const int t = cbase / kDim, head = (cbase % kDim) / kHeadDim;
-    const bool rot = EPI == EPI_QKV_ROT && t < 2;
+    const bool rot = EPI == EPI_QKV_ROT && t < 2 && hl.cosb;  // no cos table: plain q/k/v (SuperGlue)
     const bool to_q = t == 0;
     const bool to_kp = EPI == EPI_QKV_ROT ? t == 1 : t == 0;
     const bool to_vp = EPI == EPI_QKV_ROT ? t == 2 : t == 1;

@@ -147,7 +147,8 @@ struct GemmH3Args {
   RowMask rm;         // live rows (batched pruning; cnt == null: all)
   const float* ln_g;  // EPI_LN_GELU: LayerNorm weight / bias [Nout]
   const float* ln_b;
-  HeadLayout hl;      // EPI_QKV_ROT / EPI_CROSS_QKV
+  HeadLayout hl;      // EPI_QKV_ROT / EPI_CROSS_QKV (EPI_QKV_ROT with hl.cosb null: no rotary)
+  int relu;           // EPI_STORE: max(., 0) after bias / scale / residual
 };
 hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st);
 // fp32 rows [R][K] (row stride ld) -> rows row0 .. row0+R-1 of a plane image (rows_pad), with
@@ -360,5 +361,34 @@ hipError_t sp_keypoints(const int* sel_idx, const int* n, int B, int cap, int Hs
 // desc NHWC [B][Hc][Wc][256]; out [B][cap][256]; kpts_out (nullable) = kpts + 0.5
 hipError_t sp_sample(const float* kpts, const int* n, int B, int cap, const float* desc, int Hc, int Wc, int legacy,
                      float* out, float* kpts_out, hipStream_t st);
+
+
+// ---- SuperGlue (gluefactory_nonfree/superglue.py, superglue.hip) ---------------------------
+constexpr int kSgMaxEnc = 8;
+struct SgEncLayer {
+  const float* Wt;  // [Cin][Cout] (transposed Conv1d weight)
+  const float* b;
+  const float *bn_w, *bn_b, *bn_mean, *bn_var;  // eval BatchNorm (all layers but the last)
+};
+// x[r] = desc[r] + MLP([x_n, y_n(, score)]) for rows r of one image set (rows = B * n, 256 wide);
+// keypoints normalised by size[b] (w, h) or (fw, fh) (superglue.py:75-86)
+struct SgEncArgs {
+  const float* kpts;
+  const float* scores;  // null without use_scores
+  const float* size;
+  float fw, fh;
+  const float* desc;
+  float* x;
+  int rows, n, nl;
+  int ch[kSgMaxEnc + 1];
+  SgEncLayer layer[kSgMaxEnc];
+};
+hipError_t sg_keypoint_encoder(const SgEncArgs& a, hipStream_t st);
+hipError_t sg_transpose(const float* src, int rows, int cols, float* dst, hipStream_t st);
+hipError_t sg_gather_cols(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st);
+hipError_t sg_bn_fold(float* W, float* b, const float* g, const float* be, const float* mean, const float* var, int rows,
+                      int cols, hipStream_t st);
+hipError_t sg_nll_loss(const float* la, int B, int M, int N, const uint8_t* gta, const int64_t* gt0, const int64_t* gt1,
+                       int mode, float balancing, float* out, hipStream_t st);
 
 }  // namespace lg

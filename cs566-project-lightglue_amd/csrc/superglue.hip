@@ -1,0 +1,180 @@
+// SuperGlue pieces that are not shared with LightGlue (gluefactory_nonfree/superglue.py):
+//   the keypoint encoder (normalize_keypoints + MLP with eval BatchNorm, :75-104) added to the
+//   descriptors, load-time weight folds / permutations, and the NLL losses (:309-339 and
+//   gluefactory/models/utils/losses.py).  The GNN runs on the LightGlue kernels (superglue_api.cpp).
+#include <cstdint>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace lg {
+
+namespace {
+constexpr int kEncRows = 32;  // keypoints per workgroup
+constexpr int kEncMaxC = 256;
+}  // namespace
+
+// One workgroup = 32 keypoints of one image set; activations in LDS, layer by layer.  Layer l:
+// out[o] = b[o] + sum_c Wt[c][o] in[c] (sequential over c, fp32), then eval BatchNorm in ATen's
+// CPU form (alpha = w / sqrt(var + eps), out * alpha + (b - mean * alpha)) and ReLU, except after
+// the last layer, whose output is added to the descriptor row: x = desc + enc.
+__global__ __launch_bounds__(256) void sg_kenc_kernel(SgEncArgs a) {
+  __shared__ float act[2][kEncRows][kEncMaxC + 1];
+  const int tid = threadIdx.x;
+  const int row0 = blockIdx.x * kEncRows;
+  const int nrow = min(kEncRows, a.rows - row0);
+  // inputs: normalised keypoint (x, y) and the score (superglue.py:82-86, 97-101)
+  if (tid < kEncRows) {
+    const int r = row0 + tid;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if (tid < nrow) {
+      const int b = r / a.n;
+      const float w = a.size ? a.size[2 * b] : a.fw, h = a.size ? a.size[2 * b + 1] : a.fh;
+      const float scale = fmaxf(w, h) * 0.7f;
+      v0 = (a.kpts[2 * (size_t)r] - w / 2.f) / scale;
+      v1 = (a.kpts[2 * (size_t)r + 1] - h / 2.f) / scale;
+      v2 = a.scores ? a.scores[r] : 0.f;
+    }
+    act[0][tid][0] = v0;
+    act[0][tid][1] = v1;
+    act[0][tid][2] = v2;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int l = 0; l < a.nl; ++l) {
+    const int cin = a.ch[l], cout = a.ch[l + 1];
+    const SgEncLayer& L = a.layer[l];
+    const bool last = l == a.nl - 1;
+    for (int idx = tid; idx < kEncRows * cout; idx += blockDim.x) {
+      const int k = idx / cout, o = idx - k * cout;
+      float acc = 0.f;
+      for (int c = 0; c < cin; ++c) acc = fmaf(L.Wt[(size_t)c * cout + o], act[cur][k][c], acc);
+      acc += L.b[o];
+      if (!last) {
+        const float alpha = L.bn_w[o] * (1.f / sqrtf(L.bn_var[o] + 1e-5f));
+        const float beta = L.bn_b[o] - L.bn_mean[o] * alpha;
+        act[cur ^ 1][k][o] = fmaxf(acc * alpha + beta, 0.f);
+      } else if (k < nrow) {
+        const size_t r = (size_t)(row0 + k);
+        a.x[r * kEncMaxC + o] = a.desc[r * kEncMaxC + o] + acc;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+hipError_t sg_keypoint_encoder(const SgEncArgs& a, hipStream_t st) {
+  if (a.rows <= 0) return hipSuccess;
+  if (a.nl < 1 || a.nl > kSgMaxEnc || a.ch[0] < 2 || a.ch[0] > 3 || a.ch[a.nl] != kEncMaxC || a.n <= 0)
+    return hipErrorInvalidValue;
+  for (int l = 1; l < a.nl; ++l)
+    if (a.ch[l] <= 0 || a.ch[l] > kEncMaxC) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sg_kenc_kernel, dim3((a.rows + kEncRows - 1) / kEncRows), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// dst[c][o] = src[o][c] (the encoder's weights, read coalesced over o)
+__global__ void sg_transpose_kernel(const float* src, int rows, int cols, float* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int o = i / cols, c = i - o * cols;
+  dst[(size_t)c * rows + o] = src[i];
+}
+hipError_t sg_transpose(const float* src, int rows, int cols, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(sg_transpose_kernel, dim3((rows * cols + 255) / 256), dim3(256), 0, st, src, rows, cols, dst);
+  return hipGetLastError();
+}
+
+// dst[r][c] = src[r][idx[c]]
+__global__ void sg_gather_cols_kernel(float* dst, const float* src, const int* idx, int rows, int cols) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int r = i / cols, c = i - r * cols;
+  dst[i] = src[(size_t)r * cols + idx[c]];
+}
+hipError_t sg_gather_cols(float* dst, const float* src, const int* idx, int rows, int cols, hipStream_t st) {
+  hipLaunchKernelGGL(sg_gather_cols_kernel, dim3((rows * cols + 255) / 256), dim3(256), 0, st, dst, src, idx, rows, cols);
+  return hipGetLastError();
+}
+
+// eval BatchNorm folded into the preceding linear: W[o][:] *= alpha[o], b[o] = b[o] alpha[o] + beta[o]
+__global__ void sg_bn_fold_kernel(float* W, float* b, const float* g, const float* be, const float* mean, const float* var,
+                                  int rows, int cols) {
+  const int o = blockIdx.x;
+  const float alpha = g[o] * (1.f / sqrtf(var[o] + 1e-5f));
+  const float beta = be[o] - mean[o] * alpha;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) W[(size_t)o * cols + c] *= alpha;
+  if (threadIdx.x == 0) b[o] = b[o] * alpha + beta;
+}
+hipError_t sg_bn_fold(float* W, float* b, const float* g, const float* be, const float* mean, const float* var, int rows,
+                      int cols, hipStream_t st) {
+  hipLaunchKernelGGL(sg_bn_fold_kernel, dim3(rows), dim3(256), 0, st, W, b, g, be, mean, var, rows, cols);
+  return hipGetLastError();
+}
+
+// NLL of a log assignment [B][M+1][N+1] against a ground truth (one workgroup per pair; sums in
+// fp64, one rounding to fp32 at the end).  out[k * B + b]: 0 nll, 1 nll_pos, 2 nll_neg,
+// 3 num_matchable, 4 num_unmatchable.
+//   mode 0 (SuperGlue.loss, superglue.py:309-339): num_pos = max(#pos, 1), num_neg = max(#neg0 +
+//          #neg1, 1), nll_neg = (neg0 + neg1) / num_neg
+//   mode 1 (losses.py NLLLoss + weight_loss): the dustbin row weights are written at [:, -1, :M]
+//          (the caller checks M == N), counts clamped separately, num_unmatchable = (n0 + n1) / 2
+__global__ __launch_bounds__(256) void sg_nll_kernel(const float* la, int M, int N, const uint8_t* gta, const int64_t* gt0,
+                                                     const int64_t* gt1, int mode, float bal, int B, float* out) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* L = la + (size_t)b * (M + 1) * (N + 1);
+  double pos = 0.0, npos = 0.0, neg0 = 0.0, n0 = 0.0, neg1 = 0.0, n1 = 0.0;
+  for (size_t i = tid; i < (size_t)M * N; i += blockDim.x) {
+    const size_t r = i / N, c = i - r * N;
+    if (gta[(size_t)b * M * N + i]) {
+      pos += L[r * (N + 1) + c];
+      npos += 1.0;
+    }
+  }
+  for (int i = tid; i < M; i += blockDim.x)
+    if (gt0[(size_t)b * M + i] == -1) {
+      neg0 += L[(size_t)i * (N + 1) + N];
+      n0 += 1.0;
+    }
+  for (int j = tid; j < N; j += blockDim.x)
+    if (gt1[(size_t)b * N + j] == -1) {
+      neg1 += L[(size_t)M * (N + 1) + j];
+      n1 += 1.0;
+    }
+  __shared__ double red[6][256];
+  red[0][tid] = pos; red[1][tid] = npos; red[2][tid] = neg0; red[3][tid] = n0; red[4][tid] = neg1; red[5][tid] = n1;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s)
+      for (int k = 0; k < 6; ++k) red[k][tid] += red[k][tid + s];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float P = (float)red[0][0], NP = (float)red[1][0], G0 = (float)red[2][0], C0 = (float)red[3][0];
+    const float G1 = (float)red[4][0], C1 = (float)red[5][0];
+    float num_pos = fmaxf(NP, 1.f), nll_pos = -P / num_pos, nll_neg, num_neg;
+    if (mode == 0) {
+      num_neg = fmaxf(C0 + C1, 1.f);
+      nll_neg = (-G0 + -G1) / num_neg;
+    } else {
+      const float a0 = fmaxf(C0, 1.f), a1 = fmaxf(C1, 1.f);
+      nll_neg = (-G0 + -G1) / (a0 + a1);
+      num_neg = (a0 + a1) / 2.f;
+    }
+    const float nll = bal * nll_pos + (1.f - bal) * nll_neg;
+    out[0 * B + b] = nll;
+    out[1 * B + b] = nll_pos;
+    out[2 * B + b] = nll_neg;
+    out[3 * B + b] = num_pos;
+    out[4 * B + b] = num_neg;
+  }
+}
+hipError_t sg_nll_loss(const float* la, int B, int M, int N, const uint8_t* gta, const int64_t* gt0, const int64_t* gt1,
+                       int mode, float balancing, float* out, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sg_nll_kernel, dim3(B), dim3(256), 0, st, la, M, N, gta, gt0, gt1, mode, balancing, B, out);
+  return hipGetLastError();
+}
+
+}  // namespace lg

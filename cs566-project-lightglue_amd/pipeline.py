@@ -127,6 +127,12 @@ def _superpoint():
     return SuperPoint
 
 
+def _superglue():
+    from .superglue import SuperGlue
+
+    return SuperGlue
+
+
 _REGISTRY = {
     "lightglue": LightGlue,
     "matchers.lightglue": LightGlue,
@@ -137,6 +143,9 @@ _REGISTRY = {
     "gluefactory_nonfree.superpoint": _superpoint,
     "extractors.superpoint": _superpoint,
     "superpoint": _superpoint,
+    # the SuperGlue matcher (gluefactory_nonfree/superglue.py), resolved lazily
+    "gluefactory_nonfree.superglue": _superglue,
+    "superglue": _superglue,
 }
 
 
@@ -151,7 +160,7 @@ def get_model(name):
     for path in (name, f"matchers.{name}", f"extractors.{name}"):
         if path in _REGISTRY:
             obj = _REGISTRY[path]
-            return obj() if obj is _superpoint else obj
+            return obj() if obj in (_superpoint, _superglue) else obj
     paths = [name, f"gluefactory.models.{name}", f"gluefactory.models.extractors.{name}",
              f"gluefactory.models.matchers.{name}"]
     raise RuntimeError(f'Model {name} not found in any of [{" ".join(paths)}]')

@@ -67,14 +67,16 @@ def superglue_schema(conf=None):
     """[(name, shape, kind)] in the reference's state-dict order."""
     c = merged_conf(conf)
     d = c["descriptor_dim"]
-    out = _mlp("kenc.encoder", [3 if c["use_scores"] else 2] + c["keypoint_encoder"] + [d])
+    # the module's own parameter (registered last, :246-247) comes first in a state dict
+    out = [("bin_score", (), "scalar")]
+    out += _mlp("kenc.encoder", [3 if c["use_scores"] else 2] + c["keypoint_encoder"] + [d])
     for i in range(len(c["GNN_layers"])):
         p = f"gnn.layers.{i}"
         out += [(f"{p}.attn.merge.weight", (d, d, 1), "conv_w"), (f"{p}.attn.merge.bias", (d,), "conv_b")]
         for j in range(3):
             out += [(f"{p}.attn.proj.{j}.weight", (d, d, 1), "conv_w"), (f"{p}.attn.proj.{j}.bias", (d,), "conv_b")]
         out += _mlp(f"{p}.mlp", [2 * d, 2 * d, d])
-    out += [("final_proj.weight", (d, d, 1), "conv_w"), ("final_proj.bias", (d,), "conv_b"), ("bin_score", (), "scalar")]
+    out += [("final_proj.weight", (d, d, 1), "conv_w"), ("final_proj.bias", (d,), "conv_b")]
     return out
 
 

@@ -1,0 +1,282 @@
+"""MI355X-native SuperGlue matcher: drop-in for ``gluefactory_nonfree.superglue.SuperGlue``
+(reference ``superglue.py:204-342``) and for the NLL loss of ``gluefactory/models/utils/losses.py``.
+
+Same config keys (:205-217), same module tree (``kenc.encoder`` MLP, ``gnn.layers.<i>.attn``
+{``proj``, ``merge``} / ``mlp``, ``final_proj``, ``bin_score``: checkpoints load unchanged), same
+``forward(data) -> dict`` outputs (:300-307) and ``loss(pred, data)`` (:309-339).  The forward is
+the HIP path of ``liblightglue_mi355x.so`` (``include/superglue_mi355x.h``): keypoint encoder
+kernel, the LightGlue fp16x3 GEMM / attention kernels for the 18-layer GNN (merge and eval
+BatchNorm folded into the MLP's first linear at load time), bf16x6 cost GEMM, the log-domain
+Sinkhorn kernel and the mutual filter.  No CPU fallback: CPU inputs raise.
+
+Deliberate differences from the reference:
+
+* the trained checkpoint is a download (:248-251); the module starts from PyTorch's default init
+  (``weights`` is ignored) and takes weights through ``load_state_dict``;
+* eval only: BatchNorm uses its running statistics; a module in training mode raises (the
+  reference trains through ``torch.utils.checkpoint`` and batch statistics);
+* ``NLLLoss`` with explicit ``weights`` raises NotImplementedError (the kernel derives the weights
+  from the ground truth, :46-73).
+"""
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _lib
+from .lightglue import merge_conf
+from .sg_weights import SG_DEFAULT_CONF
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _mlp(channels):  # superglue.py:63-72 (parameter container)
+    layers = []
+    for i in range(1, len(channels)):
+        layers.append(nn.Conv1d(channels[i - 1], channels[i], kernel_size=1, bias=True))
+        if i < len(channels) - 1:
+            layers.append(nn.BatchNorm1d(channels[i]))
+            layers.append(nn.ReLU())
+    return nn.Sequential(*layers)
+
+
+class _KeypointEncoder(nn.Module):  # superglue.py:89-104
+    def __init__(self, feature_dim, layers, use_scores=True):
+        super().__init__()
+        self.encoder = _mlp([3 if use_scores else 2] + list(layers) + [feature_dim])
+        nn.init.constant_(self.encoder[-1].bias, 0.0)
+
+
+class _MultiHeadedAttention(nn.Module):  # superglue.py:113-128
+    def __init__(self, h, d_model):
+        super().__init__()
+        self.merge = nn.Conv1d(d_model, d_model, kernel_size=1)
+        self.proj = nn.ModuleList([nn.Conv1d(d_model, d_model, kernel_size=1) for _ in range(3)])
+
+
+class _AttentionalPropagation(nn.Module):  # superglue.py:131-139
+    def __init__(self, num_dim, num_heads):
+        super().__init__()
+        self.attn = _MultiHeadedAttention(num_heads, num_dim)
+        self.mlp = _mlp([num_dim * 2, num_dim * 2, num_dim])
+        nn.init.constant_(self.mlp[-1].bias, 0.0)
+
+
+class _AttentionalGNN(nn.Module):  # superglue.py:142-170
+    def __init__(self, feature_dim, layer_names):
+        super().__init__()
+        self.layers = nn.ModuleList([_AttentionalPropagation(feature_dim, 4) for _ in range(len(layer_names))])
+        self.names = list(layer_names)
+
+
+class SuperGlue(nn.Module):
+    default_conf = SG_DEFAULT_CONF
+    required_data_keys = ["view0", "view1", "keypoints0", "keypoints1", "descriptors0", "descriptors1",
+                          "keypoint_scores0", "keypoint_scores1"]
+    checkpoint_url = "https://github.com/magicleap/SuperGluePretrainedNetwork/raw/master/models/weights/superglue_{}.pth"
+
+    def __init__(self, conf=None):
+        super().__init__()
+        self.conf = conf = merge_conf(self.default_conf, conf or {})
+        if int(conf.descriptor_dim) != 256:
+            raise ValueError("lightglue_amd.SuperGlue: descriptor_dim must be 256")
+        if len(conf.GNN_layers) > _lib.SG_MAX_LAYERS or len(conf.keypoint_encoder) > _lib.SG_MAX_KENC:
+            raise ValueError("lightglue_amd.SuperGlue: too many GNN / keypoint-encoder layers")
+        for n in conf.GNN_layers:
+            if n not in ("self", "cross"):
+                raise ValueError(n)
+        self.kenc = _KeypointEncoder(conf.descriptor_dim, conf.keypoint_encoder, conf.use_scores)
+        self.gnn = _AttentionalGNN(conf.descriptor_dim, conf.GNN_layers)
+        self.final_proj = nn.Conv1d(conf.descriptor_dim, conf.descriptor_dim, kernel_size=1, bias=True)
+        self.register_parameter("bin_score", nn.Parameter(torch.tensor(1.0)))
+        self._handle = None
+        self._handle_device = None
+        self._weights_key = None
+        self._ws = None
+
+    # ------------------------------------------------------------ native handle
+    def _lib_config(self):
+        c = self.conf
+        cfg = _lib.SGConfig()
+        cfg.descriptor_dim = int(c.descriptor_dim)
+        cfg.n_layers = len(c.GNN_layers)
+        for i, n in enumerate(c.GNN_layers):
+            cfg.layer_types[i] = 0 if n == "self" else 1
+        cfg.n_kenc = len(c.keypoint_encoder)
+        for i, w in enumerate(c.keypoint_encoder):
+            cfg.keypoint_encoder[i] = int(w)
+        cfg.use_scores = int(bool(c.use_scores))
+        cfg.sinkhorn_iterations = int(c.num_sinkhorn_iterations)
+        cfg.filter_threshold = float(c.filter_threshold)
+        return cfg
+
+    def _weights_signature(self):
+        return tuple((id(m), n, t.data_ptr(), t._version) for m in self.modules()
+                     for n, t in list(m._parameters.items()) + list(m._buffers.items()) if t is not None)
+
+    def _ensure_handle(self, device):
+        lib = _lib.load()
+        if self._handle is not None and self._handle_device != device:
+            lib.sg_destroy(self._handle)
+            self._handle = None
+        if self._handle is None:
+            h = ctypes.c_void_p()
+            cfg = self._lib_config()
+            _lib.check(lib.sg_create(ctypes.byref(cfg), device.index or 0, ctypes.byref(h)), "sg_create")
+            self._handle, self._handle_device, self._weights_key = h, device, None
+        key = self._weights_signature()
+        if key != self._weights_key:
+            sd = {k: v for k, v in self.state_dict(keep_vars=True).items() if not k.endswith("num_batches_tracked")}
+            names = list(sd)
+            ts = []
+            for n in names:
+                t = sd[n].detach()
+                if t.device != device or t.dtype != torch.float32:
+                    raise RuntimeError(f"lightglue_amd.SuperGlue: tensor {n} is {t.dtype} on {t.device}; "
+                                       f"move the module to {device} in fp32")
+                ts.append(t.contiguous())
+            arr_n = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+            arr_p = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+            arr_k = (ctypes.c_int64 * len(ts))(*[t.numel() for t in ts])
+            stream = torch.cuda.current_stream(device).cuda_stream
+            _lib.check(lib.sg_load_weights(self._handle, len(ts), arr_n, arr_p, arr_k, ctypes.c_void_p(stream)),
+                       "sg_load_weights")
+            torch.cuda.current_stream(device).synchronize()
+            self._weights_key = key
+        return lib
+
+    def reload_weights(self):
+        self._weights_key = None
+
+    def _apply(self, fn, *args, **kwargs):
+        self._weights_key = None
+        return super()._apply(fn, *args, **kwargs)
+
+    def __del__(self):
+        try:
+            if self._handle is not None and _lib._lib is not None:
+                _lib._lib.sg_destroy(self._handle)
+        except Exception:
+            pass
+
+    def _workspace(self, lib, device, B, M, N):
+        nb = ctypes.c_size_t()
+        _lib.check(lib.sg_workspace_bytes(self._handle, B, M, N, ctypes.byref(nb)), "sg_workspace_bytes")
+        if self._ws is None or self._ws.numel() < nb.value or self._ws.device != device:
+            self._ws = torch.empty(nb.value, dtype=torch.uint8, device=device)
+        return self._ws, nb.value
+
+    # ------------------------------------------------------------ forward (superglue.py:253-307)
+    def forward(self, data: dict, return_descriptors: bool = False) -> dict:
+        """``return_descriptors``: also return the GNN output (the input of ``final_proj``) as
+        ``gnn_descriptors0/1`` [B, N, D] (a check point for tests; not a reference output)."""
+        for k in self.required_data_keys:
+            assert k in data, f"Missing key {k} in data"
+        if self.training:
+            raise NotImplementedError("lightglue_amd.SuperGlue is eval-only (BatchNorm running statistics)")
+        c = self.conf
+        kpts0, kpts1 = data["keypoints0"], data["keypoints1"]
+        if kpts0.shape[1] == 0 or kpts1.shape[1] == 0:  # no keypoints (:257-264)
+            shape0, shape1 = kpts0.shape[:-1], kpts1.shape[:-1]
+            return {
+                "matches0": kpts0.new_full(shape0, -1, dtype=torch.int),
+                "matches1": kpts1.new_full(shape1, -1, dtype=torch.int),
+                "matching_scores0": kpts0.new_zeros(shape0),
+                "matching_scores1": kpts1.new_zeros(shape1),
+            }
+        if not kpts0.is_cuda:
+            raise RuntimeError("lightglue_amd.SuperGlue runs on a HIP device; inputs are on the CPU")
+        device = kpts0.device
+        B, M, N = kpts0.shape[0], kpts0.shape[1], kpts1.shape[1]
+
+        def size_of(view):  # normalize_keypoints' size / image-shape fallback (:78-83)
+            s = view.get("image_size")
+            if s is not None:
+                return s.to(device=device, dtype=torch.float32).contiguous(), 0, 0
+            h, w = view["image"].shape[-2:]
+            return None, int(w), int(h)
+
+        s0, w0, h0 = size_of(data["view0"])
+        s1, w1, h1 = size_of(data["view1"])
+        # the reference asserts every normalised keypoint lies in [-1, 1] (:272-273)
+        for k, s, w, h in ((kpts0, s0, w0, h0), (kpts1, s1, w1, h1)):
+            size = s if s is not None else torch.tensor([[float(w), float(h)]], device=device)
+            kn = (k.float() - (size / 2)[:, None]) / (size.max(1).values * 0.7)[:, None, None]
+            assert torch.all(kn >= -1) and torch.all(kn <= 1)
+
+        def f32(t):
+            return t.to(device=device, dtype=torch.float32).contiguous()
+
+        k0, k1 = f32(kpts0), f32(kpts1)
+        d0, d1 = f32(data["descriptors0"]), f32(data["descriptors1"])
+        sc0 = f32(data["keypoint_scores0"]) if c.use_scores else None
+        sc1 = f32(data["keypoint_scores1"]) if c.use_scores else None
+        lib = self._ensure_handle(device)
+        ws, nb = self._workspace(lib, device, B, M, N)
+        m0 = torch.empty((B, M), dtype=torch.int64, device=device)
+        m1 = torch.empty((B, N), dtype=torch.int64, device=device)
+        ms0 = torch.empty((B, M), device=device)
+        ms1 = torch.empty((B, N), device=device)
+        cost = torch.empty((B, M, N), device=device)
+        la = torch.empty((B, M + 1, N + 1), device=device)
+        inp = _lib.SGInputs(B, M, N, _ptr(k0), _ptr(k1), _ptr(d0), _ptr(d1), _ptr(sc0), _ptr(sc1), _ptr(s0), _ptr(s1),
+                            w0, h0, w1, h1)
+        g0 = torch.empty((B, M, 256), device=device) if return_descriptors else None
+        g1 = torch.empty((B, N, 256), device=device) if return_descriptors else None
+        out = _lib.SGOutputs(_ptr(m0), _ptr(m1), _ptr(ms0), _ptr(ms1), _ptr(cost), _ptr(la), _ptr(g0), _ptr(g1))
+        stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+        _lib.check(lib.sg_forward(self._handle, ctypes.byref(inp), ctypes.byref(out), _ptr(ws), nb, stream), "sg_forward")
+        pred = {"sinkhorn_cost": cost, "log_assignment": la, "matches0": m0, "matches1": m1, "matching_scores0": ms0,
+                "matching_scores1": ms1}
+        if return_descriptors:
+            pred["gnn_descriptors0"], pred["gnn_descriptors1"] = g0, g1
+        return pred
+
+    def loss(self, pred, data):
+        """superglue.py:309-339 (forward values; no backward)."""
+        out = _nll(pred["log_assignment"], data, 0, float(self.conf.loss.nll_balancing))
+        losses = {"total": out[0], "assignment_nll": out[0], "nll_pos": out[1], "nll_neg": out[2],
+                  "num_matchable": out[3], "num_unmatchable": out[4], "bin_score": self.bin_score[None]}
+        return losses
+
+    def metrics(self, pred, data):
+        raise NotImplementedError
+
+
+def _nll(la, data, mode, balancing):
+    if not la.is_cuda:
+        raise RuntimeError("lightglue_amd NLL loss runs on a HIP device; inputs are on the CPU")
+    device = la.device
+    B, M1, N1 = la.shape
+    gta = data["gt_assignment"].to(device=device).bool().to(torch.uint8).contiguous()
+    g0 = data["gt_matches0"].to(device=device, dtype=torch.int64).contiguous()
+    g1 = data["gt_matches1"].to(device=device, dtype=torch.int64).contiguous()
+    la = la.float().contiguous()
+    out = torch.empty((5, B), device=device)
+    lib = _lib.load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    rc = lib.sg_nll_loss(_ptr(la), B, M1 - 1, N1 - 1, _ptr(gta), _ptr(g0), _ptr(g1), mode, balancing, _ptr(out), stream)
+    if rc == _lib.LG_E_INVALID and mode == 1 and M1 != N1:
+        raise RuntimeError(lib.lg_last_error().decode(errors="replace"))  # the reference's own error type
+    _lib.check(rc, "sg_nll_loss")
+    return out
+
+
+class NLLLoss(nn.Module):
+    """losses.py:26-73 (forward values; no backward): ``forward(pred, data) -> (nll, None, metrics)``."""
+
+    default_conf = {"nll_balancing": 0.5, "gamma_f": 0.0}
+
+    def __init__(self, conf=None):
+        super().__init__()
+        self.conf = merge_conf(self.default_conf, conf or {})
+
+    def forward(self, pred, data, weights=None):
+        if weights is not None:
+            raise NotImplementedError("explicit loss weights (the kernel derives them from the ground truth)")
+        out = _nll(pred["log_assignment"], data, 1, float(self.conf.nll_balancing))
+        metrics = {"assignment_nll": out[0], "nll_pos": out[1], "nll_neg": out[2], "num_matchable": out[3],
+                   "num_unmatchable": out[4]}
+        return out[0], None, metrics

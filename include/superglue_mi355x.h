@@ -1,0 +1,90 @@
+/* superglue_mi355x.h -- C-ABI of the SuperGlue matcher (liblightglue_mi355x.so, gfx950).
+ *
+ * Replaces the reference's eval forward and losses of
+ *   gluefactory_nonfree/superglue.py:253-307  SuperGlue._forward(data)
+ *     :75-104   normalize_keypoints + KeypointEncoder (MLP with eval BatchNorm)
+ *     :107-170  MultiHeadedAttention / AttentionalPropagation / AttentionalGNN ("self" / "cross")
+ *     :173-201  log_optimal_transport (the same Sinkhorn kernel as lg_log_optimal_transport)
+ *     :283-298  match extraction (mutual NN + exp(max) > filter_threshold)
+ *   gluefactory_nonfree/superglue.py:309-339  SuperGlue.loss       -> sg_nll_loss(mode 0)
+ *   gluefactory/models/utils/losses.py:6-73    NLLLoss (LightGlue)  -> sg_nll_loss(mode 1)
+ * The Python binding (lightglue_amd.superglue.SuperGlue) mirrors the reference module tree, so a
+ * reference state dict loads unchanged.  Conventions as include/lightglue_mi355x.h: device
+ * pointers, row-major fp32, stream-ordered and asynchronous, LG_* error codes, lg_last_error().
+ */
+#ifndef SUPERGLUE_MI355X_H
+#define SUPERGLUE_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_MAX_LAYERS 64
+#define SG_MAX_KENC 7
+
+typedef struct sg_config_t {
+  int32_t descriptor_dim;              /* 256 (kernels are specialised) */
+  int32_t n_layers;                    /* len(GNN_layers) */
+  int32_t layer_types[SG_MAX_LAYERS];  /* 0 "self", 1 "cross" */
+  int32_t n_kenc;                      /* len(keypoint_encoder) */
+  int32_t keypoint_encoder[SG_MAX_KENC];
+  int32_t use_scores;
+  int32_t sinkhorn_iterations;
+  float filter_threshold;
+} sg_config_t;
+
+typedef struct sg_inputs_t {
+  int32_t B, M, N;
+  const float* keypoints0;    /* [B][M][2] pixels */
+  const float* keypoints1;    /* [B][N][2] */
+  const float* descriptors0;  /* [B][M][256] */
+  const float* descriptors1;  /* [B][N][256] */
+  const float* scores0;       /* [B][M] keypoint scores (use_scores) */
+  const float* scores1;
+  const float* image_size0;   /* [B][2] (w, h) or null: image_w0 / image_h0 (the image shape) */
+  const float* image_size1;
+  int32_t image_w0, image_h0, image_w1, image_h1;
+} sg_inputs_t;
+
+typedef struct sg_outputs_t {
+  int64_t* matches0;          /* [B][M] */
+  int64_t* matches1;          /* [B][N] */
+  float* matching_scores0;    /* [B][M] */
+  float* matching_scores1;    /* [B][N] */
+  float* sinkhorn_cost;       /* [B][M][N] or null */
+  float* log_assignment;      /* [B][M+1][N+1] or null */
+  float* descriptors0;        /* [B][M][256] GNN output (input of final_proj) or null */
+  float* descriptors1;
+} sg_outputs_t;
+
+typedef struct sg_handle sg_handle_t;
+
+int sg_create(const sg_config_t* cfg, int device, sg_handle_t** out);
+int sg_destroy(sg_handle_t* h);
+/* the state-dict schema (names / element counts) this configuration expects; BatchNorm
+ * num_batches_tracked buffers are not part of it */
+int sg_weight_count(const sg_handle_t* h);
+const char* sg_weight_name(const sg_handle_t* h, int i);
+int64_t sg_weight_numel(const sg_handle_t* h, int i);
+/* device fp32 tensors keyed like the reference state dict; repacked on `stream` (one read-back of
+ * bin_score and the range statistics) */
+int sg_load_weights(sg_handle_t* h, int n, const char* const* names, const float* const* tensors, const int64_t* numels,
+                    void* stream);
+int sg_workspace_bytes(const sg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+/* eval forward; M, N >= 1 (the caller handles the empty case, superglue.py:257-264) */
+int sg_forward(sg_handle_t* h, const sg_inputs_t* in, sg_outputs_t* out, void* workspace, size_t workspace_bytes,
+               void* stream);
+/* NLL of a log assignment [B][M+1][N+1]; gt_assignment [B][M][N] (0/1 bytes), gt_matches [B][M] /
+ * [B][N] (-1 = unmatched).  out [5][B]: nll, nll_pos, nll_neg, num_matchable, num_unmatchable.
+ * mode 0: SuperGlue.loss; mode 1: NLLLoss (requires M == N, as the reference's indexing does) */
+int sg_nll_loss(const float* log_assignment, int32_t B, int32_t M, int32_t N, const uint8_t* gt_assignment,
+                const int64_t* gt_matches0, const int64_t* gt_matches1, int32_t mode, float nll_balancing, float* out,
+                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,156 @@
+"""SuperGlue on the GPU (lightglue_amd.SuperGlue -> sg_forward of liblightglue_mi355x.so) against the
+reference's own outputs (tests/golden/sg_*.npz, tests/golden/make_superglue_golden.py) and the
+CPU oracle (oracle/superglue_ref.py).
+
+Tolerances: the GNN runs on the fp16x3 GEMM / attention kernels (fp32-accurate products of
+22-bit operands) with merge and the eval BatchNorm folded into the MLP's first
+linear; the GNN output is held to 1e-4 absolute (values ~1), the cost (values up to ~6) and the
+log assignment to 2e-3, the matching scores to 1e-4.  Matches are exact wherever the reference's
+top-1 / top-2 gap and the threshold distance (recorded per row and column in the fixture) exceed
+1e-3; the few decisions inside that band may differ and are counted.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.superglue_ref import superglue_forward
+from sg_golden_util import sg_case, sg_case_names, sg_load
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+MARGIN = 1e-3
+
+
+def make_model(conf, sd):
+    from lightglue_amd import SuperGlue
+
+    m = SuperGlue(conf).eval().to(DEV)
+    full = m.state_dict()
+    full.update({k: torch.from_numpy(np.asarray(v).copy()) for k, v in sd.items()})
+    m.load_state_dict(full, strict=True)
+    return m
+
+
+def run(m, data, return_descriptors=True):
+    B = data["keypoints0"].shape[0]
+    d = {k: torch.from_numpy(v).to(DEV) for k, v in data.items() if k not in ("image_size", "image_hw")}
+    hw = data.get("image_hw", (480, 640))
+    view = {"image": torch.zeros(B, 1, *hw, device=DEV)}
+    if data.get("image_size") is not None:
+        view["image_size"] = torch.from_numpy(np.asarray(data["image_size"], np.float32)).to(DEV)
+    with torch.no_grad():
+        out = m({**d, "view0": view, "view1": dict(view)}, return_descriptors=return_descriptors)
+    torch.cuda.synchronize()
+    return {k: v.detach().cpu() for k, v in out.items()}
+
+
+def decided(g):
+    """Rows / columns whose match decision is outside the fp32 noise band."""
+    r = (g["margin_row_gap"] > MARGIN) & (g["margin_row_th"] > MARGIN)
+    c = (g["margin_col_gap"] > MARGIN) & (g["margin_col_th"] > MARGIN)
+    return r, c
+
+
+@pytest.mark.parametrize("name", sg_case_names())
+def test_superglue_matches_reference_golden(name):
+    g = sg_load(name)
+    conf, sd, data, gt = sg_case(g["meta"])
+    out = run(make_model(conf, sd), data)
+    np.testing.assert_allclose(out["gnn_descriptors0"].numpy(), g["gnn_desc0"].transpose(0, 2, 1), atol=1e-4, rtol=0)
+    np.testing.assert_allclose(out["gnn_descriptors1"].numpy(), g["gnn_desc1"].transpose(0, 2, 1), atol=1e-4, rtol=0)
+    np.testing.assert_allclose(out["sinkhorn_cost"].numpy(), g["out_sinkhorn_cost"], atol=2e-3, rtol=0)
+    np.testing.assert_allclose(out["log_assignment"].numpy(), g["out_log_assignment"], atol=2e-3, rtol=0)
+    np.testing.assert_allclose(out["matching_scores0"].numpy(), g["out_matching_scores0"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(out["matching_scores1"].numpy(), g["out_matching_scores1"], atol=1e-4, rtol=0)
+    r, c = decided(g)
+    m0, m1 = out["matches0"].numpy(), out["matches1"].numpy()
+    assert out["matches0"].dtype == torch.int64
+    np.testing.assert_array_equal(m0[r], g["out_matches0"][r])
+    np.testing.assert_array_equal(m1[c], g["out_matches1"][c])
+    print(f"{name}: {(~r).sum()} rows / {(~c).sum()} columns inside the {MARGIN} band, "
+          f"{(m0 != g['out_matches0']).sum()} / {(m1 != g['out_matches1']).sum()} differ")
+
+
+@pytest.mark.parametrize("name", sg_case_names())
+def test_superglue_losses_match_reference(name):
+    """SuperGlue.loss (superglue.py:309-339) and losses.NLLLoss on the reference's log assignment."""
+    from lightglue_amd.superglue import NLLLoss
+
+    g = sg_load(name)
+    conf, sd, data, gt = sg_case(g["meta"])
+    m = make_model(conf, sd)
+    la = torch.from_numpy(g["out_log_assignment"]).to(DEV)
+    gtd = {k: torch.from_numpy(v).to(DEV) for k, v in gt.items()}
+    losses = m.loss({"log_assignment": la}, gtd)
+    for k, v in losses.items():
+        np.testing.assert_allclose(v.detach().cpu().numpy(), g[f"sgloss_{k}"], rtol=1e-5, atol=1e-6, err_msg=k)
+    if g["meta"]["nll_error"] is None:
+        total, w, metrics = NLLLoss({})({"log_assignment": la}, gtd)
+        np.testing.assert_allclose(total.cpu().numpy(), g["nll_total"], rtol=1e-5)
+        for k, v in metrics.items():
+            np.testing.assert_allclose(v.cpu().numpy(), g[f"nll_{k}"], rtol=1e-5, err_msg=k)
+    else:
+        with pytest.raises(RuntimeError, match="must match the existing size"):
+            NLLLoss({})({"log_assignment": la}, gtd)
+
+
+def test_superglue_c_schema_equals_module_schema():
+    from lightglue_amd.sg_weights import superglue_schema
+
+    for conf in ({}, {"use_scores": False, "GNN_layers": ["cross"], "keypoint_encoder": [16]}):
+        m = make_model(conf, {})
+        lib = m._ensure_handle(DEV)
+        names = [lib.sg_weight_name(m._handle, i).decode() for i in range(lib.sg_weight_count(m._handle))]
+        want = [n for n, _, kind in superglue_schema(conf) if kind != "bn_count"]
+        assert names == want
+        assert [lib.sg_weight_numel(m._handle, i) for i in range(len(names))] == \
+            [int(np.prod(s)) if s else 1 for n, s, kind in superglue_schema(conf) if kind != "bn_count"]
+
+
+@pytest.mark.parametrize("B,M,N,conf", [
+    (3, 64, 48, {"GNN_layers": ["self", "cross"] * 2}),
+    (1, 33, 517, {"GNN_layers": ["cross"], "num_sinkhorn_iterations": 10}),
+    (2, 256, 256, {}),
+])
+def test_superglue_matches_oracle(B, M, N, conf):
+    from lightglue_amd.sg_weights import superglue_state_dict, synthetic_scores
+    from lightglue_amd.weights import synthetic_pair
+
+    sd = superglue_state_dict(conf, seed=B + M)
+    p = synthetic_pair(B, M, N, seed=5 + N, width=640, height=480)
+    data = {"keypoints0": p["keypoints0"], "keypoints1": p["keypoints1"], "descriptors0": p["descriptors0"],
+            "descriptors1": p["descriptors1"], "keypoint_scores0": synthetic_scores(B, M, seed=1),
+            "keypoint_scores1": synthetic_scores(B, N, seed=2), "image_size": np.tile([[640.0, 480.0]], (B, 1)).astype(np.float32)}
+    with torch.no_grad():
+        ref = superglue_forward(sd, data, conf, dtype=torch.float64)
+    out = run(make_model(conf, sd), data)
+    np.testing.assert_allclose(out["gnn_descriptors0"].numpy(), ref["gnn_desc0"].transpose(1, 2).numpy(), atol=1e-4)
+    np.testing.assert_allclose(out["log_assignment"].numpy(), ref["log_assignment"].numpy(), atol=2e-3)
+    la = ref["log_assignment"][:, :-1, :-1]
+    top = la.topk(2, dim=2).values
+    ok = ((top[..., 0] - top[..., 1]) > MARGIN).numpy() & (np.abs(top[..., 0].exp().numpy() - 0.2) > MARGIN)
+    np.testing.assert_array_equal(out["matches0"].numpy()[ok], ref["matches0"].numpy()[ok])
+    assert ok.mean() > 0.9
+
+
+def test_superglue_weight_reload_and_errors():
+    """Replacing a parameter / buffer reloads the packed weights; CPU inputs and training raise."""
+    from lightglue_amd.sg_weights import superglue_state_dict
+    from lightglue_amd.weights import synthetic_pair
+
+    conf = {"GNN_layers": ["self", "cross"]}
+    sd = superglue_state_dict(conf, seed=3)
+    m = make_model(conf, sd)
+    p = synthetic_pair(1, 40, 40, seed=2, width=640, height=480)
+    data = {**{k: v for k, v in p.items() if not k.startswith("image_size")}, "image_hw": (480, 640),
+            "keypoint_scores0": np.full((1, 40), 0.5, np.float32), "keypoint_scores1": np.full((1, 40), 0.5, np.float32)}
+    a = run(m, data)
+    with torch.no_grad():
+        m.gnn.layers[1].mlp[1].running_var.mul_(4.0)  # a buffer (folded into mlp.0 at load time)
+    b = run(m, data)
+    assert not torch.equal(a["gnn_descriptors0"], b["gnn_descriptors0"])
+    ref = superglue_forward({k: (v if k != "gnn.layers.1.mlp.1.running_var" else v * 4) for k, v in sd.items()}, data, conf)
+    np.testing.assert_allclose(b["gnn_descriptors0"].numpy(), ref["gnn_desc0"].transpose(1, 2).numpy(), atol=1e-4)
+    m.train()
+    with pytest.raises(NotImplementedError):
+        run(m, data)

@@ -21,7 +21,7 @@ def declared_symbols():
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        syms |= set(re.findall(r"\b((?:lg|sp)_[a-z_0-9]+)\s*\(", src))
+        syms |= set(re.findall(r"\b((?:lg|sp|sg)_[a-z_0-9]+)\s*\(", src))
     return syms
 
 
@@ -41,9 +41,11 @@ def test_ctypes_structs_match_header_layout(tmp_path):
     import subprocess
 
     structs = {"lg_config_t": _lib.LGConfig, "lg_inputs_t": _lib.LGInputs, "lg_outputs_t": _lib.LGOutputs,
-               "sp_config_t": _lib.SPConfig, "sp_inputs_t": _lib.SPInputs, "sp_outputs_t": _lib.SPOutputs}
+               "sp_config_t": _lib.SPConfig, "sp_inputs_t": _lib.SPInputs, "sp_outputs_t": _lib.SPOutputs,
+               "sg_config_t": _lib.SGConfig, "sg_inputs_t": _lib.SGInputs, "sg_outputs_t": _lib.SGOutputs}
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{os.path.join(ROOT, "include", "lightglue_mi355x.h")}"',
-             f'#include "{os.path.join(ROOT, "include", "superpoint_mi355x.h")}"', "int main(void) {"]
+             f'#include "{os.path.join(ROOT, "include", "superpoint_mi355x.h")}"',
+             f'#include "{os.path.join(ROOT, "include", "superglue_mi355x.h")}"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
         for f, _ in py._fields_:
@@ -171,3 +173,39 @@ def test_superpoint_cpu_input_raises():
 
     with pytest.raises(RuntimeError, match="HIP device"):
         SuperPoint({})({"image": torch.zeros(1, 1, 64, 64)})
+
+
+def test_superglue_module_schema_matches_reference_schema():
+    """The parameter containers' state dict is the reference's (superglue.py:63-139,239-247)."""
+    from lightglue_amd import SuperGlue
+    from lightglue_amd.sg_weights import superglue_schema
+
+    for conf in ({}, {"use_scores": False, "GNN_layers": ["cross", "self"]}, {"keypoint_encoder": [16, 64]}):
+        sd = SuperGlue(conf).state_dict()
+        schema = superglue_schema(conf)
+        assert list(sd.keys()) == [n for n, _, _ in schema]
+        for n, shape, _ in schema:
+            assert tuple(sd[n].shape) == tuple(shape), n
+
+
+def test_superglue_registry_and_cpu_inputs_raise():
+    import torch
+
+    from lightglue_amd import SuperGlue
+    from lightglue_amd.pipeline import get_model
+
+    assert get_model("gluefactory_nonfree.superglue") is SuperGlue and get_model("superglue") is SuperGlue
+    m = SuperGlue({"GNN_layers": ["self"]}).eval()
+    view = {"image": torch.zeros(1, 1, 48, 64)}
+    data = {"view0": view, "view1": view, "keypoints0": torch.rand(1, 5, 2) * 40,
+            "keypoints1": torch.rand(1, 6, 2) * 40, "descriptors0": torch.rand(1, 5, 256),
+            "descriptors1": torch.rand(1, 6, 256), "keypoint_scores0": torch.rand(1, 5),
+            "keypoint_scores1": torch.rand(1, 6)}
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m(data)
+    # empty view: the reference's early return (superglue.py:257-264), int32 matches
+    out = m({**data, "keypoints1": torch.zeros(1, 0, 2), "descriptors1": torch.zeros(1, 0, 256),
+             "keypoint_scores1": torch.zeros(1, 0)})
+    assert out["matches0"].dtype == torch.int32 and (out["matches0"] == -1).all() and out["matches1"].shape == (1, 0)
+    with pytest.raises(ValueError):
+        SuperGlue({"GNN_layers": ["self", "both"]})

@@ -661,21 +661,30 @@ hipError_t gemm_h3_ln_launch(const GemmH3Args& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Tile choice.  The 256 x 256 (16-wave) tile is the throughput shape; when it would leave most
-// of the 256 CUs idle (fewer tiles than CUs: B = 1 forwards, pruned token sets) the 64 x 64
-// single-wave tile spreads the same work over 16x more workgroups.  LG_GEMM_TILE=big|small
-// overrides the choice (tests run both on the golden cases).
-enum { TILE_AUTO, TILE_BIG, TILE_SMALL };
+// Tile choice.  The 256 x 256 (16-wave) tile is the throughput shape; when it would leave CUs
+// idle (fewer tiles than CUs) the 128 x 128 four-wave tile (two workgroups per CU) keeps the MFMA
+// density while quadrupling the tile count (SuperGlue's B = 16, N = 1024 row space), and when even
+// that leaves most CUs idle (B = 1 forwards, pruned token sets) the 64 x 64 single-wave tile
+// spreads the work over 16x more workgroups.  LG_GEMM_TILE=big|medium|small overrides the choice
+// (tests run each on the golden cases).
+enum { TILE_AUTO, TILE_BIG, TILE_SMALL, TILE_MEDIUM };
 static int gemm_tile_override() {
   const char* e = getenv("LG_GEMM_TILE");
   if (!e) return TILE_AUTO;
   if (!strcmp(e, "big")) return TILE_BIG;
   if (!strcmp(e, "small")) return TILE_SMALL;
+  if (!strcmp(e, "medium")) return TILE_MEDIUM;
   return TILE_AUTO;
 }
 static bool use_small_tiles(long long big_tiles) {
   const int o = gemm_tile_override();
   return o == TILE_SMALL || (o == TILE_AUTO && big_tiles < 256);
+}
+static int gemm_tile_for(long long big_tiles) {
+  const int o = gemm_tile_override();
+  if (o != TILE_AUTO) return o;
+  if (big_tiles >= 256) return TILE_BIG;
+  return 4 * big_tiles >= 512 ? TILE_MEDIUM : TILE_SMALL;  // 128 x 128: two workgroups per CU
 }
 
 #ifndef LG_GEMM_H3_TILE
@@ -699,8 +708,11 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
     if (use_small_tiles((a.R + 127) / 128)) return gemm_h3_ln_launch<64, 64>(a, st);
     return gemm_h3_ln_launch<LG_GEMM_LN_WN>(a, st);
   }
-  if (use_small_tiles((long long)((a.R + TB - 1) / TB) * (a.Nout / TB))) return gemm_h3_launch<64, 4, 64, 64>(a, epi, st);
-  return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
+  switch (gemm_tile_for((long long)((a.R + TB - 1) / TB) * (a.Nout / TB))) {
+    case TILE_SMALL: return gemm_h3_launch<64, 4, 64, 64>(a, epi, st);
+    case TILE_MEDIUM: return gemm_h3_launch<128, 2, 128, 64>(a, epi, st);
+    default: return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
+  }
 }
 
 // fp32 rows -> plane image (scaled by 2^-E, RangeOut); one thread per 8-element chunk

@@ -370,15 +370,18 @@ struct SgEncLayer {
   const float* b;
   const float *bn_w, *bn_b, *bn_mean, *bn_var;  // eval BatchNorm (all layers but the last)
 };
-// x[r] = desc[r] + MLP([x_n, y_n(, score)]) for rows r of one image set (rows = B * n, 256 wide);
-// keypoints normalised by size[b] (w, h) or (fw, fh) (superglue.py:75-86)
+// The first nl layers of the keypoint MLP for rows r of one image set (rows = B * n): out[r] =
+// (desc[r] +) layers(x_n, y_n(, score)), row stride ldo; keypoints normalised by size[b] (w, h) or
+// (fw, fh) (superglue.py:75-86).  Widths multiples of 4, at most 256.  A layer with bn_w set is
+// followed by its BatchNorm and ReLU.
 struct SgEncArgs {
   const float* kpts;
   const float* scores;  // null without use_scores
   const float* size;
   float fw, fh;
-  const float* desc;
-  float* x;
+  const float* desc;    // null: out = the last layer's output alone
+  float* out;
+  int ldo;
   int rows, n, nl;
   int ch[kSgMaxEnc + 1];
   SgEncLayer layer[kSgMaxEnc];

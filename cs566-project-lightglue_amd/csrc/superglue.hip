@@ -15,11 +15,13 @@ constexpr int kEncMaxC = 256;
 }  // namespace
 
 // One workgroup = 32 keypoints of one image set; activations in LDS, layer by layer.  Layer l:
-// out[o] = b[o] + sum_c Wt[c][o] in[c] (sequential over c, fp32), then eval BatchNorm in ATen's
-// CPU form (alpha = w / sqrt(var + eps), out * alpha + (b - mean * alpha)) and ReLU, except after
-// the last layer, whose output is added to the descriptor row: x = desc + enc.
+// out[o] = b[o] + sum_c Wt[c][o] in[c] (sequential over c, fp32; a thread computes 4 consecutive
+// outputs of one keypoint from float4 weight reads), then -- where the layer has a BatchNorm --
+// eval BatchNorm in ATen's CPU form (alpha = w / sqrt(var + eps), out * alpha + (b - mean * alpha))
+// and ReLU.  The last layer computed here writes global rows: out[r] = (desc[r] +) value.
 __global__ __launch_bounds__(256) void sg_kenc_kernel(SgEncArgs a) {
-  __shared__ float act[2][kEncRows][kEncMaxC + 1];
+  constexpr int AS = kEncMaxC + 4;  // LDS row stride (float4-aligned rows)
+  __shared__ __attribute__((aligned(16))) float act[2][kEncRows][AS];
   const int tid = threadIdx.x;
   const int row0 = blockIdx.x * kEncRows;
   const int nrow = min(kEncRows, a.rows - row0);
@@ -42,21 +44,37 @@ __global__ __launch_bounds__(256) void sg_kenc_kernel(SgEncArgs a) {
   __syncthreads();
   int cur = 0;
   for (int l = 0; l < a.nl; ++l) {
-    const int cin = a.ch[l], cout = a.ch[l + 1];
+    const int cin = a.ch[l], cout = a.ch[l + 1], og = cout / 4;
     const SgEncLayer& L = a.layer[l];
     const bool last = l == a.nl - 1;
-    for (int idx = tid; idx < kEncRows * cout; idx += blockDim.x) {
-      const int k = idx / cout, o = idx - k * cout;
-      float acc = 0.f;
-      for (int c = 0; c < cin; ++c) acc = fmaf(L.Wt[(size_t)c * cout + o], act[cur][k][c], acc);
-      acc += L.b[o];
+    for (int idx = tid; idx < kEncRows * og; idx += blockDim.x) {
+      const int k = idx / og, o = (idx - k * og) * 4;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < cin; ++c) {
+        const float x = act[cur][k][c];
+        const f32x4 w = *reinterpret_cast<const f32x4*>(L.Wt + (size_t)c * cout + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = fmaf(w[e], x, acc[e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[e] += L.b[o + e];
+        if (L.bn_w) {
+          const float alpha = L.bn_w[o + e] * (1.f / sqrtf(L.bn_var[o + e] + 1e-5f));
+          const float beta = L.bn_b[o + e] - L.bn_mean[o + e] * alpha;
+          acc[e] = fmaxf(acc[e] * alpha + beta, 0.f);
+        }
+      }
       if (!last) {
-        const float alpha = L.bn_w[o] * (1.f / sqrtf(L.bn_var[o] + 1e-5f));
-        const float beta = L.bn_b[o] - L.bn_mean[o] * alpha;
-        act[cur ^ 1][k][o] = fmaxf(acc * alpha + beta, 0.f);
+        *reinterpret_cast<f32x4*>(&act[cur ^ 1][k][o]) = acc;
       } else if (k < nrow) {
         const size_t r = (size_t)(row0 + k);
-        a.x[r * kEncMaxC + o] = a.desc[r * kEncMaxC + o] + acc;
+        if (a.desc) {
+          const f32x4 d = *reinterpret_cast<const f32x4*>(a.desc + r * kEncMaxC + o);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] = d[e] + acc[e];
+        }
+        *reinterpret_cast<f32x4*>(a.out + r * a.ldo + o) = acc;
       }
     }
     __syncthreads();
@@ -66,10 +84,11 @@ __global__ __launch_bounds__(256) void sg_kenc_kernel(SgEncArgs a) {
 
 hipError_t sg_keypoint_encoder(const SgEncArgs& a, hipStream_t st) {
   if (a.rows <= 0) return hipSuccess;
-  if (a.nl < 1 || a.nl > kSgMaxEnc || a.ch[0] < 2 || a.ch[0] > 3 || a.ch[a.nl] != kEncMaxC || a.n <= 0)
+  if (a.nl < 1 || a.nl > kSgMaxEnc || a.ch[0] < 2 || a.ch[0] > 3 || a.n <= 0 || !a.out || a.ldo < a.ch[a.nl] ||
+      (a.desc && a.ch[a.nl] != kEncMaxC))
     return hipErrorInvalidValue;
-  for (int l = 1; l < a.nl; ++l)
-    if (a.ch[l] <= 0 || a.ch[l] > kEncMaxC) return hipErrorInvalidValue;
+  for (int l = 1; l <= a.nl; ++l)
+    if (a.ch[l] <= 0 || a.ch[l] > kEncMaxC || a.ch[l] % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(sg_kenc_kernel, dim3((a.rows + kEncRows - 1) / kEncRows), dim3(256), 0, st, a);
   return hipGetLastError();
 }

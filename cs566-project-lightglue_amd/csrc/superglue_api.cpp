@@ -177,6 +177,10 @@ struct sg_handle {
   };
   std::vector<Enc> enc;
   std::vector<int> ch;
+  // the encoder's last layer as an fp16x3 GEMM with the descriptor add as its residual (its input
+  // width a multiple of 32 and at least one hidden layer); otherwise the whole MLP in VALU
+  bool enc_gemm = false;
+  Mat enc_last{};
   float bin_score = 1.f;
   bool loaded = false;
 };
@@ -189,8 +193,8 @@ int sg_create(const sg_config_t* cfg, int device, sg_handle_t** out) {
   if (cfg->n_layers < 0 || cfg->n_layers > SG_MAX_LAYERS) return fail(LG_E_INVALID, "n_layers out of range");
   if (cfg->n_kenc < 0 || cfg->n_kenc > SG_MAX_KENC) return fail(LG_E_INVALID, "keypoint_encoder too long");
   for (int i = 0; i < cfg->n_kenc; ++i)
-    if (cfg->keypoint_encoder[i] <= 0 || cfg->keypoint_encoder[i] > 256)
-      return fail(LG_E_INVALID, "keypoint_encoder widths must be in [1, 256]");
+    if (cfg->keypoint_encoder[i] <= 0 || cfg->keypoint_encoder[i] > 256 || cfg->keypoint_encoder[i] % 4)
+      return fail(LG_E_INVALID, "keypoint_encoder widths must be multiples of 4 in [4, 256]");
   for (int i = 0; i < cfg->n_layers; ++i)
     if (cfg->layer_types[i] != 0 && cfg->layer_types[i] != 1) return fail(LG_E_INVALID, "GNN layer must be self or cross");
   if (cfg->sinkhorn_iterations < 0) return fail(LG_E_INVALID, "num_sinkhorn_iterations must be >= 0");
@@ -201,6 +205,7 @@ int sg_create(const sg_config_t* cfg, int device, sg_handle_t** out) {
   h->schema = make_schema(*cfg);
   for (size_t k = 0; k < h->schema.size(); ++k) h->index[h->schema[k].name] = (int)k;
   h->ch = kenc_channels(*cfg);
+  h->enc_gemm = h->ch.size() >= 3 && h->ch[h->ch.size() - 2] % 32 == 0;
   *out = h;
   return LG_OK;
 }
@@ -276,6 +281,8 @@ int sg_load_weights(sg_handle_t* h, int n, const char* const* names, const float
     ly.w2 = {take(2 * D * D), take(D), D, 2 * D, 0, 0.f, 0.f, 0.f};
   }
   h->fin = {take(D * D), take(D), D, D, 0, 0.f, 0.f, 0.f};
+  const int kl = h->ch[h->ch.size() - 2];
+  if (h->enc_gemm) h->enc_last = {take((size_t)D * kl), take(D), D, kl, 0, 0.f, 0.f, 0.f};
   float* tmp = nullptr;
   if (h->buf) (void)hipFree(h->buf);
   h->buf = nullptr;
@@ -319,6 +326,11 @@ int sg_load_weights(sg_handle_t* h, int n, const char* const* names, const float
     SG_HIP(hipMemcpyAsync(B + ly.w2.off, raw(p + ".mlp.3.weight"), 2 * D * D * sizeof(float), hipMemcpyDeviceToDevice, st));
     SG_HIP(hipMemcpyAsync(B + ly.w2.boff, raw(p + ".mlp.3.bias"), D * sizeof(float), hipMemcpyDeviceToDevice, st));
   }
+  if (h->enc_gemm) {
+    const std::string p = "kenc.encoder." + std::to_string(3 * (h->ch.size() - 2));
+    SG_HIP(hipMemcpyAsync(B + h->enc_last.off, raw(p + ".weight"), (size_t)D * kl * sizeof(float), hipMemcpyDeviceToDevice, st));
+    SG_HIP(hipMemcpyAsync(B + h->enc_last.boff, raw(p + ".bias"), D * sizeof(float), hipMemcpyDeviceToDevice, st));
+  }
   SG_HIP(hipMemcpyAsync(B + h->fin.off, raw("final_proj.weight"), D * D * sizeof(float), hipMemcpyDeviceToDevice, st));
   SG_HIP(hipMemcpyAsync(B + h->fin.boff, raw("final_proj.bias"), D * sizeof(float), hipMemcpyDeviceToDevice, st));
   SG_HIP(hipFreeAsync(tmp, st));
@@ -331,6 +343,7 @@ int sg_load_weights(sg_handle_t* h, int n, const char* const* names, const float
     mats.push_back(&ly.w2);
   }
   mats.push_back(&h->fin);
+  if (h->enc_gemm) mats.push_back(&h->enc_last);
   size_t total = 0;
   for (auto* m : mats) total += 2 * (size_t)m->rows * m->K;
   if (h->planes) (void)hipFree(h->planes);
@@ -424,7 +437,16 @@ int sg_forward(sg_handle_t* h, const sg_inputs_t* in, sg_outputs_t* out, void* w
   };
   SG_HIP(hipMemsetAsync(rt, 0, kSlots * kRangeStride * sizeof(unsigned), st));
 
-  // ---- keypoint encoder + descriptors -> x (superglue.py:266-276)
+  // ---- keypoint encoder + descriptors -> x (superglue.py:266-276).  enc_gemm: the hidden layers
+  // in VALU into fp32 rows, their plane image, then the last layer as an fp16x3 GEMM whose residual
+  // is the descriptor rows (x = desc + W h + b, written as fp32 rows and as x's plane image)
+  const int nl_all = (int)h->enc.size();
+  const int nl_valu = h->enc_gemm ? nl_all - 1 : nl_all;
+  const int kl = h->ch[nl_valu];
+  if (h->enc_gemm) {
+    SG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
+    SG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
+  }
   for (int s = 0; s < 2; ++s) {
     SgEncArgs e;
     memset(&e, 0, sizeof(e));
@@ -433,11 +455,19 @@ int sg_forward(sg_handle_t* h, const sg_inputs_t* in, sg_outputs_t* out, void* w
     e.size = s ? in->image_size1 : in->image_size0;
     e.fw = (float)(s ? in->image_w1 : in->image_w0);
     e.fh = (float)(s ? in->image_h1 : in->image_h0);
-    e.desc = s ? in->descriptors1 : in->descriptors0;
-    e.x = w.X + (s ? (size_t)B * M * D : 0);
     e.n = s ? N : M;
     e.rows = B * e.n;
-    e.nl = (int)h->enc.size();
+    const size_t r0 = s ? (size_t)B * M : 0;
+    if (h->enc_gemm) {
+      e.desc = nullptr;
+      e.out = w.ctx + r0 * kl;  // hidden rows [R][kl] (w.ctx is free until the first attention)
+      e.ldo = kl;
+    } else {
+      e.desc = s ? in->descriptors1 : in->descriptors0;
+      e.out = w.X + r0 * D;
+      e.ldo = D;
+    }
+    e.nl = nl_valu;
     for (int l = 0; l <= e.nl; ++l) e.ch[l] = h->ch[l];
     for (int l = 0; l < e.nl; ++l) {
       e.layer[l].Wt = W + h->enc[l].wt;
@@ -451,10 +481,29 @@ int sg_forward(sg_handle_t* h, const sg_inputs_t* in, sg_outputs_t* out, void* w
     }
     SG_HIP(sg_keypoint_encoder(e, st));
   }
-  const int s_in = slot();
-  int s_x = slot();
-  SG_HIP(range_absmax(w.X, (size_t)R * D, rt, s_in, st));
-  SG_HIP(rows_to_planes(w.X, R, D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st));
+  int s_x = -1;
+  if (h->enc_gemm) {
+    const int s_d = slot(), s_hr = slot(), s_he = slot();
+    s_x = slot();
+    SG_HIP(range_absmax(in->descriptors0, (size_t)B * M * D, rt, s_d, st));
+    SG_HIP(range_absmax(in->descriptors1, (size_t)B * N * D, rt, s_d, st));
+    SG_HIP(range_absmax(w.ctx, (size_t)R * kl, rt, s_hr, st));
+    SG_HIP(rows_to_planes(w.ctx, R, kl, kl, w.Hp, RP, 0, ro(s_hr, 1.f, -1, 0.f, 0.f, s_he, 1), st));
+    GemmH3Args g;
+    memset(&g, 0, sizeof(g));
+    g.out_scale = 1.f;
+    g.A0 = image(w.Hp, kl); g.K0 = kl; g.K = kl; wplanes(g, h->enc_last);
+    g.rtab = rt; g.a0_slot = s_he; g.a1_slot = -1;
+    g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
+    g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP;
+    g.ro = ro(s_d, 1.f, s_he, h->enc_last.g, h->enc_last.bmax, s_x, 1);
+    SG_HIP(gemm_h3(g, EPI_STORE, st));
+  } else {
+    const int s_in = slot();
+    s_x = slot();
+    SG_HIP(range_absmax(w.X, (size_t)R * D, rt, s_in, st));
+    SG_HIP(rows_to_planes(w.X, R, D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st));
+  }
 
   // ---- AttentionalGNN (superglue.py:148-170)
   const size_t img1 = (size_t)B * H * M * HD;

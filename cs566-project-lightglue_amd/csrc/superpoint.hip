@@ -644,7 +644,8 @@ hipError_t sp_conv3x3(const ConvH3Args& a, hipStream_t st) {
       a.Wt.rows_pad != a.Cout || a.yrows_pad < rout || a.X.rows_pad > (1 << 26))  // 32-bit DMA byte offsets
     return hipErrorInvalidValue;
   if (a.pool && (a.H < 2 || a.W < 2)) return hipErrorInvalidValue;
-  static const bool gather = getenv("LG_SP_CONV") && !strcmp(getenv("LG_SP_CONV"), "gather");
+  const char* conv = getenv("LG_SP_CONV");  // read per launch (tests flip it between calls)
+  const bool gather = conv && !strcmp(conv, "gather");
   if (!gather) {  // halo tiles (default); LG_SP_CONV=gather: the per-tap row gather above
     if (a.Cout % 128 == 0) return a.pool ? sp_conv3x3_halo_launch<128, true>(a, st) : sp_conv3x3_halo_launch<128, false>(a, st);
     return a.pool ? sp_conv3x3_halo_launch<64, true>(a, st) : sp_conv3x3_halo_launch<64, false>(a, st);

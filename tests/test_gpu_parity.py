@@ -119,11 +119,12 @@ def test_forward_matches_reference_golden(name, precision):
 
 
 @pytest.mark.parametrize("tile,waves,assign,kernel", [("big", "8", "sim_h3", "h3g"), ("small", "4", "x6_fused", "h3m"),
-                                                       ("small", "2", "x6_unfused", "h3g"), ("big", "2", "sim_h3", "h3m")])
+                                                       ("small", "2", "x6_unfused", "h3g"), ("big", "2", "sim_h3", "h3m"),
+                                                       ("medium", "4", "sim_h3", "h3g")])
 @pytest.mark.parametrize("name", case_names())
 def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, monkeypatch):
-    """The fp16x3 GEMM picks 256x256 tiles (throughput) or 64x64 tiles (fewer big tiles than CUs,
-    e.g. B = 1) by row count, and the attention 8, 4 or 2 waves (256/128/64 queries) per
+    """The fp16x3 GEMM picks 256x256 tiles (throughput), 128x128 tiles (fewer big tiles than CUs)
+    or 64x64 tiles (fewer than a quarter, e.g. B = 1) by row count, and the attention 8, 4 or 2 waves (256/128/64 queries) per
     workgroup, and the assignment either recomputes the similarity inside two fp16x3 GEMM passes
     (M, N multiples of 16, no pruning: sim_h3) or materialises it with the bf16x6 GEMM and runs
     the two-read fused passes (N % 4 == 0, N <= 2048) or the four-read ones; LG_GEMM_TILE /

@@ -154,3 +154,15 @@ def test_superglue_weight_reload_and_errors():
     m.train()
     with pytest.raises(NotImplementedError):
         run(m, data)
+
+
+@pytest.mark.parametrize("tile", ["big", "medium", "small"])
+def test_superglue_golden_under_every_gemm_tile(tile, monkeypatch):
+    monkeypatch.setenv("LG_GEMM_TILE", tile)
+    g = sg_load("sg_b2_m96_n160")
+    conf, sd, data, gt = sg_case(g["meta"])
+    out = run(make_model(conf, sd), data)
+    np.testing.assert_allclose(out["gnn_descriptors0"].numpy(), g["gnn_desc0"].transpose(0, 2, 1), atol=1e-4, rtol=0)
+    np.testing.assert_allclose(out["log_assignment"].numpy(), g["out_log_assignment"], atol=2e-3, rtol=0)
+    r, c = decided(g)
+    np.testing.assert_array_equal(out["matches0"].numpy()[r], g["out_matches0"][r])

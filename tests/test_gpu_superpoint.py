@@ -180,3 +180,13 @@ def test_superpoint_feeds_lightglue_through_the_pipeline():
                                "view0": view, "view1": view})
     torch.testing.assert_close(pred["matches0"], direct["matches0"], rtol=0, atol=0)
     torch.testing.assert_close(pred["matching_scores0"], direct["matching_scores0"], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("name", ["sp_gray_b1_120x160", "sp_odd_b1_100x132_fix"])
+def test_superpoint_gather_convolution_matches_reference(name, monkeypatch):
+    """The per-tap gather convolution (LG_SP_CONV=gather) against the same goldens."""
+    monkeypatch.setenv("LG_SP_CONV", "gather")
+    g = sp_load(name)
+    conf, sd, data = sp_case_inputs(g["meta"])
+    out = run(make_model(conf, sd), data)
+    assert_same_keypoints(out, g["out_keypoints"], g["out_keypoint_scores"], g["out_descriptors"])

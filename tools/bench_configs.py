@@ -155,13 +155,45 @@ def cfg_sp(dev, reps, B=16, H=480, W=640, k=2048):
             "keypoints": list(pred["keypoints"].shape)}
 
 
+def sg_flops(B, M, N, L=18, D=256):
+    """Dense flops of a SuperGlue forward (GNN + final_proj + cost; the encoder and Sinkhorn are
+    not counted): per layer q/k/v + mlp.0 (merge folded) + mlp.3 on both images, attention
+    (QK^T and PV per head)."""
+    R = B * (M + N)
+    per_layer = 2 * R * D * (3 * D + 2 * D * 2 * D // D + 2 * D) + 2 * 2 * B * (M * N + N * M) * D
+    return L * per_layer + 2 * R * D * D + 2 * B * M * N * D
+
+
+def cfg_sg(dev, reps, B=16, N=1024):
+    """SuperGlue (§8f row 4): B pairs of N keypoints, 18 GNN layers, 50 Sinkhorn iterations."""
+    from lightglue_amd import SuperGlue
+    from lightglue_amd.sg_weights import superglue_state_dict, synthetic_scores
+    from lightglue_amd.weights import synthetic_pair
+
+    m = SuperGlue({}).eval().to(dev)
+    sd = m.state_dict()
+    sd.update({n: torch.from_numpy(v) for n, v in superglue_state_dict({}, seed=0).items()})
+    m.load_state_dict(sd)
+    p = synthetic_pair(B, N, N, seed=1, width=640, height=480)
+    view = {"image_size": torch.tensor([[640.0, 480.0]] * B, device=dev)}
+    data = {k: torch.from_numpy(v).to(dev) for k, v in p.items() if not k.startswith("image_size")}
+    data.update({"keypoint_scores0": torch.from_numpy(synthetic_scores(B, N, 2)).to(dev),
+                 "keypoint_scores1": torch.from_numpy(synthetic_scores(B, N, 3)).to(dev), "view0": view, "view1": view})
+    with torch.no_grad():
+        s, pred = timed(lambda: m(data), reps)
+    fl = sg_flops(B, N, N)
+    return {"config": f"SuperGlue N={N}, 18 GNN layers, 50 Sinkhorn iterations, batch={B}", "value": round(B / s, 2),
+            "unit": "image-pairs/s", "ms_per_pair": round(1e3 * s / B, 3), "dense_tflops_wall": round(fl / s / 1e12, 1),
+            "matches_per_pair": float((pred["matches0"] >= 0).sum()) / B}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="1,3,4")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    fns = {"1": cfg1, "3": cfg3, "4": cfg4, "sp": cfg_sp}
+    fns = {"1": cfg1, "3": cfg3, "4": cfg4, "sp": cfg_sp, "sg": cfg_sg}
     for k in a.only.split(","):
         print(json.dumps(fns[k](dev, a.reps)), flush=True)
 

@@ -276,4 +276,27 @@ __device__ __forceinline__ float log_sigmoid(float x) {
   return fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
 }
 
+// GELU(y) = y Phi(y) (nn.GELU(), erf form) without erff's branches: Phi(-|y|) = erfc(|y| / sqrt2) / 2
+// from the Chebyshev fit of erfc (Numerical Recipes' erfcc, fractional error < 1.2e-7 for all
+// arguments), y Phi(y) = y - y Phi(-y) for y >= 0.  Measured over every fp32 y in [-14, 14]:
+// |error| <= 2.4e-7 against fp64 (0.5 y (1 + erff(y / sqrt2)) itself: 4.5e-7).  ~15 VALU ops,
+// a third of erff's divergent two-branch polynomial -- the LN epilogue's GELU pass was 40 us of
+// the ffn.0 GEMM's 269 (tools/kbench_gemm.hip, LG_LN_PROBE).
+__device__ __forceinline__ float gelu_erf(float y) {
+  const float z = fabsf(y) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float h = 0.5f * t * __builtin_amdgcn_exp2f((p - z * z) * 1.4426950408889634f);
+  return y >= 0.f ? fmaf(-y, h, y) : y * h;
+}
+
 }  // namespace lg

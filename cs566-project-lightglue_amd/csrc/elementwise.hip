@@ -110,8 +110,8 @@ __global__ __launch_bounds__(256) void ln_gelu_kernel(float* x, const float* g, 
     for (int i = 0; i < 4; ++i) {
       float y0 = (v0[i] - mean) * rstd * g0[i] + b0[i];
       float y1 = (v1[i] - mean) * rstd * g1[i] + b1[i];
-      v0[i] = 0.5f * y0 * (1.f + erff(y0 * 0.70710678118654752f));
-      v1[i] = 0.5f * y1 * (1.f + erff(y1 * 0.70710678118654752f));
+      v0[i] = gelu_erf(y0);
+      v1[i] = gelu_erf(y1);
     }
     if (!planes) {
       *reinterpret_cast<f32x4*>(xr + lane * 4) = v0;

@@ -59,6 +59,9 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 }
 }  // namespace
 
+#ifndef LG_LN_PROBE
+#define LG_LN_PROBE 0  // timing probes of the LN epilogue (tools/kbench_gemm.hip only): 1 no GELU, 2 no stores
+#endif
 #ifndef LG_GEMM_SETPRIO
 #define LG_GEMM_SETPRIO 0
 #endif
@@ -351,7 +354,11 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
       visit(i, [&](int rr, int c, float v) {
         const int lr = wm0 + i * 32 + rr;
         const float y = (v - mean_s[lr]) * rstd_s[lr] * gj[c / LC] + bj[c / LC];
-        ep[rr * 64 + (c ^ ((rr & 1) << 2))] = 0.5f * y * (1.f + erff(y * 0.70710678118654752f));
+#if LG_LN_PROBE & 1
+        ep[rr * 64 + (c ^ ((rr & 1) << 2))] = y;
+#else
+        ep[rr * 64 + (c ^ ((rr & 1) << 2))] = gelu_erf(y);
+#endif
         return v;
       });
       {
@@ -363,7 +370,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
           const int sw = (rr & 1) << 2;
           const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + (cq ^ sw));
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
-          if (row < g.R && row_live(g.rm, row)) {
+          if (!(LG_LN_PROBE & 2) && row < g.R && row_live(g.rm, row)) {
             f16x8 h, l;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {

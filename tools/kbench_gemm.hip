@@ -42,7 +42,7 @@ double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out,
   return ms / iters;
 }
 
-template <int WN>
+template <int WN, int EPI = EPI_LN_GELU>
 double run_ln(const Shape& s, float* bias, float* gam, float* bet, _Float16* Yp, int iters, int stagger = 0) {
   GemmH3Args a;
   memset(&a, 0, sizeof(a));
@@ -53,10 +53,15 @@ double run_ln(const Shape& s, float* bias, float* gam, float* bet, _Float16* Yp,
   a.Yp = Yp; a.yps = (long long)s.R * s.N; a.yrows_pad = s.R;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  CK(gemm_h3_ln_launch<WN>(a, 0));
+  auto launch = [&]() {
+    if (EPI == EPI_LN_GELU) return gemm_h3_ln_launch<WN>(a, 0);
+    hipLaunchKernelGGL((gemm_h3_kernel<EPI_PROBE, 128, 2, 512, WN>), dim3((a.R + 127) / 128), dim3(2 * (512 / WN) * 64), 0, 0, a);
+    return hipGetLastError();
+  };
+  CK(launch());
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK(gemm_h3_ln_launch<WN>(a, 0));
+  for (int i = 0; i < iters; ++i) CK(launch());
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -154,6 +159,7 @@ int main() {
       ms = run_h3<256, 2>(s, bias, Y, it, true, Yp, stg); rep(nm, ms, true);
     }
     if (s.N == 512) {
+      ms = run_ln<64, EPI_PROBE>(s, bias, nullptr, nullptr, Yp, it); rep("h3  128x512 x2, no epilogue", ms, false);
       float *gam, *bet;
       CK(hipMalloc(&gam, s.N * 4)); CK(hipMalloc(&bet, s.N * 4));
       fill<<<(s.N + 255) / 256, 256>>>(gam, s.N, 4);

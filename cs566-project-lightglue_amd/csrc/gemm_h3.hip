@@ -62,6 +62,12 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 #ifndef LG_LN_PROBE
 #define LG_LN_PROBE 0  // timing probes of the LN epilogue (tools/kbench_gemm.hip only): 1 no GELU, 2 no stores
 #endif
+#ifndef LG_GEMM_DIAG
+// timing probes of the k-loop (tools/kbench_gemm.hip only; results are wrong under 1, 2, 4):
+// 1 every tile reads one of 8 row panels (L2-resident A), 2 no k-tile copies, 4 no vmcnt waits,
+// 8 the copies issued by the first NW/4 waves only, 16 A pieces only, 32 W pieces only
+#define LG_GEMM_DIAG 0
+#endif
 #ifndef LG_GEMM_SETPRIO
 #define LG_GEMM_SETPRIO 0
 #endif
@@ -132,16 +138,38 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   // 1 KiB pieces [A h | A l | W h | W l]; wave w copies pieces PPW*w .. PPW*w + PPW-1.
   const uint32_t voff = lane * 16;
   auto issue = [&](int kt, int stage) {
+#if LG_GEMM_DIAG & 2
+    return;
+#endif
+#if LG_GEMM_DIAG & 8
+    constexpr int IW = NW / 4 > 0 ? NW / 4 : 1;  // issuing waves
+    if (wave >= IW) return;
+#pragma unroll
+    for (int i = 0; i < PIECES / IW; ++i) {
+      const int q = wave * (PIECES / IW) + i;
+#else
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;  // wave-uniform
+#endif
       const char* src;
+#if LG_GEMM_DIAG & 16
+      if (q >= 2 * (APT / 1024)) continue;  // A pieces only
+#endif
+#if LG_GEMM_DIAG & 32
+      if (q < 2 * (APT / 1024)) continue;   // W pieces only
+#endif
       if (q < 2 * (APT / 1024)) {
         const int pl = q / (APT / 1024), pc = q % (APT / 1024);
         const bool first = kt < nk0;
         const PlaneRef& A = first ? g.A0 : g.A1;
         const int kb = first ? kt : kt - nk0;
-        src = reinterpret_cast<const char*>(A.p + pl * A.ps + ((size_t)kb * A.rows_pad + m0) * BK) + pc * 1024;
+#if LG_GEMM_DIAG & 1
+        const int am0 = m0 & 2047;
+#else
+        const int am0 = m0;
+#endif
+        src = reinterpret_cast<const char*>(A.p + pl * A.ps + ((size_t)kb * A.rows_pad + am0) * BK) + pc * 1024;
       } else {
         const int qw = q - 2 * (APT / 1024);
         const int pl = qw / (WPT / 1024), pc = qw % (WPT / 1024);
@@ -239,9 +267,13 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     if (p < nk) issue(p, p);
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = min(NSTAGE - 2, nk - 1 - kt);  // my k-tiles in flight beyond kt
+#if LG_GEMM_DIAG & 8
+    wait_vm<0>();
+#elif !(LG_GEMM_DIAG & 4)
     if (NSTAGE >= 4 && ahead >= 2) wait_vm<2 * PPW>();
     else if (NSTAGE >= 3 && ahead >= 1) wait_vm<PPW>();
     else wait_vm<0>();
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");

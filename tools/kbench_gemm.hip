@@ -147,6 +147,12 @@ int main() {
     const int it = 20;
     double ms;
     const bool only_stagger = getenv("KB_STAGGER") != nullptr;
+    if (getenv("KB_QUICK")) {  // k-loop probes (build with -DLG_GEMM_DIAG=0/1/2)
+      if (s.K < 256) continue;
+      ms = run_h3<256, 2, EPI_PROBE>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2, no epilogue", ms, false);
+      ms = run_h3<256, 2>(s, bias, Y, it, true, Yp); rep("h3  256x256 + planes", ms, !LG_GEMM_DIAG);
+      continue;
+    }
     if (!only_stagger) {
     ms = run<MODE_X6, 256, 256, 16, 64, 64>(s, A, W, bias, Y, it); rep("x6  256x256x16 (16w)", ms, true);
     ms = run_h3<256, 2>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2", ms, true);

@@ -233,7 +233,7 @@ __device__ __forceinline__ int range_slot_exp(const unsigned* tab, int slot) {
 // range_commit_lds reuses 16 floats of the caller's LDS (kernels that declare all of it) and
 // first waits for every wave to be done with it.
 template <class RO>
-__device__ __forceinline__ void range_commit_lds(const RO& r, float lane_max, int e, float* red) {
+__device__ __forceinline__ void range_commit_lds(const RO& r, float lane_max, int e, float* red, int nwaves = -1) {
   if (!r.tab) return;
   if (!r.track) {  // E only: no reduction, no barrier (E != 0 is rare)
     if (e != 0 && (threadIdx.x & 63) == 0) r.tab[r.out * kRangeStride + kRangeShards] = (unsigned)e;
@@ -245,7 +245,8 @@ __device__ __forceinline__ void range_commit_lds(const RO& r, float lane_max, in
   __syncthreads();
   if (threadIdx.x == 0) {
     float mm = 0.f;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) mm = fmaxf(mm, red[w]);
+    const int nw = nwaves > 0 ? nwaves : (int)(blockDim.x >> 6);  // waves still running
+    for (int w = 0; w < nw; ++w) mm = fmaxf(mm, red[w]);
     unsigned* slot = r.tab + r.out * kRangeStride;
     if (mm > 0.f) atomicMax(slot + (blockIdx.x % kRangeShards), __float_as_uint(mm));
     if (e != 0) slot[kRangeShards] = (unsigned)e;

@@ -84,10 +84,15 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // BN x BM tile of (BM/64) x (BN/WN) waves, each 64 x WN (2 x WN/32 MFMA tiles of 32 x 32).
-template <int EPI, int BM, int NSTAGE, int BN = TB, int WN = 64>
-__global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(GemmH3Args g) {
+// KS > 1 (single-wave tiles only): KS waves split the k-tiles of one tile, each with its own LDS
+// ring and no barriers in the k-loop; the partial accumulators meet in LDS and wave 0 adds them
+// in wave order and runs the epilogue alone (small row counts: KS times the waves in flight per
+// tile, at the cost of a different rounding order from the KS = 1 kernels).
+template <int EPI, int BM, int NSTAGE, int BN = TB, int WN = 64, int KS = 1>
+__global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kernel(GemmH3Args g) {
   constexpr int WGN = BN / WN;               // waves along N
-  constexpr int NW = (BM / 64) * WGN;
+  constexpr int NW = (BM / 64) * WGN;        // waves of the tile (per k-split group)
+  static_assert(KS == 1 || NW == 1, "split-k: single-wave tiles");
   constexpr int NJ = WN / 32;                // 32-column MFMA tiles per wave
   constexpr int BK = kKB;                    // k-tile = one k-block of the plane images (32)
   constexpr int APT = BM * BK * 2;           // one A plane tile (bytes)
@@ -96,13 +101,17 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   constexpr int PIECES = STAGE_BYTES / 1024; // 1 KiB LDS-DMA pieces per stage
   constexpr int PPW = PIECES / NW;
   static_assert(PIECES % NW == 0, "pieces per wave");
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE_BYTES];
+  constexpr int RING = NSTAGE * STAGE_BYTES;  // one k-split group's stages
+  static_assert(KS == 1 || RING >= 64 * 64 * 4, "split-k: a partial accumulator fits the ring");
+  __shared__ __attribute__((aligned(1024))) char smem[KS * RING];
   constexpr bool kQkv = EPI == EPI_QKV_ROT || EPI == EPI_CROSS_QKV;
   __shared__ int rowinfo[kQkv ? 2 * BM : 1];  // QKV epilogues: head-major base / stride per tile row
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ks = KS > 1 ? wave_all : 0;    // k-split group
+  const int wave = KS > 1 ? 0 : wave_all;  // wave within the tile
   const int l32 = lane & 31, half = lane >> 5;
   const int wm0 = (wave / WGN) * 64, wn0 = (wave % WGN) * WN;
 
@@ -131,7 +140,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     if (!any) return;
   }
 
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)smem);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)smem) + ks * RING;
 
   // k-tile kt of a plane image is one contiguous block per plane (the tile's rows of k-block kt),
   // already in the LDS tile's swizzled layout: staging is a straight copy.  The stage is cut into
@@ -212,7 +221,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     return *reinterpret_cast<const f16x8*>(st + t0 + r * (BK * 2) + ((c ^ plane_swz(r)) << 4));
   };
   auto compute = [&](int stage) {
-    const char* st = smem + stage * STAGE_BYTES;
+    const char* st = smem + ks * RING + stage * STAGE_BYTES;
     if constexpr (kMF16) {
       // lane: row (lane & 15) of each 16-row block, k chunk lane >> 4 (k = 8c .. 8c+7)
       const int c = lane >> 4, r16 = lane & 15;
@@ -262,11 +271,21 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
   // ring of NSTAGE stages, NSTAGE-1 k-tiles in flight; one barrier per k-tile: wait for my
   // copies of tile kt -> barrier (everyone's copies landed AND everyone is done reading stage
   // (kt-1) % NSTAGE) -> refill that stage with tile kt+NSTAGE-1 -> multiply tile kt
+  // k-tiles kb .. ke-1 (the whole range unless split-k)
+  const int kb = KS > 1 ? (ks * nk) / KS : 0, ke = KS > 1 ? ((ks + 1) * nk) / KS : nk;
+  auto scale_acc = [&](float f) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < TR; ++r) acc[i][j][r] *= f;
+  };
 #pragma unroll
   for (int p = 0; p < NSTAGE - 1; ++p)
-    if (p < nk) issue(p, p);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(NSTAGE - 2, nk - 1 - kt);  // my k-tiles in flight beyond kt
+    if (kb + p < ke) issue(kb + p, p);
+  for (int kt = kb; kt < ke; ++kt) {
+    const int ahead = min(NSTAGE - 2, ke - 1 - kt);  // my k-tiles in flight beyond kt
 #if LG_GEMM_DIAG & 8
     wait_vm<0>();
 #elif !(LG_GEMM_DIAG & 4)
@@ -275,29 +294,54 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
     else wait_vm<0>();
 #endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr (KS == 1) __builtin_amdgcn_s_barrier();  // split-k groups are single waves
     asm volatile("" ::: "memory");
-    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
-    if (kt == nk0 && e0 != e1) {  // switching from A0 to A1 units (exact power of two; rare)
-      const float f = ldexpf(1.f, e0 - e1);
+    if (kt + NSTAGE - 1 < ke) issue(kt + NSTAGE - 1, (kt - kb + NSTAGE - 1) % NSTAGE);
+    if (kt == nk0 && e0 != e1) scale_acc(ldexpf(1.f, e0 - e1));  // A0 -> A1 units (exact; rare)
+#if LG_GEMM_SETPRIO
+    __builtin_amdgcn_s_setprio(1);  // keeps the MFMA cluster between the barriers (guide T5)
+#endif
+    compute((kt - kb) % NSTAGE);
+#if LG_GEMM_SETPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  }
+  if (KS > 1 && ke <= nk0 && e0 != e1) scale_acc(ldexpf(1.f, e0 - e1));  // a partial of A0 k-tiles only
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if constexpr (KS > 1) {
+    // partials of groups 1.. into their own (now idle) rings, lane-major (conflict-free); wave 0
+    // adds them in group order and carries on alone (s_barrier waits only for surviving waves)
+    constexpr int NA = TI * TJ * TR;
+    if (ks > 0) {
+      float* pp = reinterpret_cast<float*>(smem + ks * RING);
+      int x = 0;
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
 #pragma unroll
-          for (int r = 0; r < TR; ++r) acc[i][j][r] *= f;
+          for (int r = 0; r < TR; ++r, ++x) pp[x * 64 + lane] = acc[i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      return;
     }
-#if LG_GEMM_SETPRIO
-    __builtin_amdgcn_s_setprio(1);  // keeps the MFMA cluster between the barriers (guide T5)
-#endif
-    compute(kt % NSTAGE);
-#if LG_GEMM_SETPRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int q = 1; q < KS; ++q) {
+      const float* pp = reinterpret_cast<const float*>(smem + q * RING);
+      int x = 0;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < TR; ++r, ++x) acc[i][j][r] += pp[x * 64 + lane];
+    }
+    static_assert(NA == 64, "single-wave 64 x 64 tile");
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
 
   // ------------------------------------------------------------------ epilogues
   float wmax = 0.f;  // max |x| this lane wrote into planes (RangeOut tracking)
@@ -421,7 +465,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
       }
     }
-    range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem));
+    range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem), NW);
   } else if constexpr (EPI == EPI_STORE) {
     static_assert(WN == 64, "EPI_STORE tile");
     // Transposed through LDS (free after the k-loop; 8 KiB per wave per 32-row pass), LDS element
@@ -533,7 +577,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
-    if (g.Yp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem));
+    if (g.Yp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem), NW);
   } else {
     static_assert(WN == 64, "QKV epilogue tile");
     // Head-major scatter through the same LDS transpose as EPI_STORE.  The wave's 64 columns are
@@ -667,22 +711,22 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64) void gemm_h3_kernel(Gem
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
-    if (to_kp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem));
-    else if (to_vp) range_commit_lds(g.ro_v, wmax, eo, reinterpret_cast<float*>(smem));
+    if (to_kp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem), NW);
+    else if (to_vp) range_commit_lds(g.ro_v, wmax, eo, reinterpret_cast<float*>(smem), NW);
   }
 }
 
-template <int BM, int NSTAGE, int BN = TB, int WN = 64>
+template <int BM, int NSTAGE, int BN = TB, int WN = 64, int KS = 1>
 hipError_t gemm_h3_launch(const GemmH3Args& a, int epi, hipStream_t st) {
   const int blocks = ((a.R + BM - 1) / BM) * (a.Nout / BN);
-  const dim3 grid(blocks), block((BM / 64) * (BN / WN) * 64);
+  const dim3 grid(blocks), block((BM / 64) * (BN / WN) * 64 * KS);
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_STORE, BM, NSTAGE, BN, WN>), grid, block, 0, st, a); break;
-    case EPI_QKV_ROT: hipLaunchKernelGGL((gemm_h3_kernel<EPI_QKV_ROT, BM, NSTAGE, BN, WN>), grid, block, 0, st, a); break;
+    case EPI_STORE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_STORE, BM, NSTAGE, BN, WN, KS>), grid, block, 0, st, a); break;
+    case EPI_QKV_ROT: hipLaunchKernelGGL((gemm_h3_kernel<EPI_QKV_ROT, BM, NSTAGE, BN, WN, KS>), grid, block, 0, st, a); break;
     case EPI_CROSS_QKV:
-      hipLaunchKernelGGL((gemm_h3_kernel<EPI_CROSS_QKV, BM, NSTAGE, BN, WN>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((gemm_h3_kernel<EPI_CROSS_QKV, BM, NSTAGE, BN, WN, KS>), grid, block, 0, st, a);
       break;
-    case EPI_PROBE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_PROBE, BM, NSTAGE, BN, WN>), grid, block, 0, st, a); break;
+    case EPI_PROBE: hipLaunchKernelGGL((gemm_h3_kernel<EPI_PROBE, BM, NSTAGE, BN, WN, KS>), grid, block, 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -748,7 +792,17 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
     return gemm_h3_ln_launch<LG_GEMM_LN_WN>(a, st);
   }
   switch (gemm_tile_for((long long)((a.R + TB - 1) / TB) * (a.Nout / TB))) {
-    case TILE_SMALL: return gemm_h3_launch<64, 4, 64, 64>(a, epi, st);
+    case TILE_SMALL: {
+      // 64 x 64 single-wave tiles (fewer than 128 big tiles: at most 2048 of them), the k-tiles
+      // split over 4 waves so that each CU runs 4 waves instead of one or two.  The split does not
+      // depend on the row count, so every small-tile launch of one shape rounds alike whatever
+      // the batch (LG_GEMM_KSPLIT=1|2|4 overrides)
+      int ksplit = 4;
+      if (const char* e = getenv("LG_GEMM_KSPLIT")) ksplit = atoi(e);
+      if (ksplit >= 4 && a.K >= 4 * kKB) return gemm_h3_launch<64, 2, 64, 64, 4>(a, epi, st);
+      if (ksplit >= 2 && a.K >= 2 * kKB) return gemm_h3_launch<64, 4, 64, 64, 2>(a, epi, st);
+      return gemm_h3_launch<64, 4, 64, 64>(a, epi, st);
+    }
     case TILE_MEDIUM: return gemm_h3_launch<128, 2, 128, 64>(a, epi, st);
     default: return gemm_h3_launch<LG_GEMM_H3_TILE>(a, epi, st);
   }

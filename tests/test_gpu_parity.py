@@ -118,19 +118,24 @@ def test_forward_matches_reference_golden(name, precision):
     check_against_golden(pred, g, f"{name}/{precision}")
 
 
-@pytest.mark.parametrize("tile,waves,assign,kernel", [("big", "8", "sim_h3", "h3g"), ("small", "4", "x6_fused", "h3m"),
-                                                       ("small", "2", "x6_unfused", "h3g"), ("big", "2", "sim_h3", "h3m"),
-                                                       ("medium", "4", "sim_h3", "h3g")])
+@pytest.mark.parametrize("tile,waves,assign,kernel,ksplit", [("big", "8", "sim_h3", "h3g", "4"),
+                                                              ("small", "4", "x6_fused", "h3m", "4"),
+                                                              ("small", "2", "x6_unfused", "h3g", "1"),
+                                                              ("small", "8", "sim_h3", "h3g", "2"),
+                                                              ("big", "2", "sim_h3", "h3m", "4"),
+                                                              ("medium", "4", "sim_h3", "h3g", "4")])
 @pytest.mark.parametrize("name", case_names())
-def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, monkeypatch):
+def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, ksplit, monkeypatch):
     """The fp16x3 GEMM picks 256x256 tiles (throughput), 128x128 tiles (fewer big tiles than CUs)
     or 64x64 tiles (fewer than a quarter, e.g. B = 1) by row count, and the attention 8, 4 or 2 waves (256/128/64 queries) per
     workgroup, and the assignment either recomputes the similarity inside two fp16x3 GEMM passes
     (M, N multiples of 16, no pruning: sim_h3) or materialises it with the bf16x6 GEMM and runs
     the two-read fused passes (N % 4 == 0, N <= 2048) or the four-read ones; LG_GEMM_TILE /
     LG_ATTN_WAVES / LG_ASSIGN_SIM_X6 / LG_ASSIGN_UNFUSED force each so that every launch shape is
-    checked against the reference on every golden case."""
+    checked against the reference on every golden case.  The 64x64 tiles split the k-tiles over
+    LG_GEMM_KSPLIT waves (4 by default at small row counts; 1 = the unsplit single-wave tile)."""
     monkeypatch.setenv("LG_GEMM_TILE", tile)
+    monkeypatch.setenv("LG_GEMM_KSPLIT", ksplit)
     monkeypatch.setenv("LG_ATTN_WAVES", waves)
     monkeypatch.setenv("LG_ATTN_KERNEL", kernel)  # fp16x3 attention: 16x16x32 (h3g) / 32x32x16 (h3m) MFMAs
     if assign != "sim_h3":  # the materialised bf16x6 similarity
@@ -144,7 +149,7 @@ def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, mon
         pred = model(_gpu_data(data))
     torch.cuda.synchronize()
     assert model.last_precision_used == "fp16x3"
-    check_against_golden(pred, g, f"{name}/tile={tile},waves={waves},{assign},{kernel}")
+    check_against_golden(pred, g, f"{name}/tile={tile},waves={waves},{assign},{kernel},ksplit={ksplit}")
 
 
 def test_weight_changes_after_first_forward_are_picked_up():

@@ -318,9 +318,14 @@ __device__ __forceinline__ float sum_x16_32(float v) {
 // (SUBS = 2: 2 x 64 KiB of LDS), and PRIO raises the second-dispatched half of the waves to
 // s_setprio 1 once.  tools/kbench_attn.hip: 862 us vs 907-918 us for the register-staged
 // attention_h3f_kernel (tools/attn_experiments.hip) at the bench shape.
-template <int SUBS, int PRIO, int WAVES = 8>
+// SPLIT (small batches): the keys of a work item are cut into nsplit ranges of lsplit keys, one
+// workgroup each; instead of the context the workgroup writes its unnormalised partial (O, the
+// softmax reference m, the 2^11-scaled sum l and the query's exponent factor c) and
+// attn_split_combine_kernel merges the ranges.
+template <int SUBS, int PRIO, int WAVES = 8, bool SPLIT = false>
 __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
-                                                                float scale_log2e) {
+                                                                float scale_log2e, float* part = nullptr,
+                                                                int nsplit = 1, int lsplit = 0) {
   constexpr int QB = 32 * WAVES;
   constexpr int KT = 64;                   // keys per sub-tile (one softmax step)
   constexpr int LT = KT * SUBS;            // keys per LDS tile (one barrier)
@@ -332,7 +337,12 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   __shared__ __attribute__((aligned(16))) _Float16 Ks[2 * 2 * PL];
   __shared__ __attribute__((aligned(16))) _Float16 Vs[2 * 2 * PL];
 
-  const int item = xcd_chunk(blockIdx.x, gridDim.x);
+  int item = xcd_chunk(blockIdx.x, gridDim.x);
+  int split = 0;
+  if constexpr (SPLIT) {
+    split = item % nsplit;
+    item /= nsplit;
+  }
   const int qb = item % nqb;
   const int sbh = item / nqb;
   const int set = sbh / (B * H), bh = sbh - set * (B * H);
@@ -340,12 +350,25 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   const int q_blk = qb * QB;
   // S.Nq / S.Nk are the layout capacities; per-pair counts (batched pruning) bound the loops
   const int NqS = S.Nq, NkS = S.Nk, pb = bh / H;
+  const int nqs = max(s0.Nq, s1.Nq);  // query stride of the split partials
   if (S.act && !S.act[pb]) return;
-  const int Nq = S.nq_cnt ? S.nq_cnt[pb] : NqS, Nk = S.nk_cnt ? S.nk_cnt[pb] : NkS;
-  if (q_blk >= Nq || Nk <= 0) return;
+  const int Nq = S.nq_cnt ? S.nq_cnt[pb] : NqS;
+  int Nk = S.nk_cnt ? S.nk_cnt[pb] : NkS;
+  const int k0 = SPLIT ? split * lsplit : 0;
+  if constexpr (SPLIT) Nk = min(lsplit, Nk - k0);
+  if (q_blk >= Nq) return;
+  if (Nk <= 0) {
+    if constexpr (SPLIT) {  // an empty key range: a partial that weighs nothing
+      for (int q = q_blk + (int)threadIdx.x; q < min(q_blk + QB, Nq); q += 64 * WAVES) {
+        const size_t rec = (((size_t)split * 2 + set) * B * H + bh) * nqs + q;
+        *reinterpret_cast<f32x4*>(part + (size_t)nsplit * 2 * B * H * nqs * kHeadDim + rec * 4) = f32x4{-INFINITY, 0.f, 1.f, 0.f};
+      }
+    }
+    return;
+  }
   const float* Q = S.q + (size_t)bh * NqS * kHeadDim;
-  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * NkS * kHeadDim;
-  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * NkS * kHeadDim;
+  const _Float16* Kp = static_cast<const _Float16*>(S.kp) + ((size_t)bh * NkS + k0) * kHeadDim;
+  const _Float16* Vp = static_cast<const _Float16*>(S.vp) + ((size_t)bh * NkS + k0) * kHeadDim;
   const long long ps = S.pstride;
   const int head = bh % H;
   const int b = bh / H;
@@ -595,6 +618,25 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   else LG_ATTN_TILES((std::integral_constant<bool, false>{}))
 #undef LG_ATTN_TILES
 
+  if constexpr (SPLIT) {
+    // partial record of (split, set, b, h, query): O [64] (lane: dims 16 dt + 4 g ..), then
+    // (m, l, c) -- the combine weighs the split by exp2((m - max m) c), as the in-loop rescale does
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float l_tot = sum_x16_32(l_run[qt]);
+      const int q = q_blk + wave * 32 + qt * 16 + r16;
+      if (q < Nq) {
+        const size_t rec = (((size_t)split * 2 + set) * B * H + bh) * nqs + q;
+        float* po = part + rec * kHeadDim;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt + 4 * g) = o[dt][qt];
+        if (g == 0)
+          *reinterpret_cast<f32x4*>(part + (size_t)nsplit * 2 * B * H * nqs * kHeadDim + rec * 4) =
+              f32x4{m_use[qt], l_tot, c_lane[qt], 0.f};
+      }
+    }
+    return;
+  }
   // context rows into the plane image: o = 2^11 sum(v p) (the MFMA scale), l_run = 2^11 sum(p),
   // so 1 / l_run is the old 2^-11 / l exactly; v arrived as v * 2^-E[v] and the context leaves
   // as ctx * 2^-E[v] (its consumer reads the value slot)
@@ -623,14 +665,87 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   }
 }
 
+// merges the NS partials of every (set, b, h, query) into the context plane image: one thread per
+// 8 dims of a query, every load issued before the first use, the splits summed in order
+template <int NS>
+__global__ __launch_bounds__(256) void attn_split_combine_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqs, const float* part) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int chunk = (int)(t & 7);
+  size_t r = t >> 3;
+  const int q = (int)(r % nqs);
+  r /= nqs;
+  const int bh = (int)(r % ((size_t)B * H));
+  const int set = (int)(r / ((size_t)B * H));
+  if (set >= 2) return;
+  const AttnSet& S = set == 0 ? s0 : s1;
+  const int head = bh % H, b = bh / H;
+  if (q >= (S.nq_cnt ? S.nq_cnt[b] : S.Nq) || (S.act && !S.act[b])) return;  // rows the kernel skipped
+  const size_t nrec = (size_t)2 * B * H * nqs;
+  const size_t rec0 = ((size_t)set * B * H + bh) * nqs + q;
+  const float* ml = part + (size_t)NS * nrec * kHeadDim;
+  f32x4 v[NS], a[NS], c[NS];
+#pragma unroll
+  for (int sp = 0; sp < NS; ++sp) {
+    const size_t rec = (size_t)sp * nrec + rec0;
+    v[sp] = *reinterpret_cast<const f32x4*>(ml + rec * 4);
+    a[sp] = *reinterpret_cast<const f32x4*>(part + rec * kHeadDim + 8 * chunk);
+    c[sp] = *reinterpret_cast<const f32x4*>(part + rec * kHeadDim + 8 * chunk + 4);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int sp = 0; sp < NS; ++sp)
+    if (v[sp][1] > 0.f) mx = fmaxf(mx, v[sp][0]);
+  float l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sp = 0; sp < NS; ++sp) {
+    if (!(v[sp][1] > 0.f)) continue;  // an empty key range
+    const float w = __builtin_amdgcn_exp2f((v[sp][0] - mx) * v[sp][2]);
+    l = fmaf(v[sp][1], w, l);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = fmaf(a[sp][e], w, o[e]);
+      o[4 + e] = fmaf(c[sp][e], w, o[4 + e]);
+    }
+  }
+  const float inv = 1.f / l;
+  const int orow = S.o_row0 + b * S.Nq + q;
+  f16x8 h, lo;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    _Float16 x, y;
+    split2h(o[e] * inv, x, y);
+    h[e] = x;
+    lo[e] = y;
+  }
+  const size_t off = plane_off(orow, head * kHeadDim + 8 * chunk, S.o_rows_pad);
+  *reinterpret_cast<f16x8*>(S.op + off) = h;
+  *reinterpret_cast<f16x8*>(S.op + S.ops + off) = lo;
+}
+
 template <int SUBS, int PRIO = 0, int WAVES = 8>
-static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st,
+                                       float* part = nullptr, int nsplit = 1) {
   constexpr int QB = 32 * WAVES;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
   if (nq == 0 || B == 0) return hipSuccess;
   if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
   const int nqb = (nq + QB - 1) / QB;
   const int items = nqb * B * H * 2;
+  if (nsplit > 1 && part) {
+    constexpr int LT = 64 * SUBS;  // keys per LDS tile
+    const int nk = s0.Nk > s1.Nk ? s0.Nk : s1.Nk;
+    const int lsplit = ((nk + nsplit - 1) / nsplit + LT - 1) / LT * LT;
+    hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES, true>), dim3(items * nsplit), dim3(64 * WAVES), 0, st, s0, s1,
+                       B, H, nqb, scale * 1.4426950408889634f, part, nsplit, lsplit);
+    const size_t threads = (size_t)2 * B * H * nq * 8;
+    const dim3 cg((unsigned)((threads + 255) / 256)), cb(256);
+    switch (nsplit) {
+      case 2: hipLaunchKernelGGL(attn_split_combine_kernel<2>, cg, cb, 0, st, s0, s1, B, H, nq, (const float*)part); break;
+      case 4: hipLaunchKernelGGL(attn_split_combine_kernel<4>, cg, cb, 0, st, s0, s1, B, H, nq, (const float*)part); break;
+      default: hipLaunchKernelGGL(attn_split_combine_kernel<8>, cg, cb, 0, st, s0, s1, B, H, nq, (const float*)part); break;
+    }
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
                      scale * 1.4426950408889634f);
   return hipGetLastError();
@@ -994,7 +1109,28 @@ static hipError_t attention_x6_launch(const AttnSet& s0, const AttnSet& s1, int 
 #define LG_ATTN_CONFIG 8, 64
 #endif
 
-hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st) {
+// Key splits for small batches (4-wave h3g items only): while the work items leave most CUs idle,
+// double the splits (at least 256 keys each, at most 512 workgroups).  B = 1, N = 1024 (64 items):
+// 4 splits 1.48 ms per forward vs 1.55 (2), 1.67 (8, one LDS tile each) and 1.68 (unsplit).
+// LG_ATTN_SPLIT=1|2|4|8 overrides.
+int attention_nsplit(int B, int H, int nq, int nk) {
+  if (attention_use_h3m() || attention_waves(B, H, nq) != 4) return 1;
+  const long long items = (long long)((nq + 127) / 128) * B * H * 2;
+  int ns = 1;
+  if (const char* e = getenv("LG_ATTN_SPLIT")) {
+    ns = atoi(e);
+    return ns == 2 || ns == 4 || ns == 8 ? ns : 1;
+  }
+  while (ns < 8 && items * ns * 2 <= 512 && nk / (ns * 2) >= 256) ns *= 2;
+  return ns;
+}
+size_t attention_split_floats(int B, int H, int nq, int nk) {
+  const int ns = attention_nsplit(B, H, nq, nk);
+  return ns > 1 ? (size_t)ns * 2 * B * H * nq * (kHeadDim + 4) : 0;
+}
+
+hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st,
+                         float* part, size_t part_floats) {
   if (prec == PREC_H3) {
     if (!s0.op || !s1.op) return hipErrorInvalidValue;
     const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
@@ -1007,7 +1143,12 @@ hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, flo
     }
     switch (attention_waves(B, H, nq)) {
       case 2: return attention_h3g_launch<2, 1, 2>(s0, s1, B, H, scale, st);
-      case 4: return attention_h3g_launch<2, 1, 4>(s0, s1, B, H, scale, st);
+      case 4: {
+        const int nk = s0.Nk > s1.Nk ? s0.Nk : s1.Nk;
+        const int ns = attention_nsplit(B, H, nq, nk);
+        const bool fits = part && part_floats >= attention_split_floats(B, H, nq, nk);
+        return attention_h3g_launch<2, 1, 4>(s0, s1, B, H, scale, st, fits ? part : nullptr, fits ? ns : 1);
+      }
       default: return attention_h3g_launch<2, 1, 8>(s0, s1, B, H, scale, st);
     }
   }

@@ -181,7 +181,11 @@ struct AttnSet {
   const int* nk_cnt;
   const int* act;
 };
-hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st);
+// part / part_floats (optional): scratch for the key-split partials of small batches
+// (attention_split_floats(B, H, max Nq, max Nk) floats; without it the launch does not split)
+hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st,
+                         float* part = nullptr, size_t part_floats = 0);
+size_t attention_split_floats(int B, int H, int nq, int nk);
 
 // Positional encoding: normalised keypoints -> cos/sin tables [rows][32].
 struct PEArgs {

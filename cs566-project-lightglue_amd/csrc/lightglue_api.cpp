@@ -313,6 +313,8 @@ struct Work {
   unsigned* rtab;  // PREC_H3 range table (kernels.h RangeOut), kRangeSlots slots
   int64_t *m0c, *m1c;
   float *s0c, *s1c;
+  float* apart;  // attention key-split partials (small batches)
+  size_t apart_floats;
   size_t bytes;
 };
 
@@ -353,6 +355,8 @@ Work carve(char* base, int B, int M, int N, bool prune, int din) {
   w.tok = tf(R);
   w.sim = tf((size_t)B * M * N);
   w.aws = tf(lg::assign_workspace_floats(B, M, N) + 64 + lg::sim_h3_workspace_floats(B, M, N));
+  w.apart_floats = lg::attention_split_floats(B, D / 64, std::max(M, N), std::max(M, N));
+  w.apart = w.apart_floats ? tf(w.apart_floats) : nullptr;
   w.rtab = reinterpret_cast<unsigned*>(ti(kRangeSlots * lg::kRangeStride));
   if (prune) {
     w.X2 = tf(R * D);
@@ -668,7 +672,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   auto image = [&](_Float16* p, int K) { return PlaneRef{p, (long long)RP * K, RP}; };
   auto attn = [&](const AttnSet& a0, const AttnSet& a1, float scale, bool cross) -> hipError_t {
     const int p = h->prof_begin(LG_KERNEL_ATTENTION, st);
-    const hipError_t e = attention_f32(a0, a1, B, H, scale, prec, st);
+    const hipError_t e = attention_f32(a0, a1, B, H, scale, prec, st, w.apart, w.apart_floats);
     // self: 2 matmuls per image (QK^T, PV); cross: one shared sim + two PV (lightglue.py:236-242)
     const double hd = 64.0 * H * B;
     const double fl = cross ? 6.0 * a0.Nq * a0.Nk * hd : 4.0 * hd * ((double)a0.Nq * a0.Nk + (double)a1.Nq * a1.Nk);
@@ -1115,12 +1119,14 @@ int lg_log_optimal_transport(const float* scores, float alpha, int32_t B, int32_
 }
 
 namespace {
-size_t attention_ws(int B, int H, int Nq, int Nk, size_t& kv_off, size_t& img_off, int& rp) {
+size_t attention_ws(int B, int H, int Nq, int Nk, size_t& kv_off, size_t& img_off, int& rp, size_t* part_off = nullptr) {
   const size_t n = (size_t)B * H * Nk * 64;
   rp = (int)(((size_t)B * Nq + 255) / 256 * 256);
-  kv_off = 4 * 32 * 4;                       // [range table (4 slots) | k planes (3 max) | v planes | ctx image]
+  kv_off = 4 * 32 * 4;  // [range table (4 slots) | k planes (3 max) | v planes | ctx image | key-split partials]
   img_off = kv_off + 2 * 3 * n * 2;
-  return img_off + (size_t)2 * rp * 256 * 2;
+  const size_t po = img_off + (size_t)2 * rp * 256 * 2;
+  if (part_off) *part_off = po;
+  return po + lg::attention_split_floats(B, H, Nq, Nk) * sizeof(float);
 }
 }  // namespace
 
@@ -1136,9 +1142,9 @@ int lg_attention(const float* q, const float* k, const float* v, int32_t B, int3
                  float scale, int32_t precision, float* ctx, void* workspace, size_t workspace_bytes, void* stream) {
   if (!q || !k || !v || !ctx) return fail(LG_E_INVALID, "null argument");
   if (H * 64 != 256 || B < 0 || Nq < 0 || Nk <= 0) return fail(LG_E_INVALID, "bad shape (H * 64 must be 256, Nk > 0)");
-  size_t kv_off, img_off;
+  size_t kv_off, img_off, part_off;
   int rp;
-  const size_t need = attention_ws(B, H, Nq, Nk, kv_off, img_off, rp);
+  const size_t need = attention_ws(B, H, Nq, Nk, kv_off, img_off, rp, &part_off);
   if (!workspace || workspace_bytes < need) return fail(LG_E_WORKSPACE, "workspace too small");
   if (B == 0 || Nq == 0) return LG_OK;
   hipStream_t st = (hipStream_t)stream;
@@ -1162,7 +1168,8 @@ int lg_attention(const float* q, const float* k, const float* v, int32_t B, int3
   const lg::AttnSet s0{q, kp, vp, (long long)n, ctx, Nq, Nk, img, (long long)rp * 256, rp, 0, h3 ? rtab : nullptr, 2};
   lg::AttnSet s1 = s0;
   s1.Nq = 0;
-  LG_HIP(lg::attention_f32(s0, s1, B, H, scale, prec, st));
+  LG_HIP(lg::attention_f32(s0, s1, B, H, scale, prec, st, reinterpret_cast<float*>(ws + part_off),
+                           lg::attention_split_floats(B, H, Nq, Nk)));
   if (h3) LG_HIP(lg::image_to_rows(img, (long long)rp * 256, rp, 256, ctx, B * Nq, rtab, 3, st));
   LG_HIP(hipStreamSynchronize(st));
   return LG_OK;

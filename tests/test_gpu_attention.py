@@ -107,6 +107,24 @@ def test_attention_matches_float64(name, precision, waves, kernel, monkeypatch):
     assert np.isfinite(err) and err <= tol, f"{name}/{precision}: max |d| = {err:.3g} > {tol:.3g}"
 
 
+@pytest.mark.parametrize("splits", ["2", "8"])
+@pytest.mark.parametrize("name", CASES)
+def test_attention_key_splits_match_float64(name, splits, monkeypatch):
+    """Small batches split each work item's keys over LG_ATTN_SPLIT workgroups (4-wave h3g) whose
+    partials (O, m, l, c) attn_split_combine_kernel merges; the lazy references of the splits
+    differ, empty key ranges (single_key, one_key_in_last_tile) weigh nothing."""
+    monkeypatch.setenv("LG_ATTN_WAVES", "4")
+    monkeypatch.setenv("LG_ATTN_KERNEL", "h3g")
+    monkeypatch.setenv("LG_ATTN_SPLIT", splits)
+    q, k, v, scale = case(name)
+    got = run_attention(q, k, v, scale, "auto")
+    ref = reference(q, k, v, scale)
+    err = (got - ref).abs().max().item()
+    L = (scale * torch.einsum("bhqd,bhkd->bhqk", q.double().abs(), k.double().abs())).max().item()
+    tol = TOL + 2.0 ** -21 * L * v.abs().max().item()
+    assert np.isfinite(err) and err <= tol, f"{name}/split {splits}: max |d| = {err:.3g} > {tol:.3g}"
+
+
 def test_increasing_scores_really_rescale():
     """The adversarial case is adversarial: the per-tile max of scale*q.k rises by more than the
     lazy threshold (3 log2 units = 2.08 nats) between consecutive 64-key tiles."""

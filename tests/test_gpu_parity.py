@@ -118,14 +118,15 @@ def test_forward_matches_reference_golden(name, precision):
     check_against_golden(pred, g, f"{name}/{precision}")
 
 
-@pytest.mark.parametrize("tile,waves,assign,kernel,ksplit", [("big", "8", "sim_h3", "h3g", "4"),
-                                                              ("small", "4", "x6_fused", "h3m", "4"),
-                                                              ("small", "2", "x6_unfused", "h3g", "1"),
-                                                              ("small", "8", "sim_h3", "h3g", "2"),
-                                                              ("big", "2", "sim_h3", "h3m", "4"),
-                                                              ("medium", "4", "sim_h3", "h3g", "4")])
+@pytest.mark.parametrize("tile,waves,assign,kernel,ksplit,asplit", [("big", "8", "sim_h3", "h3g", "4", "auto"),
+                                                                     ("small", "4", "x6_fused", "h3m", "4", "auto"),
+                                                                     ("small", "2", "x6_unfused", "h3g", "1", "auto"),
+                                                                     ("small", "8", "sim_h3", "h3g", "2", "auto"),
+                                                                     ("big", "2", "sim_h3", "h3m", "4", "auto"),
+                                                                     ("medium", "4", "sim_h3", "h3g", "4", "1"),
+                                                                     ("small", "4", "sim_h3", "h3g", "4", "8")])
 @pytest.mark.parametrize("name", case_names())
-def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, ksplit, monkeypatch):
+def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, ksplit, asplit, monkeypatch):
     """The fp16x3 GEMM picks 256x256 tiles (throughput), 128x128 tiles (fewer big tiles than CUs)
     or 64x64 tiles (fewer than a quarter, e.g. B = 1) by row count, and the attention 8, 4 or 2 waves (256/128/64 queries) per
     workgroup, and the assignment either recomputes the similarity inside two fp16x3 GEMM passes
@@ -133,9 +134,13 @@ def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, ksp
     the two-read fused passes (N % 4 == 0, N <= 2048) or the four-read ones; LG_GEMM_TILE /
     LG_ATTN_WAVES / LG_ASSIGN_SIM_X6 / LG_ASSIGN_UNFUSED force each so that every launch shape is
     checked against the reference on every golden case.  The 64x64 tiles split the k-tiles over
-    LG_GEMM_KSPLIT waves (4 by default at small row counts; 1 = the unsplit single-wave tile)."""
+    LG_GEMM_KSPLIT waves (4 by default at small row counts; 1 = the unsplit single-wave tile), and
+    the 4-wave attention splits the keys of small batches over LG_ATTN_SPLIT workgroups (auto: up
+    to 8, merged by attn_split_combine_kernel; 1 = unsplit)."""
     monkeypatch.setenv("LG_GEMM_TILE", tile)
     monkeypatch.setenv("LG_GEMM_KSPLIT", ksplit)
+    if asplit != "auto":
+        monkeypatch.setenv("LG_ATTN_SPLIT", asplit)
     monkeypatch.setenv("LG_ATTN_WAVES", waves)
     monkeypatch.setenv("LG_ATTN_KERNEL", kernel)  # fp16x3 attention: 16x16x32 (h3g) / 32x32x16 (h3m) MFMAs
     if assign != "sim_h3":  # the materialised bf16x6 similarity
@@ -149,7 +154,7 @@ def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, ksp
         pred = model(_gpu_data(data))
     torch.cuda.synchronize()
     assert model.last_precision_used == "fp16x3"
-    check_against_golden(pred, g, f"{name}/tile={tile},waves={waves},{assign},{kernel},ksplit={ksplit}")
+    check_against_golden(pred, g, f"{name}/tile={tile},waves={waves},{assign},{kernel},ksplit={ksplit},asplit={asplit}")
 
 
 def test_weight_changes_after_first_forward_are_picked_up():

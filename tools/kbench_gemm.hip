@@ -147,6 +147,17 @@ int main() {
     const int it = 20;
     double ms;
     const bool only_stagger = getenv("KB_STAGGER") != nullptr;
+    if (getenv("KB_LN")) {  // LN epilogue probes (build with -DLG_LN_PROBE=0/1/2/3)
+      if (s.N != 512) continue;
+      ms = run_ln<64, EPI_PROBE>(s, bias, nullptr, nullptr, Yp, it); rep("h3  128x512 x2, no epilogue", ms, false);
+      float *gam, *bet;
+      CK(hipMalloc(&gam, s.N * 4)); CK(hipMalloc(&bet, s.N * 4));
+      fill<<<(s.N + 255) / 256, 256>>>(gam, s.N, 4);
+      fill<<<(s.N + 255) / 256, 256>>>(bet, s.N, 5);
+      ms = run_ln<64>(s, bias, gam, bet, Yp, it); rep("h3  LN+GELU 128x512", ms, false);
+      CK(hipFree(gam)); CK(hipFree(bet));
+      continue;
+    }
     if (getenv("KB_QUICK")) {  // k-loop probes (build with -DLG_GEMM_DIAG=0/1/2)
       if (s.K < 256) continue;
       ms = run_h3<256, 2, EPI_PROBE>(s, bias, Y, it, false, Yp); rep("h3  256x256x32 x2, no epilogue", ms, false);

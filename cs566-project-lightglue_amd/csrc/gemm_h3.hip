@@ -65,7 +65,8 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 #ifndef LG_GEMM_DIAG
 // timing probes of the k-loop (tools/kbench_gemm.hip only; results are wrong under 1, 2, 4):
 // 1 every tile reads one of 8 row panels (L2-resident A), 2 no k-tile copies, 4 no vmcnt waits,
-// 8 the copies issued by the first NW/4 waves only, 16 A pieces only, 32 W pieces only
+// 8 the copies issued by the first NW/4 waves only, 16 A pieces only, 32 W pieces only,
+// 64 only the first NSTAGE k-tiles copied (later ones re-read them: realistic operands, no copy stream)
 #define LG_GEMM_DIAG 0
 #endif
 #ifndef LG_GEMM_SETPRIO
@@ -149,6 +150,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
   auto issue = [&](int kt, int stage) {
 #if LG_GEMM_DIAG & 2
     return;
+#endif
+#if LG_GEMM_DIAG & 64
+    if (kt >= NSTAGE) return;  // real data in every stage, later k-tiles re-read it (same MFMA power)
 #endif
 #if LG_GEMM_DIAG & 8
     constexpr int IW = NW / 4 > 0 ? NW / 4 : 1;  // issuing waves

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-GPU measurements of the BASELINE.json configs other than the headline one (bench.py).
 
-    python tools/bench_configs.py [--only 1,3,4] [--reps R]
+    python tools/bench_configs.py [--only 1,3,4,sp,sg,e2e] [--reps R]
 
 One JSON line per config:
   configs[1]  N=1024, 9 layers, B=1 (latency-shaped: one pair per forward)
@@ -10,6 +10,7 @@ One JSON line per config:
               B == 1, lightglue.py:528,533); MegaDepth-like 1600x1200 keypoints; also the same
               batch unpruned and one pair per forward
   sp          SuperPoint (§8f row 3): 16 gray 640x480 images per forward, top-2048 keypoints
+  e2e         configs[2] end to end: SuperPoint on both views + LightGlue, 32 pairs per forward
   configs[4]  N=4096, 8 pairs per GPU (64 over 8 GPUs): the LightGlue forward at N=4096 and the
               SuperGlue log-domain Sinkhorn (superglue.py:173-201, 50 iterations) on the
               [8, 4096, 4096] similarity, each timed on its own; Sinkhorn against the HBM roofline
@@ -187,13 +188,40 @@ def cfg_sg(dev, reps, B=16, N=1024):
             "matches_per_pair": float((pred["matches0"] >= 0).sum()) / B}
 
 
+def cfg_e2e(dev, reps, B=32, H=480, W=640, k=2048):
+    """configs[2] end to end (SuperPoint + LightGlue): B image pairs per forward through
+    TwoViewPipeline (two_view_pipeline.py:79-97) -- SuperPoint on each view's B gray 640x480
+    images (top-2048, force_num_keypoints so the pairs batch), then the 9-layer LightGlue on the
+    B pairs at N = 2048."""
+    from lightglue_amd.pipeline import TwoViewPipeline
+    from lightglue_amd.sp_weights import superpoint_state_dict, synthetic_images
+
+    conf = {"extractor": {"name": "gluefactory_nonfree.superpoint", "max_num_keypoints": k, "force_num_keypoints": True},
+            "matcher": {"name": "matchers.lightglue", "filter_threshold": 0.1}}
+    pipe = TwoViewPipeline(conf).eval().to(dev)
+    pipe.extractor.load_state_dict({n: torch.from_numpy(v) for n, v in superpoint_state_dict({}, seed=0).items()})
+    sd = synthetic_state_dict({"filter_threshold": 0.1}, seed=0)
+    pipe.matcher.load_state_dict({n: torch.from_numpy(v) for n, v in sd.items()}, strict=True)
+    size = torch.tensor([[float(W), float(H)]] * B, device=dev)
+    # both views show the same synthetic images (so the random-weight matcher has something to
+    # match; the work is the same for any pair of images)
+    img = torch.from_numpy(synthetic_images(B, 1, H, W, seed=1)).to(dev)
+    views = [{"image": img, "image_size": size} for _ in range(2)]
+    with torch.no_grad():
+        s, pred = timed(lambda: pipe({"view0": dict(views[0]), "view1": dict(views[1])}), reps)
+    return {"config": f"configs[2] end to end: SuperPoint {W}x{H} (top-{k}) + LightGlue N={k}, 9 layers, "
+                      f"batch={B} pairs, 1 GPU", "value": round(B / s, 2), "unit": "image-pairs/s",
+            "ms_per_forward": round(1e3 * s, 2), "keypoints0": list(pred["keypoints0"].shape),
+            "matches_per_pair": float((pred["matches0"] > -1).sum()) / B}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="1,3,4")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    fns = {"1": cfg1, "3": cfg3, "4": cfg4, "sp": cfg_sp, "sg": cfg_sg}
+    fns = {"1": cfg1, "3": cfg3, "4": cfg4, "sp": cfg_sp, "sg": cfg_sg, "e2e": cfg_e2e}
     for k in a.only.split(","):
         print(json.dumps(fns[k](dev, a.reps)), flush=True)
 

@@ -9,6 +9,7 @@
 #include "../cs566-project-lightglue_amd/csrc/gemm.hip"
 #include "../cs566-project-lightglue_amd/csrc/elementwise.hip"
 #include "../cs566-project-lightglue_amd/csrc/gemm_h3.hip"
+#include "gemm_persist.hip"
 
 using namespace lg;
 
@@ -35,6 +36,26 @@ double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out,
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
   for (int i = 0; i < iters; ++i) CK((gemm_h3_launch<BM, NS, BN, WN>(a, EPI, 0)));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
+double run_h3p(const Shape& s, float* bias, float* Y, int iters, _Float16* Yp, int grid) {
+  GemmH3Args a;
+  memset(&a, 0, sizeof(a));
+  a.A0 = {g_aplanes, (long long)s.R * s.K, s.R}; a.K0 = s.K; a.K = s.K;
+  a.W = {g_planes, (long long)s.N * s.K, s.N}; a.R = s.R; a.Nout = s.N;
+  a.acc_scale = g_unscale; a.out_scale = 1.f; a.bias = bias; a.Y = Y; a.ldy = s.N;
+  a.Yp = Yp; a.yps = (long long)s.R * s.N; a.yrows_pad = s.R;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(gemm_h3p(a, 0, grid));
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK(gemm_h3p(a, 0, grid));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -147,6 +168,17 @@ int main() {
     const int it = 20;
     double ms;
     const bool only_stagger = getenv("KB_STAGGER") != nullptr;
+    if (getenv("KB_PERSIST")) {  // persistent overlapped-epilogue prototype (tools/gemm_persist.hip)
+      if (s.K < 256) continue;
+      ms = run_h3<256, 2>(s, bias, Y, it, true, Yp); rep("h3  256x256 + planes", ms, true);
+      for (int grid : {256, 512}) {
+        char nm[64];
+        snprintf(nm, sizeof(nm), "h3p persistent + planes, grid %d", grid);
+        CK(hipMemset(Y, 0, (size_t)s.R * s.N * 4));
+        ms = run_h3p(s, bias, Y, it, Yp, grid); rep(nm, ms, true);
+      }
+      continue;
+    }
     if (getenv("KB_LN")) {  // LN epilogue probes (build with -DLG_LN_PROBE=0/1/2/3)
       if (s.N != 512) continue;
       ms = run_ln<64, EPI_PROBE>(s, bias, nullptr, nullptr, Yp, it); rep("h3  128x512 x2, no epilogue", ms, false);

@@ -292,7 +292,7 @@ __global__ __launch_bounds__(1024) void sim_h3_kernel(SimH3Args g) {
         for (int rr = 0; rr < 32; ++rr) {
           const int i = tm * BM + wm0 + 32 * p + rr;
           const float v = ep[rr * 64 + (lane ^ ((rr & 1) << 2))];
-          if (i < M && j < N) g.la[((size_t)b * (M + 1) + i) * (N + 1) + j] = v;
+          if (i < M && j < N) st_stream(g.la + ((size_t)b * (M + 1) + i) * (N + 1) + j, v);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }

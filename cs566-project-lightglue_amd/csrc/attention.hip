@@ -658,8 +658,9 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
           l[e] = c;
         }
         const size_t off = plane_off(orow, head * kHeadDim + 16 * dt + 4 * g, S.o_rows_pad);
-        *reinterpret_cast<f16x4*>(S.op + off) = h;
-        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+        // non-temporal: -0.1 ms per 32-pair forward (the GEMM epilogues' stores lose by it)
+        __builtin_nontemporal_store(h, reinterpret_cast<f16x4*>(S.op + off));
+        __builtin_nontemporal_store(l, reinterpret_cast<f16x4*>(S.op + S.ops + off));
       }
     }
   }
@@ -1050,8 +1051,9 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
           l[e] = c;
         }
         const size_t off = plane_off(orow, head * kHeadDim + hf * 32 + 8 * g + 4 * half, S.o_rows_pad);
-        *reinterpret_cast<f16x4*>(S.op + off) = h;
-        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+        // non-temporal: -0.1 ms per 32-pair forward (the GEMM epilogues' stores lose by it)
+        __builtin_nontemporal_store(h, reinterpret_cast<f16x4*>(S.op + off));
+        __builtin_nontemporal_store(l, reinterpret_cast<f16x4*>(S.op + S.ops + off));
       }
   }
 }

@@ -462,8 +462,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
               l[e] = c;
             }
             const size_t off = plane_off(row, n0 + wn0 + jh * 64 + cq, g.yrows_pad);
-            *reinterpret_cast<f16x8*>(g.Yp + off) = h;
-            *reinterpret_cast<f16x8*>(g.Yp + g.yps + off) = l;
+            st_stream(reinterpret_cast<f16x8*>(g.Yp + off), h);
+            st_stream(reinterpret_cast<f16x8*>(g.Yp + g.yps + off), l);
           }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
@@ -532,8 +532,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
               }
             if (g.Y) {
               float* yp = g.Y + (size_t)row * g.ldy + n0 + wn0 + c4;
-              *reinterpret_cast<f32x4*>(yp) = v0;
-              *reinterpret_cast<f32x4*>(yp + 32) = v1;
+              st_stream(reinterpret_cast<f32x4*>(yp), v0);
+              st_stream(reinterpret_cast<f32x4*>(yp + 32), v1);
             }
             if (g.Yp) {
               *reinterpret_cast<f32x4*>(pa) = v0;
@@ -574,8 +574,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
               l[e] = c;
             }
             const size_t off = plane_off(row, n0 + wn0 + cq, g.yrows_pad);
-            *reinterpret_cast<f16x8*>(g.Yp + off) = h;
-            *reinterpret_cast<f16x8*>(g.Yp + g.yps + off) = l;
+            st_stream(reinterpret_cast<f16x8*>(g.Yp + off), h);
+            st_stream(reinterpret_cast<f16x8*>(g.Yp + g.yps + off), l);
           }
         }
       }
@@ -664,8 +664,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
 #pragma unroll
           for (int e = 0; e < 8; ++e) x[e] *= sc;
           const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + c4;
-          *reinterpret_cast<f32x4*>(hl.q + off) = f32x4{x[0], x[1], x[2], x[3]};
-          *reinterpret_cast<f32x4*>(hl.q + off + 32) = f32x4{x[4], x[5], x[6], x[7]};
+          st_stream(reinterpret_cast<f32x4*>(hl.q + off), f32x4{x[0], x[1], x[2], x[3]});
+          st_stream(reinterpret_cast<f32x4*>(hl.q + off + 32), f32x4{x[4], x[5], x[6], x[7]});
           if (ppass) {
             *reinterpret_cast<f32x4*>(pa) = f32x4{x[0], x[1], x[2], x[3]};
             *reinterpret_cast<f32x4*>(pb) = f32x4{x[4], x[5], x[6], x[7]};
@@ -709,8 +709,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
             h[e] = a;
             l[e] = c;
           }
-          *reinterpret_cast<f16x8*>(base + off) = h;
-          *reinterpret_cast<f16x8*>(base + hl.pstride + off) = l;
+          st_stream(reinterpret_cast<f16x8*>(base + off), h);
+          st_stream(reinterpret_cast<f16x8*>(base + hl.pstride + off), l);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes

@@ -21,6 +21,10 @@
 #include "common.h"
 #include "kernels.h"
 
+#ifndef LG_SK_NT
+#define LG_SK_NT 1  // streaming (non-temporal) score loads in sinkhorn_scaled_kernel: 5.94 -> 5.21 ms at B = 8, N = 4096
+#endif
+
 namespace lg {
 
 __global__ __launch_bounds__(256) void transpose_kernel(const float* src, float* dst, int M, int N) {
@@ -392,7 +396,11 @@ __global__ __launch_bounds__(W * 64) void sinkhorn_scaled_kernel(const float* __
       const int c = 256 * k + 4 * lane;
       if (VEC) {
         f32x4 t = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#if LG_SK_NT
+        if (c < N) t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane)));
+#else
         if (c < N) t = *reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane));
+#endif
 #pragma unroll
         for (int e = 0; e < 4; ++e) y[k][e] = t[e];
       } else {

@@ -285,6 +285,15 @@ __device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t 
                : "memory");
 }
 
+// the same copy with the non-temporal hint (operands streamed exactly once)
+__device__ __forceinline__ void dma16_nt(const void* base, uint32_t voff, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(base), "s"(lds)
+               : "memory");
+}
+
 __device__ __forceinline__ float log_sigmoid(float x) {
   // logsigmoid(x) = min(x,0) - log1p(exp(-|x|))  (torch's CPU formulation)
   return fminf(x, 0.f) - log1pf(expf(-fabsf(x)));

@@ -69,6 +69,14 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 // 64 only the first NSTAGE k-tiles copied (later ones re-read them: realistic operands, no copy stream)
 #define LG_GEMM_DIAG 0
 #endif
+#ifndef LG_GEMM_A_NT
+// non-temporal A-operand copies (and residual reads) where every row panel is read by one
+// workgroup only (one column tile: ffn.0 + LN, ffn.3, final_proj): streamed once, they should not
+// displace the weights and the attention's K/V in L2 / the Infinity Cache.  configs[2], same box:
+// 1235 -> 1277 pairs/s.  2 = every GEMM: equal at B = 32, but the narrow tiles of small batches
+// and of SuperGlue re-read their A panels per column tile (SuperGlue 2224 -> 1827 pairs/s)
+#define LG_GEMM_A_NT 1
+#endif
 #ifndef LG_GEMM_SETPRIO
 #define LG_GEMM_SETPRIO 0
 #endif
@@ -188,7 +196,12 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
         const int pl = qw / (WPT / 1024), pc = qw % (WPT / 1024);
         src = reinterpret_cast<const char*>(g.W.p + pl * g.W.ps + ((size_t)kt * g.W.rows_pad + n0) * BK) + pc * 1024;
       }
-      dma16(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
+#if LG_GEMM_A_NT
+      // one column tile: every A row panel is read by one workgroup only -- stream it
+      if ((LG_GEMM_A_NT == 2 || num_n == 1) && q < 2 * (APT / 1024)) dma16_nt(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
+      else
+#endif
+        dma16(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
     }
   };
 
@@ -517,7 +530,12 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
             }
             if (g.res) {
               const float* rp = g.res + (size_t)row * g.ldr + n0 + wn0 + c4;
+#if LG_GEMM_A_NT
+              const f32x4 r0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(rp));
+              const f32x4 r1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(rp + 32));
+#else
               const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp), r1 = *reinterpret_cast<const f32x4*>(rp + 32);
+#endif
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 v0[e] = r0[e] + v0[e];

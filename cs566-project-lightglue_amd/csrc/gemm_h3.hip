@@ -77,6 +77,11 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 // and of SuperGlue re-read their A panels per column tile (SuperGlue 2224 -> 1827 pairs/s)
 #define LG_GEMM_A_NT 1
 #endif
+#ifndef LG_GEMM_RES_NT
+// non-temporal stores of the fp32 residual stream (ffn.3 with its residual): next read one layer
+// later, after ~1.5 GB of other traffic; configs[2] +0.4 % same box (1263 -> 1268 pairs/s)
+#define LG_GEMM_RES_NT 1
+#endif
 #ifndef LG_GEMM_SETPRIO
 #define LG_GEMM_SETPRIO 0
 #endif
@@ -550,8 +555,16 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
               }
             if (g.Y) {
               float* yp = g.Y + (size_t)row * g.ldy + n0 + wn0 + c4;
-              st_stream(reinterpret_cast<f32x4*>(yp), v0);
-              st_stream(reinterpret_cast<f32x4*>(yp + 32), v1);
+#if LG_GEMM_RES_NT
+              if (g.res) {  // the residual stream: next read a layer later
+                __builtin_nontemporal_store(v0, reinterpret_cast<f32x4*>(yp));
+                __builtin_nontemporal_store(v1, reinterpret_cast<f32x4*>(yp + 32));
+              } else
+#endif
+              {
+                st_stream(reinterpret_cast<f32x4*>(yp), v0);
+                st_stream(reinterpret_cast<f32x4*>(yp + 32), v1);
+              }
             }
             if (g.Yp) {
               *reinterpret_cast<f32x4*>(pa) = v0;

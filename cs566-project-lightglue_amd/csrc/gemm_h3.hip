@@ -82,6 +82,9 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 // later, after ~1.5 GB of other traffic; configs[2] +0.4 % same box (1263 -> 1268 pairs/s)
 #define LG_GEMM_RES_NT 1
 #endif
+#ifndef LG_GEMM_Q_NT
+#define LG_GEMM_Q_NT 0  // non-temporal query stores: measured +0.9 % and -0.1 % on two same-box pairs (noise), off
+#endif
 #ifndef LG_GEMM_SETPRIO
 #define LG_GEMM_SETPRIO 0
 #endif
@@ -554,7 +557,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
                 v1[e] = fmaxf(v1[e], 0.f);
               }
             if (g.Y) {
-              float* yp = g.Y + (size_t)row * g.ldy + n0 + wn0 + c4;
+              float* yp = (g.Y2 && row >= g.y2_row0 ? g.Y2 + (size_t)(row - g.y2_row0) * g.ldy : g.Y + (size_t)row * g.ldy) +
+                          n0 + wn0 + c4;
 #if LG_GEMM_RES_NT
               if (g.res) {  // the residual stream: next read a layer later
                 __builtin_nontemporal_store(v0, reinterpret_cast<f32x4*>(yp));
@@ -695,8 +699,13 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
 #pragma unroll
           for (int e = 0; e < 8; ++e) x[e] *= sc;
           const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + c4;
+#if LG_GEMM_Q_NT
+          __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, reinterpret_cast<f32x4*>(hl.q + off));
+          __builtin_nontemporal_store(f32x4{x[4], x[5], x[6], x[7]}, reinterpret_cast<f32x4*>(hl.q + off + 32));
+#else
           st_stream(reinterpret_cast<f32x4*>(hl.q + off), f32x4{x[0], x[1], x[2], x[3]});
           st_stream(reinterpret_cast<f32x4*>(hl.q + off + 32), f32x4{x[4], x[5], x[6], x[7]});
+#endif
           if (ppass) {
             *reinterpret_cast<f32x4*>(pa) = f32x4{x[0], x[1], x[2], x[3]};
             *reinterpret_cast<f32x4*>(pb) = f32x4{x[4], x[5], x[6], x[7]};
@@ -895,14 +904,24 @@ namespace lg {
 // max |x| -> M[slot] of a range table (the inputs' bound for the first plane images)
 __global__ void range_absmax_kernel(const float* x, size_t n, unsigned* tab, int slot) {
   float m = 0.f;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(x[i]));
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {  // 16-byte loads over the aligned body
+    const size_t n4 = n / 4;
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+    for (size_t i = t0; i < n4; i += stride) {
+      const f32x4 v = x4[i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+    for (size_t i = n4 * 4 + t0; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  } else {
+    for (size_t i = t0; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  }
   range_commit(RangeOut{tab, -1, -1, 0.f, 0.f, 0.f, slot, 1}, m, 0);
 }
 
 hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  const size_t blocks = std::min<size_t>((n + 255) / 256, 1024);
+  const size_t blocks = std::min<size_t>((n / 4 + 255) / 256 + 1, 1024);
   hipLaunchKernelGGL(range_absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, tab, slot);
   return hipGetLastError();
 }

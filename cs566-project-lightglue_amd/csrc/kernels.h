@@ -137,6 +137,8 @@ struct GemmH3Args {
   int ldr;
   float* Y;           // EPI_STORE fp32 output (nullable), row stride ldy
   int ldy;
+  float* Y2;          // EPI_STORE (nullable): rows >= y2_row0 go to Y2 + (row - y2_row0) * ldy instead
+  int y2_row0;
   _Float16* Yp;       // EPI_STORE: also write Y as a plane image (nullable), with its rows_pad
   long long yps;
   int yrows_pad;

@@ -786,6 +786,12 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
 
   const float thr_w = (float)(1.0 - c.width_confidence);  // python-float arithmetic, then fp32 compare
   const int R = B * (M + N);
+  // the last layer's ffn.3 writes the final descriptors straight into ref_descriptors0/1 (no copy)
+  // when every pair runs every layer and nothing reads the fp32 stream after it
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const bool direct_out = prec == PREC_H3 && !seg && !do_stop && !do_prune && out->ref_descriptors0 &&
+                          out->ref_descriptors1 && a16(out->ref_descriptors0) && a16(out->ref_descriptors1) &&
+                          !out->layer_descriptors0 && !out->layer_descriptors1;
   for (int i = 0; i < L; ++i) {
     const LayerW& lw = h->layers[i];
     for (int blk = 0; blk < 2; ++blk) {
@@ -865,6 +871,11 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         g.A0 = image(w.Hp, 2 * D); g.K0 = 2 * D; g.K = 2 * D; wplanes(g, bw.W2); g.bias = Wb + bw.b2;
         g.rtab = rt; g.a0_slot = s_h; g.rm = live;  // frozen / dead rows keep their residual stream
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
+        if (direct_out && i == L - 1 && blk == 1) {  // the final descriptors straight into the outputs
+          g.Y = out->ref_descriptors0;
+          g.Y2 = out->ref_descriptors1;
+          g.y2_row0 = B * M;
+        }
         g.Yp = w.Xp; g.yps = (long long)RP * D; g.yrows_pad = RP;
         g.ro = ro(s_x, 1.f, -1, 0.f, gn.g2 * gn.hb + gn.b2, s_xn, 1);  // |x + ffn(..)| <= M_x + |W2|_1 hb + |b2|
         LG_HIP(gemmh(g, EPI_STORE));
@@ -958,7 +969,12 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       g.R = R; g.Nout = D; g.Y = w.md; g.ldy = D; g.out_scale = 0.25f; g.rm = m;  // / d**0.25
       LG_HIP(gemm(g, EPI_STORE, 1));
     }
-    LG_HIP(gemv_256_masked(w.X, Wb + la.wm, Wb + la.bm, w.z, R, m, st));
+    if (direct_out) {  // the final fp32 descriptors live in the outputs (every row live)
+      LG_HIP(gemv_256_masked(out->ref_descriptors0, Wb + la.wm, Wb + la.bm, w.z, B * M, m, st));
+      LG_HIP(gemv_256_masked(out->ref_descriptors1, Wb + la.wm, Wb + la.bm, w.z + (size_t)B * M, B * N, m, st));
+    } else {
+      LG_HIP(gemv_256_masked(w.X, Wb + la.wm, Wb + la.bm, w.z, R, m, st));
+    }
     return LG_OK;
   };
   if (do_stop) {
@@ -1017,9 +1033,9 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       LG_HIP(assign(aa));
     }
   }
-  if (out->ref_descriptors0)
+  if (out->ref_descriptors0 && !direct_out)
     LG_HIP(hipMemcpyAsync(out->ref_descriptors0, w.X, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
-  if (out->ref_descriptors1)
+  if (out->ref_descriptors1 && !direct_out)
     LG_HIP(hipMemcpyAsync(out->ref_descriptors1, w.X + (size_t)B * M * D, sizeof(float) * B * N * D,
                           hipMemcpyDeviceToDevice, st));
   // kept counts and stop layers: on the device for the caller, and (one read-back, the only

@@ -206,7 +206,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
       }
 #if LG_GEMM_A_NT
       // one column tile: every A row panel is read by one workgroup only -- stream it
-      if ((LG_GEMM_A_NT == 2 || num_n == 1) && q < 2 * (APT / 1024)) dma16_nt(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
+      if (g.stream && (LG_GEMM_A_NT == 2 || num_n == 1) && q < 2 * (APT / 1024))
+        dma16_nt(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
       else
 #endif
         dma16(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
@@ -538,12 +539,14 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
             }
             if (g.res) {
               const float* rp = g.res + (size_t)row * g.ldr + n0 + wn0 + c4;
-#if LG_GEMM_A_NT
-              const f32x4 r0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(rp));
-              const f32x4 r1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(rp + 32));
-#else
-              const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp), r1 = *reinterpret_cast<const f32x4*>(rp + 32);
-#endif
+              f32x4 r0, r1;
+              if (LG_GEMM_A_NT && g.stream) {
+                r0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(rp));
+                r1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(rp + 32));
+              } else {
+                r0 = *reinterpret_cast<const f32x4*>(rp);
+                r1 = *reinterpret_cast<const f32x4*>(rp + 32);
+              }
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 v0[e] = r0[e] + v0[e];
@@ -560,7 +563,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
               float* yp = (g.Y2 && row >= g.y2_row0 ? g.Y2 + (size_t)(row - g.y2_row0) * g.ldy : g.Y + (size_t)row * g.ldy) +
                           n0 + wn0 + c4;
 #if LG_GEMM_RES_NT
-              if (g.res) {  // the residual stream: next read a layer later
+              if (g.res && g.stream) {  // the residual stream: next read a layer later
                 __builtin_nontemporal_store(v0, reinterpret_cast<f32x4*>(yp));
                 __builtin_nontemporal_store(v1, reinterpret_cast<f32x4*>(yp + 32));
               } else
@@ -824,7 +827,17 @@ static int gemm_tile_for(long long big_tiles) {
 // (layernorm_gelu_512, which writes the same plane image)
 bool gemm_h3_ln_split(int R) { return use_small_tiles((R + 127) / 128) && gemm_tile_override() != TILE_BIG; }
 
-hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st) {
+// Streamed-once hints (LG_GEMM_A_NT / LG_GEMM_RES_NT) only for operands too big to stay cached:
+// A at least LG_NT_MIN_MB (default 128) MiB.  Smaller working sets (SuperGlue's 32k rows, pruned
+// tails) live in the 256 MiB Infinity Cache from one kernel to the next.
+static size_t nt_min_bytes() {
+  const char* e = getenv("LG_NT_MIN_MB");
+  return (size_t)(e ? atof(e) : 128.0) << 20;
+}
+
+hipError_t gemm_h3(const GemmH3Args& a_in, int epi, hipStream_t st) {
+  GemmH3Args a = a_in;
+  a.stream = (size_t)a.R * a.K * 4 >= nt_min_bytes();
   if (a.R <= 0) return hipSuccess;
   if (a.Nout % TB || a.K % kKB || a.K0 % kKB || a.K0 <= 0 || a.K0 > a.K || (a.K0 < a.K && !a.A1.p) || !a.A0.p ||
       !a.W.p || a.A0.rows_pad < ((a.R + TB - 1) / TB) * TB || (a.K0 < a.K && a.A1.rows_pad < ((a.R + TB - 1) / TB) * TB) ||

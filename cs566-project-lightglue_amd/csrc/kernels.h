@@ -139,6 +139,7 @@ struct GemmH3Args {
   int ldy;
   float* Y2;          // EPI_STORE (nullable): rows >= y2_row0 go to Y2 + (row - y2_row0) * ldy instead
   int y2_row0;
+  int stream;         // set by gemm_h3: operands too big for the caches take the non-temporal hints
   _Float16* Yp;       // EPI_STORE: also write Y as a plane image (nullable), with its rows_pad
   long long yps;
   int yrows_pad;

@@ -43,6 +43,17 @@ __device__ __forceinline__ int xcd_chunk(int id, int n) {
   const int base = n >> 3, extra = n & 7;
   return xcd * base + (xcd < extra ? xcd : extra) + local;
 }
+#ifndef LG_ATTN_REVERSE
+#define LG_ATTN_REVERSE 1  // configs[2] three same-box pairs: 1326 vs 1321 pairs/s, attention -0.6 %
+#endif
+// the same chunks, each XCD walking its chunk from the end: the QKV GEMM wrote every XCD's rows
+// front to back, so the newest q/k/v (the ones still in the Infinity Cache) come first
+__device__ __forceinline__ int xcd_chunk_rev(int id, int n) {
+  const int xcd = id & 7, local = id >> 3;
+  const int base = n >> 3, extra = n & 7;
+  const int cnt = base + (xcd < extra ? 1 : 0);
+  return xcd * base + (xcd < extra ? xcd : extra) + (cnt - 1 - local);
+}
 
 __device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
   const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
@@ -340,7 +351,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   __shared__ __attribute__((aligned(16))) _Float16 Ks[2 * 2 * PL];
   __shared__ __attribute__((aligned(16))) _Float16 Vs[2 * 2 * PL];
 
-  int item = xcd_chunk(blockIdx.x, gridDim.x);
+  int item = LG_ATTN_REVERSE ? xcd_chunk_rev(blockIdx.x, gridDim.x) : xcd_chunk(blockIdx.x, gridDim.x);
   int split = 0;
   if constexpr (SPLIT) {
     split = item % nsplit;

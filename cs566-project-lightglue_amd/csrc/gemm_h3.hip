@@ -39,10 +39,11 @@ namespace lg {
 namespace {
 constexpr int TB = 256;  // column tile; rows_pad granule
 
-__device__ __forceinline__ int xcd_remap_h3(int id, int n) {
+__device__ __forceinline__ int xcd_remap_h3(int id, int n, bool rev = false) {
   const int xcd = id & 7, local = id >> 3;
   const int base = n >> 3, extra = n & 7;
-  return xcd * base + (xcd < extra ? xcd : extra) + local;
+  const int cnt = base + (xcd < extra ? 1 : 0);
+  return xcd * base + (xcd < extra ? xcd : extra) + (rev ? cnt - 1 - local : local);
 }
 
 __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, int& base, int& stride) {
@@ -142,7 +143,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
   const int eo_v = (EPI == EPI_QKV_ROT || EPI == EPI_CROSS_QKV) ? range_exponent(g.ro_v) : 0;
 
   const int num_m = (g.R + BM - 1) / BM, num_n = g.Nout / BN;
-  const int tile = xcd_remap_h3(blockIdx.x, num_m * num_n);
+  const int tile = xcd_remap_h3(blockIdx.x, num_m * num_n, g.reverse != 0);
   const int tm = tile / num_n, tn = tile - tm * num_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = g.K / BK, nk0 = g.K0 / BK;

@@ -140,6 +140,7 @@ struct GemmH3Args {
   float* Y2;          // EPI_STORE (nullable): rows >= y2_row0 go to Y2 + (row - y2_row0) * ldy instead
   int y2_row0;
   int stream;         // set by gemm_h3: operands too big for the caches take the non-temporal hints
+  int reverse;        // walk each XCD's tile range from its end (read what the previous kernel wrote last first)
   _Float16* Yp;       // EPI_STORE: also write Y as a plane image (nullable), with its rows_pad
   long long yps;
   int yrows_pad;

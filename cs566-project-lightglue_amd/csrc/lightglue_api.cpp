@@ -154,6 +154,8 @@ struct lg_handle {
   bool pass_started = false;  // forward_pass got past argument checks (work was enqueued)
   // fold out_proj / to_out into ffn.0 at load time (env LG_FOLD_OUT_PROJ=0 disables)
   bool fold = true;
+  // ffn.3 walks its tiles back to front (the LN GEMM's newest output first; LG_FFN3_REVERSE=0|1)
+  int ffn3_reverse = 1;
   // profiling (lg_profile_enable / lg_profile_read)
   struct Rec {
     hipEvent_t a, b;
@@ -419,6 +421,7 @@ int lg_create(const lg_config_t* cfg, int device, lg_handle_t** out) {
   h->cfg = *cfg;
   h->device = device;
   if (const char* f = getenv("LG_FOLD_OUT_PROJ")) h->fold = atoi(f) != 0;
+  if (const char* f = getenv("LG_FFN3_REVERSE")) h->ffn3_reverse = atoi(f) != 0;
   h->schema = make_schema(*cfg);
   for (size_t k = 0; k < h->schema.size(); ++k) h->index[h->schema[k].name] = (int)k;
   plan_layout(h);
@@ -871,6 +874,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         g.A0 = image(w.Hp, 2 * D); g.K0 = 2 * D; g.K = 2 * D; wplanes(g, bw.W2); g.bias = Wb + bw.b2;
         g.rtab = rt; g.a0_slot = s_h; g.rm = live;  // frozen / dead rows keep their residual stream
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
+        g.reverse = h->ffn3_reverse;  // read the hidden planes the LN GEMM wrote last first
         if (direct_out && i == L - 1 && blk == 1) {  // the final descriptors straight into the outputs
           g.Y = out->ref_descriptors0;
           g.Y2 = out->ref_descriptors1;

@@ -43,6 +43,12 @@ __device__ __forceinline__ int xcd_chunk(int id, int n) {
   const int base = n >> 3, extra = n & 7;
   return xcd * base + (xcd < extra ? xcd : extra) + local;
 }
+#ifndef LG_ATTN_CTX_NT
+// context planes with the non-temporal hint: -0.1 ms per forward while the attention walked its
+// items front to back; with the reversed walk the LN GEMM reads the newest context first and
+// cached stores win (three same-box pairs: 1312 vs 1301 pairs/s)
+#define LG_ATTN_CTX_NT 0
+#endif
 #ifndef LG_ATTN_REVERSE
 #define LG_ATTN_REVERSE 1  // configs[2] three same-box pairs: 1326 vs 1321 pairs/s, attention -0.6 %
 #endif
@@ -677,9 +683,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
           l[e] = c;
         }
         const size_t off = plane_off(orow, head * kHeadDim + 16 * dt + 4 * g, S.o_rows_pad);
-        // non-temporal: -0.1 ms per 32-pair forward (the GEMM epilogues' stores lose by it)
+#if LG_ATTN_CTX_NT
         __builtin_nontemporal_store(h, reinterpret_cast<f16x4*>(S.op + off));
         __builtin_nontemporal_store(l, reinterpret_cast<f16x4*>(S.op + S.ops + off));
+#else
+        *reinterpret_cast<f16x4*>(S.op + off) = h;
+        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+#endif
       }
     }
   }
@@ -1070,9 +1080,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
           l[e] = c;
         }
         const size_t off = plane_off(orow, head * kHeadDim + hf * 32 + 8 * g + 4 * half, S.o_rows_pad);
-        // non-temporal: -0.1 ms per 32-pair forward (the GEMM epilogues' stores lose by it)
+#if LG_ATTN_CTX_NT
         __builtin_nontemporal_store(h, reinterpret_cast<f16x4*>(S.op + off));
         __builtin_nontemporal_store(l, reinterpret_cast<f16x4*>(S.op + S.ops + off));
+#else
+        *reinterpret_cast<f16x4*>(S.op + off) = h;
+        *reinterpret_cast<f16x4*>(S.op + S.ops + off) = l;
+#endif
       }
   }
 }

@@ -308,9 +308,6 @@ __device__ __forceinline__ f16x4 tr_read_h(const _Float16* p) {
 //     cross-lane step between the score MFMAs and the exponentials.
 // ----------------------------------------------------------------------------------------
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-#ifndef LG_ATTN_Q_NT
-#define LG_ATTN_Q_NT 0
-#endif
 
 // (e0 - hs[0], e1 - hs[1]) rounded to fp16, one instruction per element (both differences are
 // exact in fp32: hs = fp16(e))
@@ -412,13 +409,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
     float mx = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-#if LG_ATTN_Q_NT
-      x[ks][0] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(qr + 32 * ks));
-      x[ks][1] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(qr + 32 * ks + 4));
-#else
       x[ks][0] = *reinterpret_cast<const f32x4*>(qr + 32 * ks);
       x[ks][1] = *reinterpret_cast<const f32x4*>(qr + 32 * ks + 4);
-#endif
 #pragma unroll
       for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[ks][0][e]), fabsf(x[ks][1][e])));
     }

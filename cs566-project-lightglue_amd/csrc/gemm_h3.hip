@@ -83,9 +83,6 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 // later, after ~1.5 GB of other traffic; configs[2] +0.4 % same box (1263 -> 1268 pairs/s)
 #define LG_GEMM_RES_NT 1
 #endif
-#ifndef LG_GEMM_Q_NT
-#define LG_GEMM_Q_NT 0  // non-temporal query stores: measured +0.9 % and -0.1 % on two same-box pairs (noise), off
-#endif
 #ifndef LG_GEMM_SETPRIO
 #define LG_GEMM_SETPRIO 0
 #endif
@@ -703,13 +700,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
 #pragma unroll
           for (int e = 0; e < 8; ++e) x[e] *= sc;
           const size_t off = (size_t)rowinfo[2 * lr] + (size_t)head * rowinfo[2 * lr + 1] + c4;
-#if LG_GEMM_Q_NT
-          __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, reinterpret_cast<f32x4*>(hl.q + off));
-          __builtin_nontemporal_store(f32x4{x[4], x[5], x[6], x[7]}, reinterpret_cast<f32x4*>(hl.q + off + 32));
-#else
           st_stream(reinterpret_cast<f32x4*>(hl.q + off), f32x4{x[0], x[1], x[2], x[3]});
           st_stream(reinterpret_cast<f32x4*>(hl.q + off + 32), f32x4{x[4], x[5], x[6], x[7]});
-#endif
           if (ppass) {
             *reinterpret_cast<f32x4*>(pa) = f32x4{x[0], x[1], x[2], x[3]};
             *reinterpret_cast<f32x4*>(pb) = f32x4{x[4], x[5], x[6], x[7]};

@@ -71,11 +71,11 @@ __device__ __forceinline__ void head_row_base_h3(const HeadLayout& hl, int row, 
 #define LG_GEMM_DIAG 0
 #endif
 #ifndef LG_GEMM_A_NT
-// non-temporal A-operand copies (and residual reads) where every row panel is read by one
-// workgroup only (one column tile: ffn.0 + LN, ffn.3, final_proj): streamed once, they should not
-// displace the weights and the attention's K/V in L2 / the Infinity Cache.  configs[2], same box:
-// 1235 -> 1277 pairs/s.  2 = every GEMM: equal at B = 32, but the narrow tiles of small batches
-// and of SuperGlue re-read their A panels per column tile (SuperGlue 2224 -> 1827 pairs/s)
+// non-temporal A-operand copies (and residual reads) for operands of at least LG_NT_MIN_MB
+// (gemm_h3): streamed once, they should not displace the weights and the attention's q/k/v in the
+// Infinity Cache.  configs[2], same box: 1235 -> 1277 pairs/s for the single-column-tile GEMMs,
+// +0.5 % more for QKV and cross QKV as well (three pairs, attention -0.7 %).  Ungated (every size)
+// it cost the cache-resident SuperGlue / small-batch forwards
 #define LG_GEMM_A_NT 1
 #endif
 #ifndef LG_GEMM_RES_NT
@@ -203,8 +203,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
         src = reinterpret_cast<const char*>(g.W.p + pl * g.W.ps + ((size_t)kt * g.W.rows_pad + n0) * BK) + pc * 1024;
       }
 #if LG_GEMM_A_NT
-      // one column tile: every A row panel is read by one workgroup only -- stream it
-      if (g.stream && (LG_GEMM_A_NT == 2 || num_n == 1) && q < 2 * (APT / 1024))
+      // A too big to stay cached: its row panels are read by the column tiles of one XCD within
+      // microseconds (L2) and never again -- stream them past the Infinity Cache
+      if (g.stream && q < 2 * (APT / 1024))
         dma16_nt(src, voff, lds0 + stage * STAGE_BYTES + q * 1024);
       else
 #endif
@@ -830,7 +831,7 @@ static size_t nt_min_bytes() {
 
 hipError_t gemm_h3(const GemmH3Args& a_in, int epi, hipStream_t st) {
   GemmH3Args a = a_in;
-  a.stream = (size_t)a.R * a.K * 4 >= nt_min_bytes();
+  a.stream = LG_GEMM_A_NT && (size_t)a.R * a.K * 4 >= nt_min_bytes();
   if (a.R <= 0) return hipSuccess;
   if (a.Nout % TB || a.K % kKB || a.K0 % kKB || a.K0 <= 0 || a.K0 > a.K || (a.K0 < a.K && !a.A1.p) || !a.A0.p ||
       !a.W.p || a.A0.rows_pad < ((a.R + TB - 1) / TB) * TB || (a.K0 < a.K && a.A1.rows_pad < ((a.R + TB - 1) / TB) * TB) ||

@@ -124,7 +124,8 @@ def test_forward_matches_reference_golden(name, precision):
                                                                      ("small", "8", "sim_h3", "h3g", "2", "auto"),
                                                                      ("big", "2", "sim_h3", "h3m", "4", "auto"),
                                                                      ("medium", "4", "sim_h3", "h3g", "4", "1"),
-                                                                     ("small", "4", "sim_h3", "h3g", "4", "8")])
+                                                                     ("small", "4", "sim_h3", "h3g", "4", "8"),
+                                                                     ("big", "8", "sim_h3", "h3g", "nt", "auto")])
 @pytest.mark.parametrize("name", case_names())
 def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, ksplit, asplit, monkeypatch):
     """The fp16x3 GEMM picks 256x256 tiles (throughput), 128x128 tiles (fewer big tiles than CUs)
@@ -138,7 +139,11 @@ def test_forward_golden_all_launch_shapes(name, tile, waves, assign, kernel, ksp
     the 4-wave attention splits the keys of small batches over LG_ATTN_SPLIT workgroups (auto: up
     to 8, merged by attn_split_combine_kernel; 1 = unsplit)."""
     monkeypatch.setenv("LG_GEMM_TILE", tile)
-    monkeypatch.setenv("LG_GEMM_KSPLIT", ksplit)
+    if ksplit == "nt":  # the streamed-once hints at every size, ffn.3 walking front to back
+        monkeypatch.setenv("LG_NT_MIN_MB", "0")
+        monkeypatch.setenv("LG_FFN3_REVERSE", "0")
+    else:
+        monkeypatch.setenv("LG_GEMM_KSPLIT", ksplit)
     if asplit != "auto":
         monkeypatch.setenv("LG_ATTN_SPLIT", asplit)
     monkeypatch.setenv("LG_ATTN_WAVES", waves)

@@ -93,7 +93,9 @@ typedef struct {
   float* matching_scores0;      /* device [B,M]  (required) */
   float* matching_scores1;      /* device [B,N]  (required) */
   float* log_assignment;        /* device [B,M+1,N+1] or NULL (with pruning: pair b's kept block, see kept) */
-  float* ref_descriptors0;      /* device [B,M,256] or NULL: final descriptors (first M' rows valid) */
+  float* ref_descriptors0;      /* device [B,M,256] or NULL: final descriptors (first M' rows valid);
+                                 * without pruning / early stop and with both buffers 16-byte aligned
+                                 * the last layer writes them in place (no copy) */
   float* ref_descriptors1;      /* device [B,N,256] or NULL */
   int64_t* prune0;              /* device [B,M] or NULL: layer count per point (lightglue.py:511,540,564) */
   int64_t* prune1;              /* device [B,N] or NULL */

@@ -336,11 +336,17 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if constexpr (KS > 1) {
-    // partials of groups 1.. into their own (now idle) rings, lane-major (conflict-free); wave 0
-    // adds them in group order and carries on alone (s_barrier waits only for surviving waves)
+    // every group leaves its partial accumulator in LDS, lane-major (conflict-free): group 0 in the
+    // upper half of its ring (the lower half takes the two epilogue waves' transpose buffers),
+    // groups 1.. in their own (idle) rings.  Groups 0 and 1 then each add the other partials in
+    // group order (p0 + p1 = p1 + p0 exactly, so both hold the same sum) and each runs the epilogue
+    // for one 32-row half of the tile; groups 2.. leave (s_barrier waits only for surviving waves)
     constexpr int NA = TI * TJ * TR;
-    if (ks > 0) {
-      float* pp = reinterpret_cast<float*>(smem + ks * RING);
+    static_assert(NA == 64, "single-wave 64 x 64 tile");
+    static_assert(RING >= 2 * 64 * 64 * 4, "split-k: partial + transpose buffers fit the ring");
+    auto part = [&](int q) { return reinterpret_cast<float*>(smem + q * RING + (q == 0 ? RING / 2 : 0)); };
+    {
+      float* pp = part(ks);
       int x = 0;
 #pragma unroll
       for (int i = 0; i < TI; ++i)
@@ -348,15 +354,15 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
         for (int j = 0; j < TJ; ++j)
 #pragma unroll
           for (int r = 0; r < TR; ++r, ++x) pp[x * 64 + lane] = acc[i][j][r];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      return;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (ks >= 2) return;
 #pragma unroll
-    for (int q = 1; q < KS; ++q) {
-      const float* pp = reinterpret_cast<const float*>(smem + q * RING);
+    for (int q = 0; q < KS; ++q) {
+      if (q == ks) continue;
+      const float* pp = part(q);
       int x = 0;
 #pragma unroll
       for (int i = 0; i < TI; ++i)
@@ -365,8 +371,12 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
 #pragma unroll
           for (int r = 0; r < TR; ++r, ++x) acc[i][j][r] += pp[x * 64 + lane];
     }
-    static_assert(NA == 64, "single-wave 64 x 64 tile");
   }
+  // waves running the epilogue, and this wave's share: split-k tiles give each of groups 0 and 1
+  // one 32-row pass (i == ks), otherwise a wave runs both passes of its own tile
+  constexpr int EW = KS > 1 ? 2 : NW;
+  const int ep_wave = KS > 1 ? ks : wave;
+  auto my_pass = [&](int i) { return KS == 1 || i == ks; };
 
   // ------------------------------------------------------------------ epilogues
   float wmax = 0.f;  // max |x| this lane wrote into planes (RangeOut tracking)
@@ -500,8 +510,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     // write half lines, which measured 2x the cost per byte); the finished values go back into the
     // LDS slots they came from and the plane pass re-reads them as 8 consecutive columns (one
     // 16-byte fp16 chunk per plane: consecutive rows of a k-block are contiguous).
-    static_assert(NW * 32 * 64 * 4 <= NSTAGE * STAGE_BYTES, "epilogue scratch");
-    float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
+    static_assert(EW * 32 * 64 * 4 <= NSTAGE * STAGE_BYTES, "epilogue scratch");
+    float* ep = reinterpret_cast<float*>(smem) + ep_wave * (32 * 64);
     const int cq = (lane & 7) * 8;  // plane pass: the lane's 8 columns (in the wave tile)
     const int c4 = (lane & 7) * 4;  // fp32 pass: columns c4 .. c4+3 and 32 + c4 ..
     const int eo = g.Yp ? eo_main : 0;
@@ -515,6 +525,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (!my_pass(i)) continue;
       visit(i, [&](int rr, int c, float v) {
         ep[rr * 64 + (c ^ ((rr & 1) << 2))] = v;
         return v;
@@ -618,7 +629,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
-    if (g.Yp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem), NW);
+    if (g.Yp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem), EW);
   } else {
     static_assert(WN == 64, "QKV epilogue tile");
     // Head-major scatter through the same LDS transpose as EPI_STORE.  The wave's 64 columns are
@@ -644,7 +655,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     const float sc = (EPI == EPI_CROSS_QKV && t == 0) ? hl.qk_scale : 1.f;
     const int eo = to_kp ? eo_main : to_vp ? eo_v : 0;
     const float so = ldexpf(1.f, -eo);
-    float* ep = reinterpret_cast<float*>(smem) + wave * (32 * 64);
+    float* ep = reinterpret_cast<float*>(smem) + ep_wave * (32 * 64);
     // fp32 rows (q, qk) go out as full 128-byte lines per 8 lanes (lane dims c4 .. c4+3 and
     // 32 + c4 ..: two rotary pairs each); plane rows as one 16-byte chunk per lane (dims d0 ..
     // d0+7).  qk (cross) needs both: the fp32 pass puts its finished values back into LDS and the
@@ -669,6 +680,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     };
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (!my_pass(i)) continue;
       visit(i, [&](int rr, int c, float v) {
         const int dim = c < 32 ? 2 * c : 2 * (c - 32) + 1;
         ep[rr * 64 + (dim ^ ((rr & 1) << 2))] = v;
@@ -752,8 +764,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass writes
     }
-    if (to_kp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem), NW);
-    else if (to_vp) range_commit_lds(g.ro_v, wmax, eo, reinterpret_cast<float*>(smem), NW);
+    if (to_kp) range_commit_lds(g.ro, wmax, eo, reinterpret_cast<float*>(smem), EW);
+    else if (to_vp) range_commit_lds(g.ro_v, wmax, eo, reinterpret_cast<float*>(smem), EW);
   }
 }
 

@@ -17,11 +17,13 @@ using namespace lg;
 
 struct Shape { int R, K, N; const char* name; };
 
+__global__ void empty_kernel() {}
+
 static _Float16* g_planes = nullptr;  // plane image of W * 2^sw
 static _Float16* g_aplanes = nullptr; // plane image of A
 static float g_unscale = 1.f;
 
-template <int BM, int NS, int EPI = EPI_STORE, int BN = 256, int WN = 64>
+template <int BM, int NS, int EPI = EPI_STORE, int BN = 256, int WN = 64, int KS = 1>
 double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out, _Float16* Yp, int stagger = 0) {
   GemmH3Args a;
   memset(&a, 0, sizeof(a));
@@ -32,10 +34,10 @@ double run_h3(const Shape& s, float* bias, float* Y, int iters, bool planes_out,
   if (planes_out) { a.Yp = Yp; a.yps = (long long)s.R * s.N; a.yrows_pad = s.R; }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  CK((gemm_h3_launch<BM, NS, BN, WN>(a, EPI, 0)));
+  CK((gemm_h3_launch<BM, NS, BN, WN, KS>(a, EPI, 0)));
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK((gemm_h3_launch<BM, NS, BN, WN>(a, EPI, 0)));
+  for (int i = 0; i < iters; ++i) CK((gemm_h3_launch<BM, NS, BN, WN, KS>(a, EPI, 0)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -129,8 +131,28 @@ __global__ void ref64(const float* A, const float* W, const float* bias, double*
 }
 
 int main() {
-  const Shape shapes[] = {{131072, 32, 768, "k32"}, {131072, 256, 768, "qkv"}, {131072, 512, 512, "ffn1"},
-                          {131072, 512, 256, "ffn2"}, {131072, 256, 256, "outp"}};
+  const Shape big_shapes[] = {{131072, 32, 768, "k32"}, {131072, 256, 768, "qkv"}, {131072, 512, 512, "ffn1"},
+                              {131072, 512, 256, "ffn2"}, {131072, 256, 256, "outp"}};
+  // KB_SMALL: the B = 1, N = 1024 forward's GEMMs (R = 2048 rows), small-tile launch shapes
+  const Shape small_shapes[] = {{2048, 256, 768, "qkv"}, {2048, 512, 512, "ffn1"}, {2048, 512, 256, "ffn2"},
+                                {2048, 256, 512, "xqk"}};
+  const bool small = getenv("KB_SMALL") != nullptr;
+  if (small) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    empty_kernel<<<256, 256>>>();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < 100; ++i) empty_kernel<<<256, 256>>>();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("empty kernel, 256 x 256 threads: %.2f us per launch\n", ms * 10.f);
+  }
+  std::vector<Shape> shapes;
+  if (small) shapes.assign(std::begin(small_shapes), std::end(small_shapes));
+  else shapes.assign(std::begin(big_shapes), std::end(big_shapes));
   const int RR = 512;  // rows checked against fp64
   for (const Shape& s : shapes) {
     float *A, *W, *bias, *Y;
@@ -188,6 +210,14 @@ int main() {
       fill<<<(s.N + 255) / 256, 256>>>(bet, s.N, 5);
       ms = run_ln<64>(s, bias, gam, bet, Yp, it); rep("h3  LN+GELU 128x512", ms, false);
       CK(hipFree(gam)); CK(hipFree(bet));
+      continue;
+    }
+    if (small) {  // latency decomposition (build with -DLG_GEMM_DIAG=0 / 2 no copies / 4 no waits)
+      ms = run_h3<64, 2, EPI_STORE, 64, 64, 4>(s, bias, Y, it, false, Yp); rep("64x64 ks4, fp32 out", ms, !LG_GEMM_DIAG);
+      ms = run_h3<64, 2, EPI_STORE, 64, 64, 4>(s, bias, Y, it, true, Yp); rep("64x64 ks4, fp32 + planes", ms, !LG_GEMM_DIAG);
+      ms = run_h3<64, 2, EPI_PROBE, 64, 64, 4>(s, bias, Y, it, false, Yp); rep("64x64 ks4, no epilogue", ms, false);
+      ms = run_h3<64, 4, EPI_STORE, 64, 64, 2>(s, bias, Y, it, false, Yp); rep("64x64 ks2, fp32 out", ms, !LG_GEMM_DIAG);
+      ms = run_h3<64, 4, EPI_STORE, 64, 64, 1>(s, bias, Y, it, false, Yp); rep("64x64 ks1, fp32 out", ms, !LG_GEMM_DIAG);
       continue;
     }
     if (getenv("KB_QUICK")) {  // k-loop probes (build with -DLG_GEMM_DIAG=0/1/2)

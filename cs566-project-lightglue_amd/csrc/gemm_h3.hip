@@ -335,16 +335,17 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  // waves running the epilogue: split-k tiles give each group 16 rows of the tile (4 groups, 16 x 16
+  // MFMA tiles) or 32 (2 groups); otherwise a wave runs both 32-row passes of its own tile
+  constexpr int EW = KS > 1 ? (kMF16 && KS >= 4 ? 4 : 2) : NW;
   if constexpr (KS > 1) {
-    // every group leaves its partial accumulator in LDS, lane-major (conflict-free): group 0 in the
-    // upper half of its ring (the lower half takes the two epilogue waves' transpose buffers),
-    // groups 1.. in their own (idle) rings.  Groups 0 and 1 then each add the other partials in
-    // group order (p0 + p1 = p1 + p0 exactly, so both hold the same sum) and each runs the epilogue
-    // for one 32-row half of the tile; groups 2.. leave (s_barrier waits only for surviving waves)
-    constexpr int NA = TI * TJ * TR;
-    static_assert(NA == 64, "single-wave 64 x 64 tile");
-    static_assert(RING >= 2 * 64 * 64 * 4, "split-k: partial + transpose buffers fit the ring");
-    auto part = [&](int q) { return reinterpret_cast<float*>(smem + q * RING + (q == 0 ? RING / 2 : 0)); };
+    // every group leaves its partial accumulator in the upper half of its (idle) ring, lane-major
+    // (conflict-free); the lower half becomes its transpose buffer.  Each epilogue group then adds
+    // up the partials of its own rows in group order, p0 + p1 + p2 + ..., the same order for every
+    // row whichever group stores it; groups beyond EW leave (s_barrier waits only for surviving waves)
+    static_assert(TI * TJ * TR == 64, "single-wave 64 x 64 tile");
+    static_assert(RING >= 2 * 64 * 64 * 4, "split-k: partial + transpose buffer fit the ring");
+    auto part = [&](int q) { return reinterpret_cast<float*>(smem + q * RING + RING / 2); };
     {
       float* pp = part(ks);
       int x = 0;
@@ -358,25 +359,26 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (ks >= 2) return;
+    if (ks >= EW) return;
 #pragma unroll
-    for (int q = 0; q < KS; ++q) {
-      if (q == ks) continue;
-      const float* pp = part(q);
-      int x = 0;
+    for (int i = 0; i < TI; ++i) {
+      if (EW == 4 ? i != ks : (i * 2 / TI) != ks) continue;  // MFMA row tiles this group stores
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+      for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
+        for (int r = 0; r < TR; ++r) {
+          const int x = (i * TJ + j) * TR + r;
+          float v = part(0)[x * 64 + lane];
 #pragma unroll
-          for (int r = 0; r < TR; ++r, ++x) acc[i][j][r] += pp[x * 64 + lane];
+          for (int q = 1; q < KS; ++q) v += part(q)[x * 64 + lane];
+          acc[i][j][r] = v;
+        }
     }
   }
-  // waves running the epilogue, and this wave's share: split-k tiles give each of groups 0 and 1
-  // one 32-row pass (i == ks), otherwise a wave runs both passes of its own tile
-  constexpr int EW = KS > 1 ? 2 : NW;
-  const int ep_wave = KS > 1 ? ks : wave;
-  auto my_pass = [&](int i) { return KS == 1 || i == ks; };
+  float* const ep_buf = KS > 1 ? reinterpret_cast<float*>(smem + ks * RING) : reinterpret_cast<float*>(smem) + wave * (32 * 64);
+  // this wave's 32-row passes, and within a pass its 8-row store groups k (rows 8k .. 8k+7)
+  auto my_pass = [&](int i) { return KS == 1 || (EW == 4 ? i == (ks >> 1) : i == ks); };
+  auto my_rows = [&](int k) { return KS == 1 || EW != 4 || (k >> 1) == (ks & 1); };
 
   // ------------------------------------------------------------------ epilogues
   float wmax = 0.f;  // max |x| this lane wrote into planes (RangeOut tracking)
@@ -476,6 +478,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+          if (!my_rows(k)) continue;
           const int rr = (lane >> 3) + 8 * k;
           const int row = m0 + wm0 + i * 32 + rr;
           const int sw = (rr & 1) << 2;
@@ -510,8 +513,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     // write half lines, which measured 2x the cost per byte); the finished values go back into the
     // LDS slots they came from and the plane pass re-reads them as 8 consecutive columns (one
     // 16-byte fp16 chunk per plane: consecutive rows of a k-block are contiguous).
-    static_assert(EW * 32 * 64 * 4 <= NSTAGE * STAGE_BYTES, "epilogue scratch");
-    float* ep = reinterpret_cast<float*>(smem) + ep_wave * (32 * 64);
+    static_assert(KS > 1 || NW * 32 * 64 * 4 <= NSTAGE * STAGE_BYTES, "epilogue scratch");
+    float* ep = ep_buf;
     const int cq = (lane & 7) * 8;  // plane pass: the lane's 8 columns (in the wave tile)
     const int c4 = (lane & 7) * 4;  // fp32 pass: columns c4 .. c4+3 and 32 + c4 ..
     const int eo = g.Yp ? eo_main : 0;
@@ -534,6 +537,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
       if (fp32_pass) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+          if (!my_rows(k)) continue;
           const int rr = (lane >> 3) + 8 * k;
           const int row = m0 + wm0 + i * 32 + rr;
           const int sw = (rr & 1) << 2;
@@ -594,6 +598,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
       if (g.Yp) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+          if (!my_rows(k)) continue;
           const int rr = (lane >> 3) + 8 * k;
           const int row = m0 + wm0 + i * 32 + rr;
           const int sw = (rr & 1) << 2;
@@ -655,7 +660,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     const float sc = (EPI == EPI_CROSS_QKV && t == 0) ? hl.qk_scale : 1.f;
     const int eo = to_kp ? eo_main : to_vp ? eo_v : 0;
     const float so = ldexpf(1.f, -eo);
-    float* ep = reinterpret_cast<float*>(smem) + ep_wave * (32 * 64);
+    float* ep = ep_buf;
     // fp32 rows (q, qk) go out as full 128-byte lines per 8 lanes (lane dims c4 .. c4+3 and
     // 32 + c4 ..: two rotary pairs each); plane rows as one 16-byte chunk per lane (dims d0 ..
     // d0+7).  qk (cross) needs both: the fp32 pass puts its finished values back into LDS and the
@@ -690,6 +695,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
       if (qpass) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+          if (!my_rows(k)) continue;
           const int rr = (lane >> 3) + 8 * k;
           const int lr = wm0 + i * 32 + rr;
           const int row = m0 + lr;
@@ -725,6 +731,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
       if (ppass) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+          if (!my_rows(k)) continue;
           const int rr = (lane >> 3) + 8 * k;
           const int lr = wm0 + i * 32 + rr;
           const int row = m0 + lr;

@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LIGHTGLUE_MI355X_LIB", os.path.join(_HERE, "liblightglue_mi355x.so"))
 ABI_VERSION = 4
 
-LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE = 0, -1, -2, -3, -4
+LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE, LG_E_INTERNAL = 0, -1, -2, -3, -4, -5
 
 EXPORTED_SYMBOLS = [
     "lg_abi_version",

@@ -94,7 +94,9 @@ std::vector<Tensor> make_schema(const lg_config_t& c) {
 }
 
 constexpr int D = 256;
-constexpr int kRangeSlots = 256;  // range-table slots per forward (about 5 per block are used)
+// range-table slots one forward uses at most: 3 for the inputs, 5 per block (4 with out_proj
+// folded), 1 per pruned layer, 1 for the assignment head's md image
+int range_slots(int n_layers) { return 8 + 11 * n_layers; }
 
 // Packed per-layer weights (offsets in floats into one device buffer).
 struct BlockW {
@@ -312,7 +314,8 @@ struct Work {
   int rows_pad;
   size_t R;
   int *flags, *pos, *ind, *indb, *cnt, *cntb, *act, *stop;  // pruning / early stop (SegLayout)
-  unsigned* rtab;  // PREC_H3 range table (kernels.h RangeOut), kRangeSlots slots
+  unsigned* rtab;  // PREC_H3 range table (kernels.h RangeOut), nslots slots
+  int nslots;
   int64_t *m0c, *m1c;
   float *s0c, *s1c;
   float* apart;  // attention key-split partials (small batches)
@@ -320,7 +323,7 @@ struct Work {
   size_t bytes;
 };
 
-Work carve(char* base, int B, int M, int N, bool prune, int din) {
+Work carve(char* base, int B, int M, int N, bool prune, int din, int n_layers) {
   const size_t R = (size_t)B * (M + N);
   const size_t RP = (R + 255) / 256 * 256;
   Work w{};
@@ -359,7 +362,8 @@ Work carve(char* base, int B, int M, int N, bool prune, int din) {
   w.aws = tf(lg::assign_workspace_floats(B, M, N) + 64 + lg::sim_h3_workspace_floats(B, M, N));
   w.apart_floats = lg::attention_split_floats(B, D / 64, std::max(M, N), std::max(M, N));
   w.apart = w.apart_floats ? tf(w.apart_floats) : nullptr;
-  w.rtab = reinterpret_cast<unsigned*>(ti(kRangeSlots * lg::kRangeStride));
+  w.nslots = range_slots(n_layers);
+  w.rtab = reinterpret_cast<unsigned*>(ti((size_t)w.nslots * lg::kRangeStride));
   if (prune) {
     w.X2 = tf(R * D);
     w.cos2 = tf(R * 32);
@@ -613,7 +617,7 @@ int lg_load_weights(lg_handle_t* h, int n, const char* const* names, const float
 
 int lg_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
   if (!h || !bytes || B < 0 || M < 0 || N < 0) return fail(LG_E_INVALID, "bad argument");
-  *bytes = carve(nullptr, B, M, N, prune_enabled(h->cfg), h->cfg.input_dim).bytes;
+  *bytes = carve(nullptr, B, M, N, prune_enabled(h->cfg), h->cfg.input_dim, h->cfg.n_layers).bytes;
   return LG_OK;
 }
 
@@ -641,13 +645,13 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   if ((out->layer_descriptors0 || out->layer_descriptors1) && (do_stop || do_prune))
     return fail(LG_E_INVALID, "layer_descriptors need early stop and pruning off (training-mode outputs)");
   if (do_prune && (!out->prune0 || !out->prune1)) return fail(LG_E_INVALID, "prune0/prune1 outputs required with pruning");
-  const Work need = carve(nullptr, B, M0, N0, prune_enabled(c), c.input_dim);
+  const Work need = carve(nullptr, B, M0, N0, prune_enabled(c), c.input_dim, c.n_layers);
   const bool din_a16 = ((uintptr_t)in->descriptors0 % 16 == 0) && ((uintptr_t)in->descriptors1 % 16 == 0);
   if (!workspace || workspace_bytes < need.bytes)
     return fail(LG_E_WORKSPACE, "workspace too small: need " + std::to_string(need.bytes));
   LG_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
-  Work w = carve((char*)workspace, B, M0, N0, prune_enabled(c), c.input_dim);
+  Work w = carve((char*)workspace, B, M0, N0, prune_enabled(c), c.input_dim, c.n_layers);
   const float* Wb = h->wbuf;
   int M = M0, N = N0;
   const int RP = w.rows_pad;
@@ -696,11 +700,18 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   // cannot be exceeded and nothing is read back -- the forward stays asynchronous
   unsigned* rt = prec == PREC_H3 ? w.rtab : nullptr;
   int nslot = 0;
-  auto slot = [&]() { return nslot < kRangeSlots ? nslot++ : kRangeSlots - 1; };
+  // a slot is never shared: an exhausted table is an internal error (range_slots() undercounts),
+  // reported after the pass instead of silently aliasing two tensors' exponents
+  bool slots_overflow = false;
+  auto slot = [&]() {
+    if (nslot < w.nslots) return nslot++;
+    slots_overflow = true;
+    return w.nslots - 1;
+  };
   auto ro = [&](int in0, float g0, int in1, float g1, float add, int out, int track = 0) {
     return RangeOut{rt, in0, in1, g0, g1, add, out, track};
   };
-  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.rtab, 0, kRangeSlots * lg::kRangeStride * sizeof(unsigned), st));
+  if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.rtab, 0, (size_t)w.nslots * lg::kRangeStride * sizeof(unsigned), st));
   h->pass_started = true;
   int s_x = -1;  // slot of the current residual-stream plane image Xp
   // ---- input projection (lightglue.py:370-373,486-487); H3 also builds x's plane image
@@ -945,6 +956,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     }
   }
   out->precision_used = prec;
+  if (slots_overflow) return fail(LG_E_INTERNAL, "range table exhausted (internal: range_slots undercounts)");
 
   // ---- assignment head of each pair's last executed layer (lightglue.py:549-551,
   // MatchAssignment :306-315): one final_proj / matchability launch per layer a pair may have
@@ -1013,6 +1025,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       fprintf(stderr, "range slot %d: max %.4g exp %d\n", k, m, (int)tab[(size_t)k * lg::kRangeStride + lg::kRangeShards]);
     }
   }
+  if (slots_overflow) return fail(LG_E_INTERNAL, "range table exhausted (internal: range_slots undercounts)");
   AssignArgs aa;
   memset(&aa, 0, sizeof(aa));
   aa.sim = w.sim; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = out->log_assignment; aa.ws = w.aws;

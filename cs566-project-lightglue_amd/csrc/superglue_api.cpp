@@ -43,6 +43,8 @@ int fail(int code, const std::string& msg) { return lg::api_fail(code, msg.c_str
 
 constexpr int D = 256, H = 4, HD = 64;
 constexpr int kSlots = 512;
+// per forward: at most 6 slots for the encoder / inputs, 4 per GNN layer, 1 for the head
+static_assert(kSlots >= 8 + 4 * SG_MAX_LAYERS, "range table too small for SG_MAX_LAYERS");
 
 struct Tensor {
   std::string name;

@@ -138,7 +138,11 @@ class LightGlue(nn.Module):
         self._weights_key = None
         self._weight_entries = None
         self._weight_modules = None
-        self._graphs = None  # compile(): {signature: (hipGraph, static inputs, static outputs, weights key)}
+        self._graphs = None  # compile(): {signature: (hipGraph, static inputs, static outputs, generation, workspace)}
+        # bumped whenever the native handle is (re)created or its weights are (re)uploaded: both
+        # free device memory a captured graph may point at, so graphs of older generations are
+        # recaptured instead of replayed
+        self._gen = 0
         self._ws = None
 
         state_dict = None
@@ -183,19 +187,23 @@ class LightGlue(nn.Module):
         return self
 
     def _graph_forward(self, inputs, key):
-        """Replay (capturing on first use) the HIP graph of one forward signature."""
-        wkey = self._weights_signature()
+        """Replay (capturing on first use) the HIP graph of one forward signature.  The handle is
+        validated first (config, weights): a re-upload or a new handle bumps ``self._gen`` and
+        every graph captured before it is recaptured, never replayed against freed memory."""
+        self._ensure_handle(inputs[0].device)
         ent = self._graphs.get(key)
-        if ent is None or ent[3] != wkey:
+        if ent is None or ent[3] != self._gen:
             static = [None if t is None else t.clone() for t in inputs]
             self._forward_native(*static)  # eager: weights upload, workspace sizing, lazy init
             torch.cuda.synchronize(static[0].device)
+            gen = self._gen
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 pred = self._forward_native(*static)
+            assert self._gen == gen, "lightglue_amd: the handle changed during graph capture"
             # the graph keeps the workspace it was captured with alive (a later, larger eager
             # forward replaces self._ws)
-            ent = (g, static, pred, self._weights_signature(), self._ws)
+            ent = (g, static, pred, gen, self._ws)
             self._graphs[key] = ent
         g, static, pred = ent[0], ent[1], ent[2]
         for dst, src in zip(static, inputs):
@@ -231,6 +239,7 @@ class LightGlue(nn.Module):
             _lib.check(lib.lg_create(ctypes.byref(cfg), device.index or 0, ctypes.byref(h)), "lg_create")
             self._handle, self._handle_device, self._cfg_key = h, device, cfg_key
             self._weights_key = None
+            self._gen += 1
         key = self._weights_signature()
         if key != self._weights_key:
             sd = self.state_dict(keep_vars=True)
@@ -250,13 +259,17 @@ class LightGlue(nn.Module):
             _lib.check(lib.lg_load_weights(self._handle, len(ts), arr_n, arr_p, arr_k, ctypes.c_void_p(stream)), "lg_load_weights")
             torch.cuda.current_stream(device).synchronize()  # sources may be temporaries
             self._weights_key = self._weights_signature()
+            self._gen += 1
         return lib
 
     def reload_weights(self):
         """Force the next forward to re-upload every parameter.  Needed only after writes the
         forward cannot see: in-place writes through ``p.data`` (``p.data.copy_(...)``, EMA
-        updates) bump the version counter of a temporary tensor, not of ``p``."""
+        updates) bump the version counter of a temporary tensor, not of ``p``.  Captured HIP graphs
+        (:meth:`compile`) are dropped as well."""
         self._weights_key = None
+        if self._graphs is not None:
+            self._graphs = {}
 
     def _weights_signature(self):
         """(data_ptr, _version) of every parameter / persistent buffer plus the identity of every

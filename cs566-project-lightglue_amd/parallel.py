@@ -7,10 +7,12 @@ holds the whole batch.
 
 * :func:`match_static`  — contiguous B/world slices, one ``all_gather_into_tensor`` of the packed
   results (configs[2]/[4]: uniform per-pair cost).
-* :func:`match_dynamic` — pruning makes per-pair cost data dependent (configs[3], B == 1 per
-  launch per reference semantics, lightglue.py:528,533): ranks pull pair indices from an atomic
-  counter in the process group's c10d store (``store.add``), then one ``all_reduce(MAX)`` merges
-  the outputs (each pair is written by exactly one rank; the rest of the buffer holds -2 / -inf).
+* :func:`match_dynamic` — pruning makes per-pair cost data dependent (configs[3]): ranks pull
+  CHUNKS of pair indices (guided self-scheduling) from an atomic counter in the process group's
+  c10d store (``store.add``) and match each chunk in one batched forward -- the reference asserts
+  B == 1 when pruning (lightglue.py:528,533); the HIP forward prunes and stops every pair of a batch
+  on its own -- then one ``all_reduce(MAX)`` merges the outputs (each pair is written by exactly one
+  rank; the rest of the buffer holds -2 / -inf).
 
 ``matcher`` is any callable with the ``LightGlue.forward`` contract; in production it is
 ``lightglue_amd.LightGlue`` on this rank's GPU (the gather then runs on RCCL).  The CPU tests
@@ -80,28 +82,62 @@ def match_static(matcher, data, group=None):
     return _unpack(rows, M, N)
 
 
-def match_dynamic(matcher, data, group=None, store=None, key="lightglue_amd/next_pair"):
-    """Work-queue sharding: each rank pulls single pairs until the batch is exhausted."""
-    world_rank = dist.get_rank(group)
+_dynamic_calls = 0
+
+
+def guided_chunk(remaining, world, chunk, min_chunk=1):
+    """Guided self-scheduling: a rank takes ceil(remaining / world) pairs, capped at ``chunk`` (the
+    per-forward batch that maximises pruned pairs/s) and floored at ``min_chunk``.  Early pulls are
+    full chunks (batched pruning runs at ~4.8x the pairs/s of one pair per forward,
+    profiles/r02/configs.jsonl); near the end of the queue the chunks shrink so the ranks finish
+    together when per-pair cost varies."""
+    return max(min_chunk, min(chunk, -(-remaining // max(world, 1))))
+
+
+def match_dynamic(matcher, data, group=None, store=None, key="lightglue_amd/next_pair", chunk=32, min_chunk=1):
+    """Work-queue sharding in chunks of pairs: each rank pulls a contiguous chunk of pair indices
+    from an atomic counter in the process group's c10d store (``store.add``), matches it in ONE
+    batched forward (pruning / early stop are per pair inside the batch), and repeats until the
+    batch is exhausted; one ``all_reduce(MAX)`` then merges the outputs (each pair is written by
+    exactly one rank; the rest of the buffer holds -2 / -inf).  Chunk sizes follow
+    :func:`guided_chunk`.  Without an initialised process group the same loop runs on a local
+    counter (world size 1).  Returns (results, [(start, stop) chunks this rank matched])."""
+    global _dynamic_calls
     B, M = data["keypoints0"].shape[:2]
     N = data["keypoints1"].shape[1]
     device = data["keypoints0"].device
-    if store is None:
+    distributed = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if distributed else 1
+    # a fresh counter per call: every rank makes the same sequence of calls, so the key needs no
+    # reset and no barrier (TCPStore.add creates a missing key at 0)
+    _dynamic_calls += 1
+    ckey = f"{key}/{_dynamic_calls}"
+    if distributed and store is None:
         store = dist.distributed_c10d._get_default_store()
-    dist.barrier(group)
-    if world_rank == 0:
-        store.set(key, "0")
-    dist.barrier(group)
+    local = [0]
+
+    def pull(n):  # atomic fetch-and-add; returns the counter value before the add
+        if not distributed:
+            local[0] += n
+            return local[0] - n
+        return store.add(ckey, n) - n
+
     buf = torch.full((B, 2 * M + 2 * N), -2.0, dtype=torch.float64, device=device)
     buf[:, M + N :] = float("-inf")
     done = []
     while True:
-        i = store.add(key, 1) - 1
-        if i >= B:
+        seen = pull(0)
+        if seen >= B:
             break
+        c = guided_chunk(B - seen, world, chunk, min_chunk)
+        a = pull(c)
+        if a >= B:
+            break
+        b = min(B, a + c)
         with torch.no_grad():
-            pred = matcher(_slice(data, i, i + 1))
-        buf[i : i + 1] = _pack(pred, M, N, 1, device)
-        done.append(i)
-    dist.all_reduce(buf, op=dist.ReduceOp.MAX, group=group)
+            pred = matcher(_slice(data, a, b))
+        buf[a:b] = _pack(pred, M, N, b - a, device)
+        done.append((a, b))
+    if distributed:
+        dist.all_reduce(buf, op=dist.ReduceOp.MAX, group=group)
     return _unpack(buf, M, N), done

@@ -40,7 +40,8 @@ enum {
   LG_E_INVALID = -1,  /* bad argument / shape (reference: assert, lightglue.py:446,481-482,528) */
   LG_E_HIP = -2,      /* HIP runtime error */
   LG_E_WEIGHTS = -3,  /* missing / mis-shaped weight tensor */
-  LG_E_WORKSPACE = -4 /* workspace too small */
+  LG_E_WORKSPACE = -4, /* workspace too small */
+  LG_E_INTERNAL = -5   /* internal consistency check failed (a library bug, not a caller error) */
 };
 
 typedef struct lg_handle lg_handle_t;

@@ -640,3 +640,80 @@ def test_compile_replays_hip_graphs():
         for k in ("matches0", "matches1", "matching_scores0", "matching_scores1", "log_assignment"):
             assert torch.equal(got[k], ref[k]), (k, M, N, seed)
     assert len(graphed._graphs) == 2
+
+
+def test_compile_graphs_follow_conf_and_weight_changes():
+    """a replayed graph must never run against stale weights, a stale config or device
+    memory a later upload freed.  Capture two signatures, then (1) change the config, (2) write a
+    parameter through p.data + reload_weights(), (3) change a weight in place and run the OTHER
+    signature first (its eager forward re-uploads the weights): every replay equals a fresh eager
+    model with the same config and weights."""
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1}
+    sd = synthetic_state_dict(conf, seed=0)
+    graphed = _model(conf, sd, "auto").compile()
+    da = _gpu_data(synthetic_pair(B=2, M=256, N=230, seed=1))
+    db = _gpu_data(synthetic_pair(B=1, M=192, N=200, seed=2))
+
+    def expect(model_conf, state, data, got):
+        ref = _model(model_conf, {k: v.detach().cpu().numpy() for k, v in state.items()}, "auto")
+        with torch.no_grad():
+            r = ref(data)
+        torch.cuda.synchronize()
+        for k in ("matches0", "matches1", "matching_scores0", "matching_scores1", "log_assignment"):
+            assert torch.equal(got[k], r[k]), k
+
+    with torch.no_grad():
+        graphed(da)
+        graphed(db)
+        # (1) config change: the handle is recreated, both graphs are stale
+        graphed.conf.filter_threshold = 0.3
+        got = {k: v.clone() for k, v in graphed(da).items() if torch.is_tensor(v)}
+        expect({"filter_threshold": 0.3}, graphed.state_dict(), da, got)
+        # (2) a write the version counter cannot see, then reload_weights()
+        graphed.log_assignment[-1].final_proj.weight.data.mul_(0.5)
+        graphed.reload_weights()
+        got = {k: v.clone() for k, v in graphed(da).items() if torch.is_tensor(v)}
+        expect({"filter_threshold": 0.3}, graphed.state_dict(), da, got)
+        # (3) an in-place change, picked up by the other signature first
+        graphed.log_assignment[-1].matchability.bias.add_(0.5)
+        graphed(db)
+        got = {k: v.clone() for k, v in graphed(da).items() if torch.is_tensor(v)}
+        expect({"filter_threshold": 0.3}, graphed.state_dict(), da, got)
+
+
+@pytest.mark.parametrize("prune", [False, True])
+def test_deep_config_matches_oracle(prune):
+    """a 32-layer model needs more range-table slots than the round-2 fixed table had
+    (9 L + 2 with pruning); the table is sized from n_layers, so a deep forward matches the oracle
+    (indices exact outside fp64 near-ties, scores within 1e-4)."""
+    import oracle
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1, "n_layers": 32}
+    if prune:
+        conf.update(width_confidence=0.99, depth_confidence=-1)
+    sd = synthetic_state_dict(conf, seed=0)
+    data = synthetic_pair(B=1, M=96, N=80, seed=5)
+    ref = oracle.lightglue_forward(sd, data, conf)
+    ref64 = oracle.lightglue_forward(sd, data, conf, dtype=torch.float64)
+    model = _model(conf, sd)
+    with torch.no_grad():
+        pred = model(_gpu_data(data))
+    m0, m1 = pred["matches0"].cpu().numpy(), pred["matches1"].cpu().numpy()
+    r0, r1 = ref["matches0"].numpy(), ref["matches1"].numpy()
+    ok0, ok1 = np.ones_like(m0, dtype=bool), np.ones_like(m1, dtype=bool)
+    la = ref64["log_assignment"][:, :-1, :-1]
+    if la.shape[1:] == (m0.shape[1], m1.shape[1]):  # every point kept: fp64 margins per row / column
+        t0, t1 = la.topk(2, dim=2).values, la.topk(2, dim=1).values
+        ok0 = (t0[..., 0] - t0[..., 1] >= NEAR_TIE).numpy()
+        ok1 = (t1[:, 0] - t1[:, 1] >= NEAR_TIE).numpy()
+    np.testing.assert_array_equal(m0[ok0], r0[ok0])
+    np.testing.assert_array_equal(m1[ok1], r1[ok1])
+    if prune:
+        np.testing.assert_array_equal(pred["prune0"].cpu().numpy(), ref["prune0"].numpy())
+        np.testing.assert_array_equal(pred["prune1"].cpu().numpy(), ref["prune1"].numpy())
+    same = ok0 & ((m0 > -1) == (r0 > -1))
+    np.testing.assert_allclose(pred["matching_scores0"].cpu().numpy()[same], ref["matching_scores0"].numpy()[same],
+                               atol=SCORE_TOL)

@@ -19,17 +19,26 @@ def _free_port():
     return p
 
 
-def _setup():
+def _setup(prune=False):
     import lgamd  # noqa: F401
     import oracle
     from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
 
     conf = {"filter_threshold": 0.1, "n_layers": 2}
+    if prune:  # per-pair cost varies: width pruning + early stop (configs[3]'s regime)
+        conf.update(width_confidence=0.9, depth_confidence=0.9)
     sd = synthetic_state_dict(conf, seed=0)
-    data = {k: torch.from_numpy(v) for k, v in synthetic_pair(B=5, M=40, N=36, seed=2).items()}
+    if prune:
+        sd["log_assignment.0.matchability.bias"][:] = -2.0  # prunes part of the points at layer 0
+    B = 7 if prune else 5
+    data = {k: torch.from_numpy(v) for k, v in synthetic_pair(B=B, M=40, N=36, seed=2).items()}
 
     def matcher(d):
-        return oracle.lightglue_forward(sd, {k: v.numpy() for k, v in d.items()}, conf)
+        # the oracle follows the reference's B == 1 pruning (lightglue.py:528,533): one pair at a
+        # time, stacked (the HIP forward batches the chunk instead)
+        outs = [oracle.lightglue_forward(sd, {k: v[i : i + 1].numpy() for k, v in d.items()}, conf)
+                for i in range(d["keypoints0"].shape[0])]
+        return {k: torch.cat([o[k] for o in outs]) for k in ("matches0", "matches1", "matching_scores0", "matching_scores1")}
 
     return matcher, data
 
@@ -45,33 +54,69 @@ def _worker(rank, world, port, mode, out_dir):
         from lightglue_amd import parallel
 
         torch.set_num_threads(1)
-        matcher, data = _setup()
+        matcher, data = _setup(prune=mode.endswith("prune"))
         if mode == "static":
             res = parallel.match_static(matcher, data)
         else:
-            res, done = parallel.match_dynamic(matcher, data)
-            torch.save(torch.tensor(done, dtype=torch.int64), os.path.join(out_dir, f"done{rank}.pt"))
+            chunk = 1 if mode == "dynamic" else 3
+            # two calls in a row: every call gets its own queue counter (no reset between calls)
+            for _ in range(2):
+                res, done = parallel.match_dynamic(matcher, data, chunk=chunk)
+            torch.save(torch.tensor(done, dtype=torch.int64).reshape(-1, 2), os.path.join(out_dir, f"done{rank}.pt"))
         torch.save(res, os.path.join(out_dir, f"res{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["static", "dynamic"])
+@pytest.mark.parametrize("mode", ["static", "dynamic", "dynamic_chunked", "dynamic_chunked_prune"])
 def test_sharded_matches_equal_unsharded(tmp_path, mode):
     import sys
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), mode, str(tmp_path)), nprocs=world, join=True)
-    matcher, data = _setup()
+    matcher, data = _setup(prune=mode.endswith("prune"))
     ref = matcher(data)
     for r in range(world):
         res = torch.load(tmp_path / f"res{r}.pt", weights_only=True)
         for k in ("matches0", "matches1", "matching_scores0", "matching_scores1"):
             np.testing.assert_array_equal(res[k].numpy(), ref[k].numpy(), err_msg=f"rank {r} {k}")
-    if mode == "dynamic":
-        done = sorted(sum((torch.load(tmp_path / f"done{r}.pt", weights_only=True).tolist() for r in range(world)), []))
-        assert done == list(range(5))  # every pair exactly once
+    if mode.startswith("dynamic"):
+        chunks = sum((torch.load(tmp_path / f"done{r}.pt", weights_only=True).tolist() for r in range(world)), [])
+        pairs = sorted(i for a, b in chunks for i in range(a, b))
+        assert pairs == list(range(data["keypoints0"].shape[0]))  # every pair exactly once
+        if mode != "dynamic":
+            assert max(b - a for a, b in chunks) > 1  # pairs really travel in chunks
+
+
+def test_guided_chunks_shrink_towards_the_tail():
+    import lgamd  # noqa: F401
+    from lightglue_amd.parallel import guided_chunk
+
+    assert guided_chunk(512, 8, 32) == 32
+    assert guided_chunk(100, 8, 32) == 13
+    assert guided_chunk(3, 8, 32) == 1
+    assert guided_chunk(3, 8, 32, min_chunk=2) == 2
+    # single process: the whole queue in chunks of at most `chunk`
+    seen, rem, sizes = 0, 70, []
+    while seen < rem:
+        c = guided_chunk(rem - seen, 1, 32)
+        sizes.append(min(c, rem - seen))
+        seen += c
+    assert sizes == [32, 32, 6]
+
+
+def test_match_dynamic_without_process_group():
+    """World size 1 (no process group): the same chunk loop on a local counter."""
+    import lgamd  # noqa: F401
+    from lightglue_amd import parallel
+
+    matcher, data = _setup()
+    res, done = parallel.match_dynamic(matcher, data, chunk=2)
+    assert done == [(0, 2), (2, 4), (4, 5)]
+    ref = matcher(data)
+    for k in ("matches0", "matches1", "matching_scores0", "matching_scores1"):
+        np.testing.assert_array_equal(res[k].numpy(), ref[k].numpy())
 
 
 def test_shard_range_covers_batch():

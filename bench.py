@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput of the MI355X LightGlue matcher: image-pairs/s at N=2048 keypoints, d=256.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--npts N]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--npts N] [--workload W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py spawns the N ranks itself
@@ -14,6 +14,16 @@ image, 9 layers, no pruning, B=32 pairs per GPU per step (weak scaling: every ra
 Weights: deterministic random init of the full architecture (no network for checkpoints).
 One step = one full LightGlue.forward (positional encoding, 9 x self+cross layers, dual-softmax
 assignment with the [B,N+1,N+1] log_assignment written, mutual filter).
+
+Other BASELINE.json configs through the same multi-rank launch (--workload; the default line above
+is unchanged):
+  configs3  N=2048, width + depth pruning 0.95 (weights that prune ~10 % per layer and stop after
+            layer 6; MegaDepth-like 1600x1200 keypoints), 64 pairs per GPU per step pulled from a
+            shared queue in guided chunks of <= 32 pairs, each chunk one batched-pruning forward
+            (parallel.match_dynamic; per-pair cost varies)
+  configs4  N=4096, 8 pairs per GPU per step (64 over 8 GPUs), static shards (parallel.match_static):
+            LightGlue forward -> its final similarity -> log-domain Sinkhorn (superglue.py:173-201,
+            50 iterations, dustbin score 1.0) -> mutual filter (superglue.py:288-298, threshold 0.2)
 
 Prints ONE JSON line on rank 0 with the metric, the attention kernel's roofline (in-library HIP
 events around every attention launch in the timed region; algorithmic flops per launch) and the
@@ -158,18 +168,35 @@ def cpu_pairs(B, N, dim, seed):
             "view0": {"image_size": isz}, "view1": {"image_size": isz}}
 
 
+# workload -> (pairs per GPU per step, keypoints, description)
+WORKLOADS = {
+    "configs2": (32, 2048, "configs[2]: SuperPoint+LightGlue N=2048, 9 layers, no pruning, batch=32 per GPU"),
+    "configs3": (64, 2048, "configs[3]: MegaDepth-like N=2048 (1600x1200), adaptive depth/width pruning 0.95, "
+                           "64 pairs per GPU from a shared queue in guided chunks of <= 32"),
+    "configs4": (8, 4096, "configs[4]: N=4096 d=256, Sinkhorn assignment (50 iterations), 8 pairs per GPU "
+                          "(batch 64 over 8 GPUs)"),
+}
+SINKHORN_ITERS, SINKHORN_ALPHA, SINKHORN_THRESHOLD = 50, 1.0, 0.2  # superglue.py:214-215, bin_score init 1.0
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32, help="pairs per GPU per step")
-    ap.add_argument("--npts", type=int, default=2048)
+    ap.add_argument("--workload", default="configs2", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step (default: the workload's)")
+    ap.add_argument("--npts", type=int, default=None, help="keypoints per image (default: the workload's)")
+    ap.add_argument("--chunk", type=int, default=32, help="configs3: largest chunk of pairs per forward")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of timed CPU-baseline work (0 = skip)")
     ap.add_argument("--precision", default="auto", choices=["auto", "bf16x6"])
     ap.add_argument("--selftest-cpu", action="store_true",
                     help="CPU/gloo rehearsal of the launch and gather logic with a stand-in matcher")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    b, n, _ = WORKLOADS[a.workload]
+    a.batch = b if a.batch is None else a.batch
+    a.npts = n if a.npts is None else a.npts
+    return a
 
 
 def _free_port():
@@ -213,30 +240,59 @@ def run(args):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     B, N = args.batch, args.npts
+    wl = args.workload
     conf = {"filter_threshold": 0.1}
+    if wl == "configs3":
+        conf.update(width_confidence=0.95, depth_confidence=0.95)
+    if wl == "configs4":
+        conf["return_similarity"] = True
+    size = (1600.0, 1200.0) if wl == "configs3" else (640.0, 640.0)
     if selftest:
         device = torch.device("cpu")
         model = _CpuStandIn()
         data = cpu_pairs(B * world, N, 256, seed=1)
     else:
         from lightglue_amd import LightGlue
+        from lightglue_amd.weights import prune_recipe_state_dict
 
         device = torch.device("cuda", local)
         model = LightGlue({**conf, "precision": args.precision}).eval().to(device)
-        sd = synthetic_state_dict(conf, seed=0)
+        sd = prune_recipe_state_dict(conf) if wl == "configs3" else synthetic_state_dict(conf, seed=0)
         model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
         # every rank holds the same global batch (B pairs per GPU) and matches its shard
-        data = gpu_pairs(B * world, N, 256, seed=1, device=device)
+        data = gpu_pairs(B * world, N, 256, seed=3 if wl == "configs3" else 1, device=device, size=size)
+
+    sk_events = []
+
+    def sinkhorn_matcher(d):
+        """configs[4]: the matcher's final similarity through the Sinkhorn head (superglue.py:173-201,
+        288-298) instead of the dual softmax."""
+        from lightglue_amd import filter_matches, log_optimal_transport
+
+        pred = model(d)
+        if selftest:
+            return pred
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        Z = log_optimal_transport(pred["similarity"], SINKHORN_ALPHA, SINKHORN_ITERS)
+        e1.record()
+        sk_events.append((e0, e1, d["keypoints0"].shape[0]))
+        m0, m1, s0, s1 = filter_matches(Z, SINKHORN_THRESHOLD)
+        return {"matches0": m0, "matches1": m1, "matching_scores0": s0, "matching_scores1": s1}
+
+    matcher = sinkhorn_matcher if wl == "configs4" else model
 
     def sync():
         if not selftest:
             torch.cuda.synchronize()
 
     def step():
+        if wl == "configs3":  # shared queue of guided chunks, one batched-pruning forward per chunk
+            return parallel.match_dynamic(matcher, data, chunk=args.chunk)[0]
         if distributed:  # this rank's B pairs, then the RCCL all-gather of the match results (SURVEY §8e)
-            return parallel.match_static(model, data)
+            return parallel.match_static(matcher, data)
         with torch.no_grad():
-            return model(data)
+            return matcher(data)
 
     for _ in range(args.warmup):
         step()
@@ -249,6 +305,7 @@ def run(args):
     sync()
     if distributed:
         dist.barrier()
+    sk_events.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pred = step()
@@ -256,6 +313,7 @@ def run(args):
     if distributed:
         dist.barrier()
     el = time.perf_counter() - t0
+    sk_timed = list(sk_events)
     result_kernels, roofline = None, None
     if not selftest:
         att_ms, att_n, att_fl, att_by = model.profile_read("attention")
@@ -287,6 +345,9 @@ def run(args):
             "avg_launch_ms": round(att_ms / max(att_n, 1), 4),
             "algorithmic_flops_per_launch": att_fl / max(att_n, 1),
         }
+        if wl == "configs3":
+            roofline["flops_note"] = ("pruned forwards: each launch's flops over the kept points of the running pairs "
+                                      "(per-pair counts copied at launch time, lg_profile_read)")
         result_kernels = {
             "attention_ms_per_step": round(att_ms / args.steps, 3),
             "breakdown_note": f"gemm/assign from {bsteps} untimed steps with every kernel family evented",
@@ -300,6 +361,16 @@ def run(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
+    if sk_timed:  # configs4: the Sinkhorn kernel against the HBM roofline (one read of the scores per iteration)
+        sk_ms = sum(a.elapsed_time(b) for a, b, _ in sk_timed)
+        sk_pairs = sum(n for _, _, n in sk_timed)
+        by = sk_pairs * (SINKHORN_ITERS * N * N * 4.0 + (N + 1) * (N + 1) * 4.0 + N * N * 4.0)
+        result_kernels["sinkhorn_ms_per_step"] = round(sk_ms / args.steps, 3)
+        result_kernels["sinkhorn_roofline"] = {
+            "bound": "hbm", "achieved": round(by / (sk_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(by / (sk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_pair": by / sk_pairs,
+            "note": "scores read once per iteration + final read and Z write; > 1 means on-die cache reuse"}
     pairs = B * args.steps * world  # every rank matched B pairs per step
     value = pairs / el
     result = {
@@ -317,10 +388,12 @@ def run(args):
         "data": "synthetic (SuperPoint-shaped keypoints/descriptors, random-init weights)"
                 + (" [CPU self-test: stand-in matcher, no compute]" if selftest else ""),
         "config": {
-            "workload": "configs[2]: SuperPoint+LightGlue N=2048, 9 layers, no pruning, batch=32 per GPU",
+            "workload": WORKLOADS[wl][2] if (B, N) == WORKLOADS[wl][:2] else f"{wl} shape, N={N}, batch={B} per GPU",
             "npts": N, "descriptor_dim": 256, "n_layers": 9, "pairs_per_gpu_per_step": B,
             "global_batch": B * world,
-            "parallelism": f"pair-sharded x{world}" + (" (parallel.match_static: RCCL all-gather of matches)" if distributed else ""),
+            "parallelism": f"pair-sharded x{world}" + (
+                f" (parallel.match_dynamic: guided chunks <= {args.chunk} from a c10d-store queue, one all_reduce merge)"
+                if wl == "configs3" else (" (parallel.match_static: RCCL all-gather of matches)" if distributed else "")),
             "matrix_operands": model.last_precision_used,
         },
         "achieved_tflops_total": round(total_flops_per_pair(N) * pairs / el / 1e12, 2),
@@ -329,7 +402,9 @@ def run(args):
         "pairs_timed": pairs,
         "matches_per_pair": float((pred["matches0"] > -1).float().sum(1).mean()),
     }
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
+    if wl == "configs3" and not selftest:
+        result["config"]["pruning"] = "width 0.95, depth 0.95 (weights: weights.prune_recipe_state_dict)"
+    if rank == 0 and world == 1 and args.cpu_budget > 0 and wl == "configs2":
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LIGHTGLUE_MI355X_LIB", os.path.join(_HERE, "liblightglue_mi355x.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE, LG_E_INTERNAL = 0, -1, -2, -3, -4, -5
 
@@ -32,6 +32,8 @@ EXPORTED_SYMBOLS = [
     "lg_profile_read",
     "lg_attention_workspace_bytes",
     "lg_attention",
+    "lg_assignment_workspace_bytes",
+    "lg_assignment_head",
     # SuperPoint extractor (include/superpoint_mi355x.h)
     "sp_create",
     "sp_destroy",
@@ -115,6 +117,7 @@ class LGOutputs(ctypes.Structure):
         ("kept0", ctypes.c_int32),
         ("kept1", ctypes.c_int32),
         ("precision_used", ctypes.c_int32),
+        ("similarity", _P),
     ]
 
 
@@ -251,6 +254,8 @@ def load():
             ctypes.c_int,
             [_P, _P, _P, i32, i32, i32, i32, ctypes.c_float, i32, _P, _P, sz, _P],
         ),
+        "lg_assignment_workspace_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_assignment_head": (ctypes.c_int, [_P, i32, _P, _P, i32, i32, i32, _P, _P, _P, _P, _P, sz, _P]),
         "sp_create": (ctypes.c_int, [ctypes.POINTER(SPConfig), ctypes.c_int, ctypes.POINTER(_P)]),
         "sp_destroy": (ctypes.c_int, [_P]),
         "sp_weight_count": (ctypes.c_int, [_P]),

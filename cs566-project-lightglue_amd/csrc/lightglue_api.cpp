@@ -163,11 +163,19 @@ struct lg_handle {
     hipEvent_t a, b;
     int kind;
     double flops, bytes;
+    // pruned forwards: the per-pair counts at launch time (a stream-ordered copy into snap), from
+    // which lg_profile_read recomputes the launch's algorithmic flops over the LIVE rows only
+    int snap = -1;  // offset (ints) into snap: cnt[2B], then sel[B] when has_sel
+    int B = 0, sel_eq = 0, mode = 0;  // mode 1: self attention, 2: cross attention, 3: GEMM
+    bool has_sel = false;
+    double unit = 0.0;  // self/cross: 64 * heads; GEMM: 2 * K * Nout
   };
   bool prof_on = false;
   unsigned prof_mask = 0;  // bit k: kernel family k is timed
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
+  int* snap = nullptr;
+  size_t snap_cap = 0, snap_used = 0;
   hipEvent_t ev() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -190,6 +198,22 @@ struct lg_handle {
     recs[idx].flops = flops;
     recs[idx].bytes = bytes;
     (void)hipEventRecord(recs[idx].b, st);
+  }
+  // attach the live-row counts of a pruned forward to record idx (no-op outside profiling)
+  void prof_counts(int idx, int mode, double unit, const int* cnt, const int* sel, int sel_eq, int B, hipStream_t st) {
+    if (idx < 0 || !cnt || !snap) return;
+    const size_t need = 3 * (size_t)B;
+    if (snap_used + need > snap_cap) return;  // out of snapshot space: the capacity flops stay
+    Rec& r = recs[idx];
+    r.snap = (int)snap_used;
+    r.B = B;
+    r.mode = mode;
+    r.unit = unit;
+    r.sel_eq = sel_eq;
+    r.has_sel = sel != nullptr;
+    (void)hipMemcpyAsync(snap + snap_used, cnt, 2 * B * sizeof(int), hipMemcpyDeviceToDevice, st);
+    if (sel) (void)hipMemcpyAsync(snap + snap_used + 2 * B, sel, B * sizeof(int), hipMemcpyDeviceToDevice, st);
+    snap_used += need;
   }
 };
 
@@ -458,6 +482,7 @@ int lg_destroy(lg_handle_t* h) {
   if (h->wbuf) (void)hipFree(h->wbuf);
   if (h->perm) (void)hipFree(h->perm);
   if (h->wplanes) (void)hipFree(h->wplanes);
+  if (h->snap) (void)hipFree(h->snap);
   for (auto& r : h->recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -668,6 +693,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     const hipError_t e = gemm_h3(g, epi, st);
     const double R = g.R, K = g.K, O = g.Nout;
     h->prof_end(p, 2.0 * R * K * O, 4.0 * (R * K + O * K + R * O), st);
+    if (g.rm.cnt) h->prof_counts(p, 3, 2.0 * K * O, g.rm.cnt, g.rm.sel, g.rm.sel_eq, B, st);
     return e;
   };
   // fp16x3 plane image of a packed weight matrix (by its fp32 offset) / of a workspace tensor
@@ -685,6 +711,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     const double fl = cross ? 6.0 * a0.Nq * a0.Nk * hd : 4.0 * hd * ((double)a0.Nq * a0.Nk + (double)a1.Nq * a1.Nk);
     const double by = 4.0 * 256.0 * B * 4.0 * (a0.Nq + a1.Nq);  // q, k, v read + o written, per row
     h->prof_end(p, fl, by, st);
+    if (a0.nq_cnt) h->prof_counts(p, cross ? 2 : 1, 64.0 * H, a0.nq_cnt, a0.act, 1, B, st);
     return e;
   };
   auto assign = [&](const AssignArgs& a) -> hipError_t {
@@ -963,7 +990,10 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   // stopped at (rows of the other pairs are masked out)
   // fused assignment (assign_h3.hip): the similarity is recomputed from md's plane image, held
   // to |md| <= 16 (the "y" side of the fp16x3 product), instead of a bf16x6 GEMM into w.sim
-  const bool fused_sim = prec == PREC_H3 && !seg && sim_h3_supported(M, N);
+  // a caller that wants the similarity (lg_outputs_t.similarity) gets it from the materialised
+  // bf16x6 GEMM, written straight into its buffer
+  const bool fused_sim = prec == PREC_H3 && !seg && sim_h3_supported(M, N) && !out->similarity;
+  float* simbuf = out->similarity ? out->similarity : w.sim;
   const int md_rows_pad = RP + 256;
   const int s_md = fused_sim ? slot() : -1;
   auto head = [&](int li, const RowMask& m) -> int {
@@ -1008,7 +1038,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     GemmArgs g = gemm_base();
     g.A0 = w.md; g.lda0 = D; g.K0 = D; g.K = D; g.sA = (long long)M * D;
     g.W = w.md + (size_t)B * M * D; g.ldw = D; g.sW = (long long)N * D;
-    g.R = M; g.Nout = N; g.Y = w.sim; g.ldy = N; g.sY = (long long)M * N;
+    g.R = M; g.Nout = N; g.Y = simbuf; g.ldy = N; g.sY = (long long)M * N;
     LG_HIP(gemm(g, EPI_STORE, B));
   }
   if (rt && getenv("LG_DEBUG_RANGE")) {  // diagnostic: the range table of this forward
@@ -1028,7 +1058,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   if (slots_overflow) return fail(LG_E_INTERNAL, "range table exhausted (internal: range_slots undercounts)");
   AssignArgs aa;
   memset(&aa, 0, sizeof(aa));
-  aa.sim = w.sim; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = out->log_assignment; aa.ws = w.aws;
+  aa.sim = simbuf; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = out->log_assignment; aa.ws = w.aws;
   aa.B = B; aa.M = M; aa.N = N; aa.th = (float)c.filter_threshold;
   if (seg) {  // per-pair kept counts; la holds pair b's [M_b+1][N_b+1] block at the capacity strides
     aa.Mb = cnt;
@@ -1085,6 +1115,96 @@ int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* w
                       h->cfg.precision == LG_PREC_X6 ? lg::PREC_X6 : lg::PREC_H3);
 }
 
+// ---- MatchAssignment of one layer on caller descriptors (lightglue.py:306-315 + :284-296); the
+// training loss evaluates it on every layer's descriptors (:614-620).  Not a hot path: bf16x6
+// GEMMs straight from the fp32 rows (no plane images, no range table), the materialised similarity
+// and the unfused assignment kernels of the pruning path.
+namespace {
+struct HeadWork {
+  float *md, *z, *sim, *aws, *s0, *s1;
+  int64_t *m0, *m1;
+  size_t bytes;
+};
+HeadWork carve_head(char* base, int B, int M, int N) {
+  HeadWork w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += (bytes + 255) & ~size_t(255);
+    return p;
+  };
+  const size_t R = (size_t)B * (M + N);
+  w.md = reinterpret_cast<float*>(take(R * D * 4));
+  w.z = reinterpret_cast<float*>(take(R * 4));
+  w.sim = reinterpret_cast<float*>(take((size_t)B * M * N * 4));
+  w.aws = reinterpret_cast<float*>(take((lg::assign_workspace_floats(B, M, N) + 64) * 4));
+  w.s0 = reinterpret_cast<float*>(take((size_t)B * M * 4));
+  w.s1 = reinterpret_cast<float*>(take((size_t)B * N * 4));
+  w.m0 = reinterpret_cast<int64_t*>(take((size_t)B * M * 8));
+  w.m1 = reinterpret_cast<int64_t*>(take((size_t)B * N * 8));
+  w.bytes = off;
+  return w;
+}
+}  // namespace
+
+int lg_assignment_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (!h || !bytes || B < 0 || M < 0 || N < 0) return fail(LG_E_INVALID, "bad argument");
+  *bytes = carve_head(nullptr, B, M, N).bytes;
+  return LG_OK;
+}
+
+int lg_assignment_head(lg_handle_t* h, int32_t layer, const float* desc0, const float* desc1, int32_t B, int32_t M,
+                       int32_t N, float* log_assignment, float* similarity, float* token_logits0, float* token_logits1,
+                       void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace lg;
+  if (!h || !desc0 || !desc1 || !log_assignment) return fail(LG_E_INVALID, "null argument");
+  if (!h->loaded) return fail(LG_E_WEIGHTS, "weights not loaded");
+  const int L = h->cfg.n_layers;
+  if (layer < 0) layer += L;  // python-style index: -1 = the last layer's head
+  if (layer < 0 || layer >= L) return fail(LG_E_INVALID, "layer index out of range");
+  if ((token_logits0 || token_logits1) && layer >= L - 1)
+    return fail(LG_E_INVALID, "token_confidence exists for layers 0..n_layers-2 only (lightglue.py:395-397)");
+  if (B <= 0) return fail(LG_E_INVALID, "batch must be >= 1");
+  if (M <= 0 || N <= 0) return fail(LG_E_INVALID, "max(): Expected reduction dim to have non-zero size (empty keypoint set)");
+  const HeadWork need = carve_head(nullptr, B, M, N);
+  if (!workspace || workspace_bytes < need.bytes) return fail(LG_E_WORKSPACE, "workspace too small: need " + std::to_string(need.bytes));
+  LG_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  HeadWork w = carve_head((char*)workspace, B, M, N);
+  const float* Wb = h->wbuf;
+  const LayerW& lw = h->layers[layer];
+  float* sim = similarity ? similarity : w.sim;
+  // md = final_proj(desc) / d**0.25 (:308-310), per image
+  for (int s2 = 0; s2 < 2; ++s2) {
+    GemmArgs g = gemm_base();
+    g.A0 = s2 == 0 ? desc0 : desc1; g.lda0 = D; g.K0 = D; g.K = D; g.W = Wb + lw.Wf; g.ldw = D; g.bias = Wb + lw.bf;
+    g.R = B * (s2 == 0 ? M : N); g.Nout = D; g.Y = w.md + (s2 == 0 ? 0 : (size_t)B * M * D); g.ldy = D;
+    g.out_scale = 0.25f;
+    LG_HIP(gemm_x6(g, EPI_STORE, 1, st));
+  }
+  // matchability logits z (:314) and, for the loss, the token-confidence logits (:109-110)
+  LG_HIP(gemv_256(desc0, Wb + lw.wm, Wb + lw.bm, w.z, B * M, 0, st));
+  LG_HIP(gemv_256(desc1, Wb + lw.wm, Wb + lw.bm, w.z + (size_t)B * M, B * N, 0, st));
+  if (token_logits0) LG_HIP(gemv_256(desc0, Wb + lw.wt, Wb + lw.bt, token_logits0, B * M, 0, st));
+  if (token_logits1) LG_HIP(gemv_256(desc1, Wb + lw.wt, Wb + lw.bt, token_logits1, B * N, 0, st));
+  // sim = md0 md1^T (:311), per pair
+  {
+    GemmArgs g = gemm_base();
+    g.A0 = w.md; g.lda0 = D; g.K0 = D; g.K = D; g.sA = (long long)M * D;
+    g.W = w.md + (size_t)B * M * D; g.ldw = D; g.sW = (long long)N * D;
+    g.R = M; g.Nout = N; g.Y = sim; g.ldy = N; g.sY = (long long)M * N;
+    LG_HIP(gemm_x6(g, EPI_STORE, B, st));
+  }
+  // sigmoid_log_double_softmax (:284-296); the filter outputs go to scratch
+  AssignArgs aa;
+  memset(&aa, 0, sizeof(aa));
+  aa.sim = sim; aa.z0 = w.z; aa.z1 = w.z + (size_t)B * M; aa.la = log_assignment; aa.ws = w.aws;
+  aa.B = B; aa.M = M; aa.N = N; aa.th = (float)h->cfg.filter_threshold;
+  aa.m0 = w.m0; aa.m1 = w.m1; aa.s0 = w.s0; aa.s1 = w.s1;
+  LG_HIP(assign_and_filter(aa, st));
+  return LG_OK;
+}
+
 int lg_profile_enable(lg_handle_t* h, int enable) {
   if (!h) return fail(LG_E_INVALID, "null handle");
   for (auto& r : h->recs) {
@@ -1092,7 +1212,13 @@ int lg_profile_enable(lg_handle_t* h, int enable) {
     h->pool.push_back(r.b);
   }
   h->recs.clear();
+  h->snap_used = 0;
   h->prof_on = enable != 0;
+  if (h->prof_on && !h->snap) {  // live-count snapshots of pruned forwards (lg_profile_read)
+    LG_HIP(hipSetDevice(h->device));
+    LG_HIP(hipMalloc((void**)&h->snap, (1u << 20) * sizeof(int)));
+    h->snap_cap = 1u << 20;
+  }
   // 1 = every family; otherwise bit (k + 1) selects family k (LG_PROFILE_ONLY(k))
   h->prof_mask = enable == 1 ? ~0u : ((unsigned)enable >> 1);
   return LG_OK;
@@ -1102,13 +1228,31 @@ int lg_profile_read(lg_handle_t* h, int kernel, double* total_ms, int64_t* launc
   if (!h || kernel < 0 || kernel >= LG_KERNEL_COUNT) return fail(LG_E_INVALID, "bad argument");
   double ms = 0.0, fl = 0.0, by = 0.0;
   int64_t n = 0;
+  std::vector<int> snap;
   for (auto& r : h->recs) {
     if (r.kind != kernel) continue;
     LG_HIP(hipEventSynchronize(r.b));
     float t = 0.f;
     LG_HIP(hipEventElapsedTime(&t, r.a, r.b));
     ms += t;
-    fl += r.flops;
+    double f = r.flops;
+    if (r.snap >= 0) {  // pruned forward: flops over the live rows / kept points at launch time
+      if (snap.empty()) {
+        snap.resize(h->snap_used);
+        LG_HIP(hipMemcpy(snap.data(), h->snap, h->snap_used * sizeof(int), hipMemcpyDeviceToHost));
+      }
+      const int* c = snap.data() + r.snap;
+      const int* sel = r.has_sel ? c + 2 * r.B : nullptr;
+      f = 0.0;
+      for (int b = 0; b < r.B; ++b) {
+        if (sel && sel[b] != r.sel_eq) continue;
+        const double c0 = c[b], c1 = c[r.B + b];
+        if (r.mode == 1) f += 4.0 * r.unit * (c0 * c0 + c1 * c1);
+        else if (r.mode == 2) f += 6.0 * r.unit * c0 * c1;
+        else f += r.unit * (c0 + c1);
+      }
+    }
+    fl += f;
     by += r.bytes;
     ++n;
   }

@@ -15,7 +15,11 @@ Deliberate behaviour differences from the reference:
   raising ``UnboundLocalError`` (:452-455);
 * ``ref_descriptors*`` is ``[B, 1, M', 256]`` in eval mode and ``[B, L, M, 256]`` (every layer) in
   training mode, as the reference (:521-524,572); training mode also turns early stop and pruning
-  off (:502-503).  There is no autograd: a training-mode call with gradients enabled raises.
+  off (:502-503).  There is no autograd: a training-mode call with gradients enabled raises, and
+  :meth:`LightGlue.loss` returns forward values only.
+* with pruning and B > 1, ``log_assignment`` and ``ref_descriptors*`` are per-pair LISTS (pair b's
+  kept block; the reference asserts B == 1, :528,533); ``kept0/1`` and ``stop_layer`` give the
+  per-pair counts.
 """
 import ctypes
 import warnings
@@ -112,8 +116,10 @@ def _ptr(t):
 
 # Extension keys (no reference counterpart).  "precision": matrix-core operand format of the HIP
 # kernels, both fp32-accurate -- "auto" (fp16x3, run-time operands range-scaled on the device) or "bf16x6"
-# (DESIGN.md §3).
-EXTENSION_CONF = {"precision": "auto"}
+# (DESIGN.md §3).  "return_similarity": also return the final head's similarity md0 md1^T
+# [B, M, N] as pred["similarity"] (MatchAssignment's second output, lightglue.py:311,315; the input
+# of a Sinkhorn assignment head, configs[4]).
+EXTENSION_CONF = {"precision": "auto", "return_similarity": False}
 
 
 class LightGlue(nn.Module):
@@ -393,8 +399,9 @@ class LightGlue(nn.Module):
         final1, layers1 = (None, rd1) if self.training else (rd1, None)
         kept = torch.empty((2, b), dtype=torch.int32, device=device) if pruning else None
         stop = torch.empty((b,), dtype=torch.int32, device=device) if pruning else None
+        sim = torch.empty((b, m, n), dtype=torch.float32, device=device) if c.return_similarity else None
         out = _lib.LGOutputs(*[_ptr(t) for t in (m0, m1, ms0, ms1, la, final, final1, p0, p1, layers, layers1, kept, stop)],
-                             0, 0, 0, 0)
+                             0, 0, 0, 0, _ptr(sim))
         stream = torch.cuda.current_stream(device).cuda_stream
         _lib.check(
             lib.lg_forward(self._handle, ctypes.byref(inp), ctypes.byref(out), _ptr(self._ws), ws_bytes.value, ctypes.c_void_p(stream)),
@@ -419,6 +426,8 @@ class LightGlue(nn.Module):
             # extension key (no reference counterpart): index of the last executed layer, per pair
             "stop_layer": torch.full((b,), out.stop_layer, dtype=torch.int64),
         }
+        if sim is not None:
+            pred["similarity"] = sim
         if pruning:
             # kept points per pair (the library synchronised once to return them): the
             # reference's outputs cover the kept points only -- its log_assignment is
@@ -459,8 +468,116 @@ class LightGlue(nn.Module):
         )
         return ms.value, n.value, fl.value, by.value
 
+    # ------------------------------------------------------------ training loss (forward values)
+    def assignment_head(self, layer, desc0, desc1, token_logits=False):
+        """``self.log_assignment[layer](desc0, desc1)`` (MatchAssignment, lightglue.py:306-315 +
+        :284-296) on the HIP library: returns (log_assignment [B, M+1, N+1], similarity [B, M, N])
+        and, with ``token_logits``, the ``token_confidence[layer]`` logits (before the sigmoid) of
+        both descriptor sets.  ``layer`` indexes like a list (-1 = the last head)."""
+        device = desc0.device
+        if device.type != "cuda":
+            raise RuntimeError("lightglue_amd: inputs must be on a HIP (cuda) device; there is no CPU path")
+        lib = self._ensure_handle(device)
+        d0 = desc0.to(torch.float32).contiguous()
+        d1 = desc1.to(torch.float32).contiguous()
+        b, m, _ = d0.shape
+        n = d1.shape[1]
+        la = torch.empty((b, m + 1, n + 1), dtype=torch.float32, device=device)
+        sim = torch.empty((b, m, n), dtype=torch.float32, device=device)
+        t0 = torch.empty((b, m), dtype=torch.float32, device=device) if token_logits else None
+        t1 = torch.empty((b, n), dtype=torch.float32, device=device) if token_logits else None
+        nb = ctypes.c_size_t()
+        _lib.check(lib.lg_assignment_workspace_bytes(self._handle, b, m, n, ctypes.byref(nb)), "lg_assignment_workspace_bytes")
+        ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        _lib.check(lib.lg_assignment_head(self._handle, int(layer), _ptr(d0), _ptr(d1), b, m, n, _ptr(la), _ptr(sim),
+                                          _ptr(t0), _ptr(t1), _ptr(ws), nb.value, ctypes.c_void_p(stream)),
+                   "lg_assignment_head")
+        return (la, sim, t0, t1) if token_logits else (la, sim)
+
     def loss(self, pred, data):
-        raise NotImplementedError("training is out of scope for the MI355X matcher (SURVEY.md §2)")
+        """LightGlue.loss (lightglue.py:614-663), forward values (no backward): the NLL of every
+        layer's assignment head on that layer's descriptors (``pred["ref_descriptors*"]`` is
+        [B, L, M, 256] in training mode, [B, 1, M, 256] in eval mode, so eval evaluates the last
+        head only), weighted by ``gamma ** (L - i - 1)``; the token-confidence BCE of layers
+        0..L-2 (:108-122; added to ``total`` in training mode); ``row_norm``; and, in eval mode,
+        ``matcher_metrics`` (models/utils/metrics.py).  The heads and the NLL sums run in the HIP
+        library (``lg_assignment_head``, ``sg_nll_loss``); what stays in torch is the reference's
+        per-point glue (argmax agreement, BCE on [B, M] logits, metric ratios)."""
+        from .superglue import NLLLoss
+
+        lconf = self.conf.loss
+        if lconf.get("fn", "nll") != "nll":
+            raise NotImplementedError(f"loss fn {lconf.fn!r} (the reference defines only 'nll')")
+        loss_fn = NLLLoss({"nll_balancing": lconf.nll_balancing})
+        rd0, rd1 = pred["ref_descriptors0"], pred["ref_descriptors1"]
+        N = rd0.shape[1]
+        la_last, _ = self.assignment_head(-1, rd0[:, -1], rd1[:, -1])
+        nll, gt_weights, loss_metrics = loss_fn({"log_assignment": la_last}, data)
+        sum_weights = 1.0
+        losses = {"total": nll, "last": nll.clone().detach(), **loss_metrics}
+        if self.training:
+            losses["confidence"] = 0.0
+        losses["row_norm"] = pred["log_assignment"].exp()[:, :-1].sum(2).mean(1)
+        la_final = pred["log_assignment"]
+        for i in range(N - 1):
+            la_i, _, lg0, lg1 = self.assignment_head(i, rd0[:, i], rd1[:, i], token_logits=True)
+            nll_i, _, _ = loss_fn({"log_assignment": la_i}, data, weights=gt_weights)
+            weight = lconf.gamma ** (N - i - 1) if lconf.gamma > 0.0 else i + 1
+            sum_weights += weight
+            losses["total"] = losses["total"] + nll_i * weight
+            # TokenConfidence.loss (:108-122): does layer i already pick the final argmax?
+            correct0 = la_final[:, :-1, :].max(-1).indices == la_i[:, :-1, :].max(-1).indices
+            correct1 = la_final[:, :, :-1].max(-2).indices == la_i[:, :, :-1].max(-2).indices
+            bce = torch.nn.functional.binary_cross_entropy_with_logits
+            tok = (bce(lg0, correct0.float(), reduction="none").mean(-1)
+                   + bce(lg1, correct1.float(), reduction="none").mean(-1)) / 2.0
+            losses["confidence"] = losses.get("confidence", 0.0) + tok / (N - 1)
+        losses["total"] = losses["total"] / sum_weights
+        if self.training:
+            losses["total"] = losses["total"] + losses["confidence"]
+        metrics = {} if self.training else matcher_metrics(pred, data)
+        return losses, metrics
+
+
+@torch.no_grad()
+def matcher_metrics(pred, data, prefix="", prefix_gt=None):
+    """gluefactory/models/utils/metrics.py: match recall / precision / accuracy and the ranking AP
+    of ``matches0`` against ``gt_matches0`` (per-pair ratios over [B, M] index tensors)."""
+
+    def recall(m, gt_m):
+        mask = (gt_m > -1).float()
+        return ((m == gt_m) * mask).sum(1) / (1e-8 + mask.sum(1))
+
+    def accuracy(m, gt_m):
+        mask = (gt_m >= -1).float()
+        return ((m == gt_m) * mask).sum(1) / (1e-8 + mask.sum(1))
+
+    def precision(m, gt_m):
+        mask = ((m > -1) & (gt_m >= -1)).float()
+        return ((m == gt_m) * mask).sum(1) / (1e-8 + mask.sum(1))
+
+    def ranking_ap(m, gt_m, scores):
+        p_mask = ((m > -1) & (gt_m >= -1)).float()
+        r_mask = (gt_m > -1).float()
+        order = torch.argsort(-scores)
+        sp = torch.gather(p_mask, -1, order)
+        sr = torch.gather(r_mask, -1, order)
+        tp = torch.gather(m == gt_m, -1, order)
+        p_pts = torch.cumsum(tp * sp, -1) / (1e-8 + torch.cumsum(sp, -1))
+        r_pts = torch.cumsum(tp * sr, -1) / (1e-8 + sr.sum(-1)[:, None])
+        return torch.sum((r_pts[..., 1:] - r_pts[..., :-1]) * p_pts[:, None, -1], dim=-1)
+
+    if prefix_gt is None:
+        prefix_gt = prefix
+    m0 = pred[f"{prefix}matches0"]
+    gt0 = data[f"gt_{prefix_gt}matches0"].to(m0.device)
+    return {
+        f"{prefix}match_recall": recall(m0, gt0),
+        f"{prefix}match_precision": precision(m0, gt0),
+        f"{prefix}accuracy": accuracy(m0, gt0),
+        f"{prefix}average_precision": ranking_ap(m0, gt0, pred[f"{prefix}matching_scores0"]),
+    }
 
 
 __main_model__ = LightGlue

@@ -15,8 +15,8 @@ Deliberate differences from the reference:
   (``weights`` is ignored) and takes weights through ``load_state_dict``;
 * eval only: BatchNorm uses its running statistics; a module in training mode raises (the
   reference trains through ``torch.utils.checkpoint`` and batch statistics);
-* ``NLLLoss`` with explicit ``weights`` raises NotImplementedError (the kernel derives the weights
-  from the ground truth, :46-73).
+* ``NLLLoss`` with explicit ``weights`` other than the ground truth's raises NotImplementedError
+  (the kernel derives the weights from the ground truth, losses.py:46-73).
 """
 import ctypes
 
@@ -264,8 +264,25 @@ def _nll(la, data, mode, balancing):
     return out
 
 
+def nll_weights(la, data):
+    """losses.py:62-73 (``NLLLoss.nll_loss``): the [B, M+1, N+1] loss weights of a ground truth,
+    built on the device exactly as the reference builds them (column dustbin written at [:, -1, :m],
+    so only M == N runs, as in the reference)."""
+    m, n = data["gt_matches0"].size(-1), data["gt_matches1"].size(-1)
+    dev = la.device
+    weights = torch.zeros_like(la)
+    weights[:, :m, :n] = data["gt_assignment"].to(dev).float()
+    weights[:, :m, -1] = (data["gt_matches0"].to(dev) == -1).float()
+    weights[:, -1, :m] = (data["gt_matches1"].to(dev) == -1).float()
+    return weights
+
+
 class NLLLoss(nn.Module):
-    """losses.py:26-73 (forward values; no backward): ``forward(pred, data) -> (nll, None, metrics)``."""
+    """losses.py:26-73 (forward values; no backward): ``forward(pred, data, weights=None) ->
+    (nll, weights, metrics)``.  The sums run in ``sg_nll_kernel`` (fp64), which derives the weights
+    from the ground truth itself; the returned ``weights`` tensor is the reference's [B, M+1, N+1]
+    one (losses.py:52-60).  Explicit ``weights`` must be those ground-truth weights (what
+    LightGlue.loss passes back, lightglue.py:633); any other weighting raises NotImplementedError."""
 
     default_conf = {"nll_balancing": 0.5, "gamma_f": 0.0}
 
@@ -274,9 +291,11 @@ class NLLLoss(nn.Module):
         self.conf = merge_conf(self.default_conf, conf or {})
 
     def forward(self, pred, data, weights=None):
-        if weights is not None:
-            raise NotImplementedError("explicit loss weights (the kernel derives them from the ground truth)")
-        out = _nll(pred["log_assignment"], data, 1, float(self.conf.nll_balancing))
+        la = pred["log_assignment"]
+        derived = nll_weights(la, data)
+        if weights is not None and not (weights.shape == derived.shape and torch.equal(weights.to(la.device), derived)):
+            raise NotImplementedError("explicit loss weights other than the ground truth's (the kernel derives them)")
+        out = _nll(la, data, 1, float(self.conf.nll_balancing))
         metrics = {"assignment_nll": out[0], "nll_pos": out[1], "nll_neg": out[2], "num_matchable": out[3],
                    "num_unmatchable": out[4]}
-        return out[0], None, metrics
+        return out[0], derived, metrics

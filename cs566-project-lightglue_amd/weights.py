@@ -137,6 +137,26 @@ def synthetic_state_dict(conf=None, seed=0, sharpen=True):
     return sd
 
 
+# configs[3] recipe (N = 2048, width = depth = 0.95): per-layer token-confidence and matchability
+# biases on top of the seed-8 weights, found by tools/tune_prune_golden.py -- layers 0..4 prune
+# ~10 % of the points each, layer 5 fires the early stop; every decision threshold sits in a
+# >= 1e-3 gap of the sorted decision logits.  None = keep the recipe value.
+PRUNE2K_TOKEN_BIAS = [2.0127, 2.2824, 1.7838, 1.715, 0.9317, 6.3066, None, None]
+PRUNE2K_MATCH_BIAS = [-2.5056, -2.4873, -1.8882, -3.3078, -2.4224, None, None, None]
+
+
+def prune_recipe_state_dict(conf=None, seed=8):
+    """Weights that really prune and stop early at N = 2048 (the configs[3] workload and the
+    ``prune_depth_width_n2048`` golden): ``synthetic_state_dict(conf, seed)`` with the biases above."""
+    sd = synthetic_state_dict(conf, seed=seed)
+    for i, (tb, mb) in enumerate(zip(PRUNE2K_TOKEN_BIAS, PRUNE2K_MATCH_BIAS)):
+        if tb is not None and f"token_confidence.{i}.token.0.bias" in sd:
+            sd[f"token_confidence.{i}.token.0.bias"][:] = tb
+        if mb is not None and f"log_assignment.{i}.matchability.bias" in sd:
+            sd[f"log_assignment.{i}.matchability.bias"][:] = mb
+    return sd
+
+
 def synthetic_pair(B, M, N=None, dim=256, seed=1, width=640, height=640, noise=0.05, kpt_noise=1.0):
     """Synthetic pair batch.  Returns a dict of NumPy arrays.
 

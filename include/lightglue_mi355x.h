@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define LG_ABI_VERSION 4
+#define LG_ABI_VERSION 5
 
 enum {
   LG_OK = 0,
@@ -112,6 +112,12 @@ typedef struct {
   int32_t stop_layer;           /* host out: last executed layer (of pair 0) */
   int32_t kept0, kept1;         /* host out: M', N' of pair 0 after width pruning (= M, N without) */
   int32_t precision_used;       /* host out: 0 = fp16x3, 1 = bf16x6 (LG_PREC_X6) */
+  float* similarity;            /* device [B,M,N] or NULL: md0 md1^T of the final assignment head, the
+                                 * second output of MatchAssignment.forward (lightglue.py:311,315;
+                                 * the input of a Sinkhorn head, configs[4]); with pruning pair b's
+                                 * kept block at the [M, N] strides.  Requesting it materialises the
+                                 * similarity (bf16x6 GEMM) instead of recomputing it in the fused
+                                 * assignment passes */
 } lg_outputs_t;
 
 int lg_abi_version(void);
@@ -141,6 +147,18 @@ int lg_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, si
  * own, with the counts kept on the device) and synchronise the stream once at the end. */
 int lg_forward(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out, void* workspace,
                size_t workspace_bytes, void* stream);
+
+/* MatchAssignment of layer `layer` (python-style: -1 = last) on caller descriptors desc0 [B,M,256],
+ * desc1 [B,N,256] (lightglue.py:306-315 followed by sigmoid_log_double_softmax :284-296):
+ * log_assignment [B,M+1,N+1] (required), similarity [B,M,N] (nullable).  token_logits0/1 [B,M] /
+ * [B,N] (nullable; layers 0..L-2): the token_confidence Linear before its sigmoid, which
+ * TokenConfidence.loss feeds to BCEWithLogits (:108-122).  LightGlue.loss (:614-663) evaluates
+ * every layer's head this way.  Stream-ordered, asynchronous.  Workspace:
+ * lg_assignment_workspace_bytes. */
+int lg_assignment_workspace_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+int lg_assignment_head(lg_handle_t* h, int32_t layer, const float* desc0, const float* desc1, int32_t B,
+                       int32_t M, int32_t N, float* log_assignment, float* similarity, float* token_logits0,
+                       float* token_logits1, void* workspace, size_t workspace_bytes, void* stream);
 
 /* In-library kernel timing (no reference counterpart; the reference times whole forwards with
  * CUDA events, gluefactory/utils/benchmark.py:7-33).  While enabled, lg_forward brackets every

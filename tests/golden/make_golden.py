@@ -42,7 +42,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 import lgamd  # noqa: E402,F401
-from lightglue_amd.weights import synthetic_pair, synthetic_state_dict  # noqa: E402
+from lightglue_amd.weights import PRUNE2K_MATCH_BIAS, PRUNE2K_TOKEN_BIAS, synthetic_pair, synthetic_state_dict  # noqa: E402,F401
 
 
 class _ADict(dict):
@@ -124,12 +124,9 @@ def sha(arrs):
 # unpruned logits).
 PRUNE_BIAS = [-2.97, -2.32, -2.90, -2.29, -3.00, -2.80, -2.14, -2.37]
 
-# configs[3]-shaped case (N = 2048, width = depth = 0.95): per-layer biases from
-# tools/tune_prune_golden.py -- layers 0..4 prune ~10 % of the points each, layer 5 stops early;
-# every decision threshold sits in a >= 1e-3 gap of the sorted decision logits.  None = keep the
-# recipe value (layers the forward never reaches, and the head of the stopping layer).
-PRUNE2K_TOKEN_BIAS = [2.0127, 2.2824, 1.7838, 1.715, 0.9317, 6.3066, None, None]
-PRUNE2K_MATCH_BIAS = [-2.5056, -2.4873, -1.8882, -3.3078, -2.4224, None, None, None]
+# configs[3]-shaped case (N = 2048, width = depth = 0.95): PRUNE2K_TOKEN_BIAS / PRUNE2K_MATCH_BIAS
+# (lightglue_amd.weights, from tools/tune_prune_golden.py) -- layers 0..4 prune ~10 % of the points
+# each, layer 5 stops early.
 
 # name -> (conf overrides, pair kwargs, weight kwargs, weight overrides, store_full)
 CASES = {

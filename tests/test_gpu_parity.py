@@ -717,3 +717,34 @@ def test_deep_config_matches_oracle(prune):
     same = ok0 & ((m0 > -1) == (r0 > -1))
     np.testing.assert_allclose(pred["matching_scores0"].cpu().numpy()[same], ref["matching_scores0"].numpy()[same],
                                atol=SCORE_TOL)
+
+
+def test_profile_flops_count_kept_points_only():
+    """lg_profile_read on a pruned forward: each attention launch's algorithmic flops come from the
+    per-pair kept counts at launch time (stopped pairs excluded), so they equal what the prune
+    counts imply -- point i of a pair takes part in layers l < prune[i] (lightglue.py:540)."""
+    g = load("prune_depth_width_n512")
+    conf, sd, data = case_inputs(g["meta"])
+    from lightglue_amd.weights import synthetic_pair
+
+    pkw = dict(g["meta"]["pair"])
+    pairs = []
+    for s_ in (22, 5):
+        pkw["seed"] = s_
+        pairs.append(synthetic_pair(**pkw))
+    model = _model(conf, sd)
+    batch = _gpu_data(_stack_pairs(pairs))
+    with torch.no_grad():
+        model(batch)
+        model.profile_enable(True, only=("attention",))
+        pred = model(batch)
+        ms, n, fl, _ = model.profile_read("attention")
+        model.profile_enable(False)
+    p0, p1 = pred["prune0"].cpu().numpy(), pred["prune1"].cpu().numpy()
+    want = 0.0
+    for b in range(2):
+        for li in range(int(pred["stop_layer"][b]) + 1):
+            m_, n_ = float((p0[b] > li).sum()), float((p1[b] > li).sum())
+            want += 4.0 * 256 * (m_ * m_ + n_ * n_) + 6.0 * 256 * m_ * n_
+    assert n >= 2 * int(pred["stop_layer"].max() + 1)
+    assert fl == pytest.approx(want, rel=1e-12)

@@ -87,6 +87,17 @@ def test_superglue_losses_match_reference(name):
     if g["meta"]["nll_error"] is None:
         total, w, metrics = NLLLoss({})({"log_assignment": la}, gtd)
         np.testing.assert_allclose(total.cpu().numpy(), g["nll_total"], rtol=1e-5)
+        # the weights tensor of losses.py:62-73 is returned, and passing it back is accepted
+        mm = gt["gt_matches0"].shape[-1]
+        want = np.zeros(la.shape, np.float32)
+        want[:, :mm, :mm] = gt["gt_assignment"]
+        want[:, :mm, -1] = gt["gt_matches0"] == -1
+        want[:, -1, :mm] = gt["gt_matches1"] == -1
+        np.testing.assert_array_equal(w.cpu().numpy(), want)
+        again, _, _ = NLLLoss({})({"log_assignment": la}, gtd, weights=w)
+        assert torch.equal(again, total)
+        with pytest.raises(NotImplementedError):
+            NLLLoss({})({"log_assignment": la}, gtd, weights=w * 2)
         for k, v in metrics.items():
             np.testing.assert_allclose(v.cpu().numpy(), g[f"nll_{k}"], rtol=1e-5, err_msg=k)
     else:

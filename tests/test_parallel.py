@@ -177,3 +177,14 @@ def test_bench_rejects_world_size_mismatch():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--selftest-cpu", "--cpu-budget", "0"], cwd=root,
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+@pytest.mark.parametrize("workload,path", [("configs3", "match_dynamic"), ("configs4", "match_static")])
+def test_bench_workload_rehearsals(workload, path):
+    """bench.py --workload configs3 / configs4 through two spawned gloo ranks (CPU stand-in
+    matcher): configs3 pulls guided chunks from the shared queue, configs4 runs static shards."""
+    res = _bench_json(["bench.py", "--gpus", "2", "--selftest-cpu", "--steps", "2", "--warmup", "1",
+                       "--batch", "5", "--npts", "16", "--cpu-budget", "0", "--workload", workload, "--chunk", "2"])
+    assert res["n_gpus"] == 2 and res["pairs_timed"] == 2 * 5 * 2
+    assert path in res["config"]["parallelism"]
+    assert res["config"]["workload"].startswith(workload)

@@ -66,19 +66,12 @@ def cfg1(dev, reps):
 
 
 def prune_recipe_model(conf, dev):
-    """Weights that really prune and stop (tests/golden/make_golden.py, configs[3] case: layers 0..4
-    prune ~10 % of the points, layer 5 fires the early stop)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-    from make_golden import PRUNE2K_MATCH_BIAS, PRUNE2K_TOKEN_BIAS  # noqa: E402
+    """Weights that really prune and stop (weights.prune_recipe_state_dict, the configs[3] golden's
+    recipe: layers 0..4 prune ~10 % of the points, layer 5 fires the early stop)."""
+    from lightglue_amd.weights import prune_recipe_state_dict
 
-    sd = synthetic_state_dict(conf, seed=8)
-    for i, (tb, mb) in enumerate(zip(PRUNE2K_TOKEN_BIAS, PRUNE2K_MATCH_BIAS)):
-        if tb is not None:
-            sd[f"token_confidence.{i}.token.0.bias"][:] = tb
-        if mb is not None:
-            sd[f"log_assignment.{i}.matchability.bias"][:] = mb
     m = LightGlue(conf).eval().to(dev)
-    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in prune_recipe_state_dict(conf).items()}, strict=True)
     return m
 
 

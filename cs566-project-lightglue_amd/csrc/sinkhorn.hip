@@ -17,6 +17,8 @@
 // General path (N > 4096): the u-step walks rows of `scores`, the v-step walks rows of a
 // transposed copy made once (tiled LDS transpose); one wave per row, two-pass max-then-sum.
 #include <algorithm>
+#include <cstdlib>
+#include <mutex>
 
 #include "common.h"
 #include "kernels.h"
@@ -327,7 +329,7 @@ __global__ void sinkhorn_colmerge_kernel(const float2* part, float* v, int B, in
 // LSE_i(Zc_ij + u_i) = log S_j - v_j.  Terms below fp32's range are lost where the exact kernel
 // keeps them; the merge flags any column whose S_j falls under 2^-100 and
 // log_optimal_transport then reruns with sinkhorn_fused_kernel (running max per column).
-template <int K4, bool VEC, int W>
+template <int K4, bool VEC, int W, bool NT>
 __global__ __launch_bounds__(W * 64) void sinkhorn_scaled_kernel(const float* __restrict__ scores,
                                                                  const float* __restrict__ v, float* u, float* part,
                                                                  int M, int N, int rw, int P, float alpha, float lm_in,
@@ -396,11 +398,11 @@ __global__ __launch_bounds__(W * 64) void sinkhorn_scaled_kernel(const float* __
       const int c = 256 * k + 4 * lane;
       if (VEC) {
         f32x4 t = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#if LG_SK_NT
-        if (c < N) t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane)));
-#else
-        if (c < N) t = *reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane));
-#endif
+        if (NT) {
+          if (c < N) t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane)));
+        } else {
+          if (c < N) t = *reinterpret_cast<const f32x4*>(row + 1024 * k + (uint32_t)(16 * lane));
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) y[k][e] = t[e];
       } else {
@@ -498,6 +500,49 @@ __global__ void sinkhorn_scaled_merge_kernel(const float* part, float* v, int* f
   if (__ballot(low) != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
+// The same merge with the P partials of a column spread over WAYS threads (fixed order: way w sums
+// partials w, w + WAYS, ..., then the ways are added in order): a pair group of one or two pairs
+// has P = 128-256 partials per column, whose sequential sum in one thread was latency-bound
+// (one 4097-thread launch, 256 dependent-latency loads each).  grid (ceil((N+1)/64), B), block (64, WAYS).
+template <int WAYS>
+__global__ __launch_bounds__(64 * WAYS) void sinkhorn_scaled_merge_ways_kernel(const float* part, float* v, int* flag, int N,
+                                                                               int P, float lm_in, float lm_bin) {
+  __shared__ float red[WAYS][64];
+  const int tx = threadIdx.x, w = threadIdx.y;
+  const int b = blockIdx.y, j = blockIdx.x * 64 + tx;
+  float S = 0.f;
+  if (j <= N) {
+    const float* q = part + (size_t)b * P * (N + 1) + j;
+#pragma unroll 4
+    for (int p = w; p < P; p += WAYS) S += q[(size_t)p * (N + 1)];
+  }
+  red[w][tx] = S;
+  __syncthreads();
+  if (w != 0) return;
+  S = 0.f;
+#pragma unroll
+  for (int k = 0; k < WAYS; ++k) S += red[k][tx];
+  bool low = false;
+  if (j <= N) {
+    const size_t t = (size_t)b * (N + 1) + j;
+    low = !(S >= 0x1p-100f);
+    const float lse = logf(S) - v[t];
+    v[t] = (j == N ? lm_bin : lm_in) - lse;
+  }
+  if (__ballot(low) != 0ull && tx == 0) atomicOr(flag, 1);
+}
+
+static void launch_scaled_merge(const float* part, float* v, int* flag, int B, int N, int P, float lm_in, float lm_bin,
+                                hipStream_t st) {
+  if (P >= 64) {
+    hipLaunchKernelGGL(sinkhorn_scaled_merge_ways_kernel<8>, dim3((N + 1 + 63) / 64, B), dim3(64, 8), 0, st, part, v, flag, N,
+                       P, lm_in, lm_bin);
+  } else {
+    hipLaunchKernelGGL(sinkhorn_scaled_merge_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, part, v, flag, B, N,
+                       P, lm_in, lm_bin);
+  }
+}
+
 template <int K4>
 static void launch_fused(const float* scores, const float* v, float* u, float2* part, int B, int M, int N,
                          const SkPlan& pl, float alpha, float lm_in, float mu_bin, hipStream_t st) {
@@ -516,21 +561,90 @@ static void launch_fused(const float* scores, const float* v, float* u, float2* 
 
 template <int K4>
 static void launch_scaled(const float* scores, const float* v, float* u, float* part, int B, int M, int N,
-                          const SkPlan& pl, float alpha, float lm_in, float mu_bin, hipStream_t st) {
+                          const SkPlan& pl, float alpha, float lm_in, float mu_bin, bool nt, hipStream_t st) {
   constexpr int W = sk_waves(K4, false);
   const dim3 grid(B * pl.p), block(W * 64);
-  if (N % 4 == 0)
-    hipLaunchKernelGGL((sinkhorn_scaled_kernel<K4, true, W>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw, pl.p,
-                       alpha, lm_in, mu_bin);
-  else
-    hipLaunchKernelGGL((sinkhorn_scaled_kernel<K4, false, W>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw,
+  if (N % 4 == 0) {
+    if (nt)
+      hipLaunchKernelGGL((sinkhorn_scaled_kernel<K4, true, W, true>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw,
+                         pl.p, alpha, lm_in, mu_bin);
+    else
+      hipLaunchKernelGGL((sinkhorn_scaled_kernel<K4, true, W, false>), grid, block, 0, st, scores, v, u, part, M, N,
+                         pl.rw, pl.p, alpha, lm_in, mu_bin);
+  } else {
+    hipLaunchKernelGGL((sinkhorn_scaled_kernel<K4, false, W, false>), grid, block, 0, st, scores, v, u, part, M, N, pl.rw,
                        pl.p, alpha, lm_in, mu_bin);
+  }
 }
 
+// Pair blocking (opt-in, LG_SK_GROUP=<pairs> or LG_SK_GROUP_MB=<MiB>): the scores of all B pairs
+// (B*M*N*4 bytes; 537 MB at configs[4]) do not fit the 256 MiB Infinity Cache, so iterating over
+// every pair streams them from HBM 50 times.  Pairs are independent, so they can run in groups
+// whose scores fit, each group through all its iterations before the next, with normal (allocating)
+// loads.  Measured at B = 8, N = 4096 (profiles/r03/sk_sweep.log): streaming 5.21 ms; groups of
+// 1 / 2 / 4 pairs 11.5 / 7.5 / 6.0 ms on one stream, 7.1 / 5.3 / 5.5 ms on two streams.  A group's
+// row kernel has only ~2 rows per wave, so its fixed costs (v staging, the 8-wave merge tree, the
+// partial write, the merge launch) outweigh the faster Infinity-Cache reads; streaming stays the
+// default.
+static int sk_group(int B, int M, int N) {
+  const size_t per = (size_t)M * N * 4;
+  if (const char* e = getenv("LG_SK_GROUP")) {
+    const int g = atoi(e);
+    return g <= 0 ? B : std::min(g, B);
+  }
+  const char* e = getenv("LG_SK_GROUP_MB");
+  if (!e) return B;  // streaming schedule
+  const size_t cap = (size_t)atof(e) << 20;
+  if ((size_t)B * per <= cap) return B;
+  return (int)std::max<size_t>(1, std::min<size_t>(B, cap / per));
+}
+
+// Pair groups run on LG_SK_STREAMS (default 2) library-owned streams, forked from and joined back
+// to the caller's stream with events: one group's small merge launch and launch gaps overlap the
+// other group's row kernel, and both groups' scores share the Infinity Cache (2 x 67 MB at N =
+// 4096).  Streams and events are created once per device and reused.
+static int sk_streams_wanted(int groups) {
+  int s = 2;
+  if (const char* e = getenv("LG_SK_STREAMS")) s = atoi(e);
+  return std::max(1, std::min({s, groups, 4}));
+}
+struct SkStreams {
+  hipStream_t s[4] = {};
+  hipEvent_t fork = nullptr, join[4] = {};
+  bool ok = false;
+};
+static hipError_t sk_streams_for_device(SkStreams*& out) {
+  static std::mutex mu;
+  static SkStreams per_dev[64];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(mu);
+  SkStreams& x = per_dev[dev];
+  if (!x.ok) {
+    for (int i = 0; i < 4; ++i) {
+      if ((e = hipStreamCreateWithFlags(&x.s[i], hipStreamNonBlocking)) != hipSuccess) return e;
+      if ((e = hipEventCreateWithFlags(&x.join[i], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    if ((e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming)) != hipSuccess) return e;
+    x.ok = true;
+  }
+  out = &x;
+  return hipSuccess;
+}
+
+// partial buffers (floats of (N+1)) one launch of pair group gb needs
+static size_t sk_group_parts(int gb, int M, int N) { return (size_t)gb * sk_plan(gb, M, N, false).p; }
+
 size_t sinkhorn_workspace_floats(int B, int M, int N) {
-  if (sk_fused_ok(M, N))  // [u | v | partials (max, sum) B x P x (N+1)]
-    return (size_t)B * (M + 1) + 64 + (size_t)B * (N + 1) + 64 +
-           2 * (size_t)B * std::max(sk_plan(B, M, N, true).p, sk_plan(B, M, N, false).p) * (N + 1) + 256 + 64;
+  if (sk_fused_ok(M, N)) {  // [u | v | partials (max, sum) B x P x (N+1) | flag]
+    const int G = sk_group(B, M, N);
+    const int ns = G < B ? sk_streams_wanted((B + G - 1) / G) : 1;
+    const size_t parts = std::max((size_t)B * std::max(sk_plan(B, M, N, true).p, sk_plan(B, M, N, false).p),
+                                  (size_t)ns * sk_group_parts(G, M, N));
+    return (size_t)B * (M + 1) + 64 + (size_t)B * (N + 1) + 64 + 2 * parts * (N + 1) + 256 + 64;
+  }
   return (size_t)B * M * N + (size_t)B * (M + 1) + (size_t)B * (N + 1) + 256;
 }
 
@@ -551,21 +665,51 @@ hipError_t log_optimal_transport(const float* scores, float alpha, int B, int M,
   if (fused) {
     float2* part = reinterpret_cast<float2*>(v + (size_t)B * (N + 1) + 64);
     const SkPlan pl = sk_plan(B, M, N, false), ple = sk_plan(B, M, N, true);
-    int* flag = reinterpret_cast<int*>(part + (size_t)B * std::max(pl.p, ple.p) * (N + 1)) + 64;
+    const int G0 = sk_group(B, M, N);
+    const int ns0 = G0 < B ? sk_streams_wanted((B + G0 - 1) / G0) : 1;
+    const size_t parts = std::max((size_t)B * std::max(pl.p, ple.p), (size_t)ns0 * sk_group_parts(G0, M, N));
+    int* flag = reinterpret_cast<int*>(part + parts * (N + 1)) + 64;
     const int k4 = (N + 255) / 256;
     int low = 0;
     if (kSkScaled) {
       if ((e = hipMemsetAsync(flag, 0, sizeof(int), st)) != hipSuccess) return e;
-      float* fp = reinterpret_cast<float*>(part);
-      for (int it = 0; it < iters; ++it) {
-        if (k4 <= 1) launch_scaled<1>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
-        else if (k4 <= 2) launch_scaled<2>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
-        else if (k4 <= 4) launch_scaled<4>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
-        else if (k4 <= 8) launch_scaled<8>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
-        else launch_scaled<16>(scores, v, u, fp, B, M, N, pl, alpha, norm, mu_bin, st);
-        hipLaunchKernelGGL(sinkhorn_scaled_merge_kernel, dim3((B * (N + 1) + 255) / 256), dim3(256), 0, st, fp, v, flag,
-                           B, N, pl.p, norm, nu_bin);
+      const int G = G0;
+      // streaming schedule (one group of every pair): the scores pass the caches non-temporally;
+      // pair-blocked groups keep theirs in the Infinity Cache
+      const bool nt = LG_SK_NT && G == B;
+      const int ns = ns0;
+      SkStreams* ss = nullptr;
+      if (ns > 1) {
+        if ((e = sk_streams_for_device(ss)) != hipSuccess) return e;
+        if ((e = hipEventRecord(ss->fork, st)) != hipSuccess) return e;
+        for (int q = 0; q < ns; ++q)
+          if ((e = hipStreamWaitEvent(ss->s[q], ss->fork, 0)) != hipSuccess) return e;
       }
+      for (int b0 = 0, gi = 0; b0 < B; b0 += G, ++gi) {
+        const int gb = std::min(G, B - b0);
+        const int q = gi % ns;
+        hipStream_t sq = ns > 1 ? ss->s[q] : st;
+        float* fp = reinterpret_cast<float*>(part) + (size_t)q * sk_group_parts(G, M, N) * (N + 1);
+        const SkPlan pg = sk_plan(gb, M, N, false);
+        const float* sc = scores + (size_t)b0 * M * N;
+        float* ug = u + (size_t)b0 * (M + 1);
+        float* vg = v + (size_t)b0 * (N + 1);
+        for (int it = 0; it < iters; ++it) {
+          if (k4 <= 1) launch_scaled<1>(sc, vg, ug, fp, gb, M, N, pg, alpha, norm, mu_bin, nt, sq);
+          else if (k4 <= 2) launch_scaled<2>(sc, vg, ug, fp, gb, M, N, pg, alpha, norm, mu_bin, nt, sq);
+          else if (k4 <= 4) launch_scaled<4>(sc, vg, ug, fp, gb, M, N, pg, alpha, norm, mu_bin, nt, sq);
+          else if (k4 <= 8) launch_scaled<8>(sc, vg, ug, fp, gb, M, N, pg, alpha, norm, mu_bin, nt, sq);
+          else launch_scaled<16>(sc, vg, ug, fp, gb, M, N, pg, alpha, norm, mu_bin, nt, sq);
+          launch_scaled_merge(fp, vg, flag, gb, N, pg.p, norm, nu_bin, sq);
+        }
+      }
+      if (ns > 1) {
+        for (int q = 0; q < ns; ++q) {
+          if ((e = hipEventRecord(ss->join[q], ss->s[q])) != hipSuccess) return e;
+          if ((e = hipStreamWaitEvent(st, ss->join[q], 0)) != hipSuccess) return e;
+        }
+      }
+      if ((e = hipGetLastError()) != hipSuccess) return e;
       // the flag decides whether the exact kernel reruns: one 4-byte read-back
       if ((e = hipMemcpyAsync(&low, flag, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
       if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;

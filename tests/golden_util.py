@@ -48,6 +48,10 @@ def case_inputs(meta):
     if "token_bias_layer" in over:
         li, val = over["token_bias_layer"]
         sd[f"token_confidence.{li}.token.0.bias"][:] = val
+    if "final_proj_scale" in over:
+        for k in sd:
+            if k.startswith("log_assignment.") and ".final_proj." in k:
+                sd[k] = (sd[k] * np.float32(over["final_proj_scale"])).astype(np.float32)
     pkw = dict(meta["pair"])
     data = synthetic_pair(**pkw)
     if conf.get("add_scale_ori"):

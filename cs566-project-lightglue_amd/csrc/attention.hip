@@ -455,6 +455,31 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       dma16(base, voff, dst);
     }
   };
+  // the same staging for a tile with no row past Nk (every tile but the ragged last one): the
+  // per-lane source offsets do not depend on t0 and are computed once here, so a full tile's
+  // pieces cost no VALU (the clamp above was ~16 VALU per 64-key step, ~7 % of the loop's VALU)
+  uint32_t voff_full[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int q = wave * PPW + i;
+    const bool isv = q >= PIECES / 2;
+    const int qq = isv ? q - PIECES / 2 : q;
+    const int r = (qq % (LT / 8)) * 8 + (lane >> 3), cs = lane & 7;
+    const int c = isv ? cs ^ (((r >> 1) & 3) << 1) : cs ^ ((r >> 1) & 7);
+    voff_full[i] = (uint32_t)(r * kHeadDim + c * 8) * 2u;
+  }
+  auto issue_full = [&](int t0, int buf) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;
+      const bool isv = q >= PIECES / 2;
+      const int qq = isv ? q - PIECES / 2 : q;
+      const int pl = qq / (LT / 8);
+      const _Float16* base = (isv ? Vp : Kp) + (size_t)pl * ps + (size_t)t0 * kHeadDim;
+      const uint32_t dst = (isv ? vs_lds : ks_lds) + (uint32_t)(((buf * 2 + pl) * PL + (qq % (LT / 8)) * 8 * kHeadDim) * 2);
+      dma16(base, voff_full[i], dst);
+    }
+  };
 
   const int kswz = (r16 >> 1) & 7;
   const int vq = (lane & 15) >> 2, vp4 = lane & 3;
@@ -471,6 +496,9 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   for (int dt = 0; dt < 4; ++dt) o[dt][0] = o[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_use[2] = {-INFINITY, -INFINITY};
   float l_run[2] = {0.f, 0.f};
+  // raise test (lmax - m_use) c > 3 as one compare against m_use + 3 / c, updated with m_use
+  float thr[2] = {-INFINITY, -INFINITY};
+  const float inv3c[2] = {3.f / c_lane[0], 3.f / c_lane[1]};
 
   // one 64-key softmax step over LDS rows off .. off+63 of the current buffer (off: element
   // offset buf*2*PL + sub*KT*kHeadDim, a compile-time constant in the main loop)
@@ -531,12 +559,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       const float lmax = fmaxf(max3f(m0, m1, m2), max3f(m3, m4, sc[3][qt][3]));
       // the lane-local max decides whether any query can need a raise; only then are the four
       // lanes of each query reduced (the raise itself is per query, exactly as in h3/h3m)
-      if (__ballot((lmax - m_use[qt]) * c_lane[qt] > 3.f) != 0ull) {
+      if (__ballot(lmax > thr[qt]) != 0ull) {
         const float tmax = max_x16_32(lmax);
         const bool need = (tmax - m_use[qt]) * c_lane[qt] > 3.f;
         const float m_new = need ? tmax : m_use[qt];
         const float alpha = __builtin_amdgcn_exp2f((m_use[qt] - m_new) * c_lane[qt]);
         m_use[qt] = m_new;
+        thr[qt] = m_new + inv3c[qt];
         l_run[qt] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
@@ -609,12 +638,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   {                                                                                 \
     int t = 0;                                                                      \
     for (; t + 2 <= nfull; t += 2) {                                                \
-      if (t + 1 < nlt) issue((t + 1) * LT, 1); /* buffer 1 released by the barrier */ \
+      issue_full((t + 1) * LT, 1); /* buffer 1 released by the barrier; t+1 < nfull */ \
       body(IC0{}, NoMask{}, EXc, t * LT);                                           \
       if constexpr (SUBS == 2) body(IC1{}, NoMask{}, EXc, t * LT + KT);             \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
       __syncthreads();                                                              \
-      if (t + 2 < nlt) issue((t + 2) * LT, 0);                                      \
+      if (t + 2 < nfull) issue_full((t + 2) * LT, 0);                               \
+      else if (t + 2 < nlt) issue((t + 2) * LT, 0);                                 \
       body(IC2{}, NoMask{}, EXc, (t + 1) * LT);                                     \
       if constexpr (SUBS == 2) body(IC3{}, NoMask{}, EXc, (t + 1) * LT + KT);       \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \

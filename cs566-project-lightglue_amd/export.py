@@ -18,6 +18,8 @@ Differences from the reference, all deliberate:
 """
 from pathlib import Path
 
+import warnings
+
 import numpy as np
 import torch
 
@@ -106,7 +108,13 @@ def _renormalize(pred, data):
 def export_predictions(loader, model, output_file=None, as_half=False, keys="*", callback_fn=None,
                        optional_keys=(), writer=None, device=None):
     """export_predictions.py:17-85 for any batch size.  ``writer`` defaults to
-    :class:`H5Writer` (``output_file``).  Returns ``output_file`` (or the writer)."""
+    :class:`H5Writer` (``output_file``).  Returns ``output_file`` (or the writer).
+
+    Tensor-valued predictions are written per pair (``v[b]``).  Per-pair LISTS of tensors (length B,
+    what the matcher returns for ``log_assignment`` / ``ref_descriptors*`` of a pruned B > 1 batch:
+    each pair's kept block) are written per pair too (``v[b]``).  Any other value (scalars, nested
+    dicts, lists of another length) has no per-pair form; such keys are skipped with one warning
+    naming them (the reference exports tensors only, ``export_predictions.py:66-68``)."""
     assert keys == "*" or isinstance(keys, (tuple, list))
     if writer is None:
         writer = H5Writer(output_file)
@@ -123,13 +131,17 @@ def export_predictions(loader, model, output_file=None, as_half=False, keys="*",
         with torch.cuda.stream(copy_stream):
             return batch_to_device(batch, device, non_blocking=True)
 
+    warned = set()
+
     def finish(item):  # host side of one batch: wait for its D2H copies, write every pair
-        host, names, event = item
+        host, host_lists, names, event = item
         if event is not None:
             event.synchronize()
         host = {k: v.numpy() for k, v in host.items()}
+        host_lists = {k: [x.numpy() for x in v] for k, v in host_lists.items()}
         for b, name in enumerate(names):
             arrays = {k: v[b] for k, v in host.items()}
+            arrays.update({k: v[b] for k, v in host_lists.items()})
             if as_half:
                 arrays = {k: (v.astype(np.float16) if v.dtype == np.float32 else v) for k, v in arrays.items()}
             try:
@@ -157,17 +169,26 @@ def export_predictions(loader, model, output_file=None, as_half=False, keys="*",
                 raise ValueError(f"Missing key {missing}")
             pred = {k: v for k, v in pred.items() if k in list(keys) + list(optional_keys)}
         assert len(pred) > 0
-        pred = {k: v for k, v in _renormalize(pred, data).items() if torch.is_tensor(v)}
+        names = list(data_host["name"])
+        pred = _renormalize(pred, data)
+        lists = {k: v for k, v in pred.items() if isinstance(v, (list, tuple)) and len(v) == len(names)
+                 and all(torch.is_tensor(x) for x in v)}
+        tensors = {k: v for k, v in pred.items() if torch.is_tensor(v)}
+        skipped = sorted(set(pred) - set(tensors) - set(lists) - warned)
+        if skipped:
+            warnings.warn(f"export_predictions: keys without a per-pair tensor form are not written: {skipped}")
+            warned.update(skipped)
         if on_gpu:
-            host = {k: v.to("cpu", non_blocking=True) for k, v in pred.items()}
+            host = {k: v.to("cpu", non_blocking=True) for k, v in tensors.items()}
+            host_lists = {k: [x.to("cpu", non_blocking=True) for x in v] for k, v in lists.items()}
             event = torch.cuda.Event()
             event.record(torch.cuda.current_stream(device))
         else:
-            host, event = {k: v.cpu() for k, v in pred.items()}, None
-        names = list(data_host["name"])
+            host, event = {k: v.cpu() for k, v in tensors.items()}, None
+            host_lists = {k: [x.cpu() for x in v] for k, v in lists.items()}
         if pending is not None:
             finish(pending)  # batch i-1 is written while batch i runs
-        pending = (host, names, event)
+        pending = (host, host_lists, names, event)
     if pending is not None:
         finish(pending)
     writer.close()

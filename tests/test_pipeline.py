@@ -126,3 +126,28 @@ def test_h5_writer_is_unavailable_here():
     except ImportError:
         with pytest.raises(ImportError):
             export.H5Writer("/tmp/nope.h5")
+
+
+class ListMatcher(FakeMatcher):
+    """A pruned B > 1 batch: per-pair LISTS of kept blocks for log_assignment / ref_descriptors,
+    plus a scalar that has no per-pair form (lightglue_amd.LightGlue with pruning)."""
+
+    def forward(self, data):
+        out = super().forward(data)
+        b = data["keypoints0"].shape[0]
+        out["log_assignment"] = [torch.full((i + 2, i + 3), float(i)) for i in range(b)]
+        out["stop_note"] = 7
+        return out
+
+
+def test_export_writes_per_pair_lists_and_names_skipped_keys():
+    pipeline.register_model("matchers.fake_lists", ListMatcher)
+    m = pipeline.TwoViewPipeline({"extractor": {"name": "extractors.fake"}, "matcher": {"name": "fake_lists"}})
+    loader = [_data(3, ["a/0", "a/1", "a/2"])]
+    w = export.MemoryWriter()
+    with pytest.warns(UserWarning, match="stop_note"):
+        export.export_predictions(loader, m, writer=w, device="cpu")
+    for i in range(3):
+        la = w.groups[f"a/{i}"]["log_assignment"]
+        assert la.shape == (i + 2, i + 3) and float(la[0, 0]) == i
+        assert "stop_note" not in w.groups[f"a/{i}"]

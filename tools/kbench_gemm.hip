@@ -65,7 +65,7 @@ double run_h3p(const Shape& s, float* bias, float* Y, int iters, _Float16* Yp, i
   return ms / iters;
 }
 
-template <int WN, int EPI = EPI_LN_GELU>
+template <int WN, int EPI = EPI_LN_GELU, int BM = 128>
 double run_ln(const Shape& s, float* bias, float* gam, float* bet, _Float16* Yp, int iters, int stagger = 0) {
   GemmH3Args a;
   memset(&a, 0, sizeof(a));
@@ -77,8 +77,8 @@ double run_ln(const Shape& s, float* bias, float* gam, float* bet, _Float16* Yp,
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto launch = [&]() {
-    if (EPI == EPI_LN_GELU) return gemm_h3_ln_launch<WN>(a, 0);
-    hipLaunchKernelGGL((gemm_h3_kernel<EPI_PROBE, 128, 2, 512, WN>), dim3((a.R + 127) / 128), dim3(2 * (512 / WN) * 64), 0, 0, a);
+    if (EPI == EPI_LN_GELU) return gemm_h3_ln_launch<WN, BM>(a, 0);
+    hipLaunchKernelGGL((gemm_h3_kernel<EPI_PROBE, BM, 2, 512, WN>), dim3((a.R + BM - 1) / BM), dim3((BM / 64) * (512 / WN) * 64), 0, 0, a);
     return hipGetLastError();
   };
   CK(launch());
@@ -199,6 +199,19 @@ int main() {
         CK(hipMemset(Y, 0, (size_t)s.R * s.N * 4));
         ms = run_h3p(s, bias, Y, it, Yp, grid); rep(nm, ms, true);
       }
+      continue;
+    }
+    if (getenv("KB_LN64")) {  // LN GEMM at 64-row vs 128-row tiles (k-loop and full)
+      if (s.N != 512) continue;
+      float *gam, *bet;
+      CK(hipMalloc(&gam, s.N * 4)); CK(hipMalloc(&bet, s.N * 4));
+      fill<<<(s.N + 255) / 256, 256>>>(gam, s.N, 4);
+      fill<<<(s.N + 255) / 256, 256>>>(bet, s.N, 5);
+      ms = run_ln<64, EPI_PROBE, 128>(s, bias, nullptr, nullptr, Yp, it); rep("h3  128x512, no epilogue", ms, false);
+      ms = run_ln<64, EPI_LN_GELU, 128>(s, bias, gam, bet, Yp, it); rep("h3  LN+GELU 128x512", ms, false);
+      ms = run_ln<64, EPI_PROBE, 64>(s, bias, nullptr, nullptr, Yp, it); rep("h3  64x512, no epilogue", ms, false);
+      ms = run_ln<64, EPI_LN_GELU, 64>(s, bias, gam, bet, Yp, it); rep("h3  LN+GELU 64x512", ms, false);
+      CK(hipFree(gam)); CK(hipFree(bet));
       continue;
     }
     if (getenv("KB_LN")) {  // LN epilogue probes (build with -DLG_LN_PROBE=0/1/2/3)

@@ -915,6 +915,29 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
       dma16(base, voff, dst);
     }
   };
+  // full tiles: t0-independent per-lane source offsets, computed once (as attention_h3g_kernel)
+  uint32_t voff_full[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int q = wave * PPW + i;
+    const bool isv = q >= PIECES / 2;
+    const int qq = isv ? q - PIECES / 2 : q;
+    const int r = (qq % (LT / 8)) * 8 + (lane >> 3), cs = lane & 7;
+    const int c = isv ? cs ^ (((r >> 1) & 1) << 2) : cs ^ ((r >> 1) & 7);
+    voff_full[i] = (uint32_t)(r * kHeadDim + c * 8) * 2u;
+  }
+  auto issue_full = [&](int t0, int buf) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;
+      const bool isv = q >= PIECES / 2;
+      const int qq = isv ? q - PIECES / 2 : q;
+      const int pl = qq / (LT / 8);
+      const _Float16* base = (isv ? Vp : Kp) + (size_t)pl * ps + (size_t)t0 * kHeadDim;
+      const uint32_t dst = (isv ? vs_lds : ks_lds) + (uint32_t)(((buf * 2 + pl) * PL + (qq % (LT / 8)) * 8 * kHeadDim) * 2);
+      dma16(base, voff_full[i], dst);
+    }
+  };
 
   // per-lane LDS offsets: K fragment row l32, chunk 2ks + half (swizzled); transposed V reads:
   // 16-lane group covers dims 16 ((lane >> 4) & 1) + 4 (lane & 3) of lane half `half`, rows
@@ -930,6 +953,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
   f32x16 o0 = f32x16{0.f}, o1 = f32x16{0.f};  // O^T (x 2^11): dims [0,32) and [32,64)
   float m_use = -INFINITY;
   float l_run = 0.f;
+  float thr = -INFINITY;  // raise test (lmax - m_use) c > 3 as one compare, kept with m_use
+  const float inv3c = 3.f / c_lane;
 
   auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0) {
     const int off = OFFc;
@@ -983,12 +1008,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
     mt[10] = fmaxf(sc[1][14], sc[1][15]);
     const float lmax = fmaxf(max3f(max3f(mt[0], mt[1], mt[2]), max3f(mt[3], mt[4], mt[5]), max3f(mt[6], mt[7], mt[8])),
                              fmaxf(mt[9], mt[10]));
-    if (__ballot((lmax - m_use) * c_lane > 3.f) != 0ull) {
+    if (__ballot(lmax > thr) != 0ull) {
       const float tmax = max_xor32(lmax);
       const bool need = (tmax - m_use) * c_lane > 3.f;
       const float m_new = need ? tmax : m_use;
       const float alpha = __builtin_amdgcn_exp2f((m_use - m_new) * c_lane);
       m_use = m_new;
+      thr = m_new + inv3c;
       l_run *= alpha;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -1056,12 +1082,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
   {                                                                                 \
     int t = 0;                                                                      \
     for (; t + 2 <= nfull; t += 2) {                                                \
-      if (t + 1 < nlt) issue((t + 1) * LT, 1);                                      \
+      issue_full((t + 1) * LT, 1); /* t + 1 < nfull */                              \
       body(IC0{}, NoMask{}, EXc, t * LT);                                           \
       if constexpr (SUBS == 2) body(IC1{}, NoMask{}, EXc, t * LT + KT);             \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
       __syncthreads();                                                              \
-      if (t + 2 < nlt) issue((t + 2) * LT, 0);                                      \
+      if (t + 2 < nfull) issue_full((t + 2) * LT, 0);                               \
+      else if (t + 2 < nlt) issue((t + 2) * LT, 0);                                 \
       body(IC2{}, NoMask{}, EXc, (t + 1) * LT);                                     \
       if constexpr (SUBS == 2) body(IC3{}, NoMask{}, EXc, (t + 1) * LT + KT);       \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \

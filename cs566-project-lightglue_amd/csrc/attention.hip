@@ -452,7 +452,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       const _Float16* base = (isv ? Vp : Kp) + (size_t)pl * ps + (size_t)t0 * kHeadDim;
       const uint32_t voff = (uint32_t)((min(t0 + r, Nk - 1) - t0) * kHeadDim + c * 8) * 2u;
       const uint32_t dst = (isv ? vs_lds : ks_lds) + (uint32_t)(((buf * 2 + pl) * PL + (qq % (LT / 8)) * 8 * kHeadDim) * 2);
-      dma16(base, voff, dst);
+      dma16_u(base, voff, dst);
     }
   };
   // the same staging for a tile with no row past Nk (every tile but the ragged last one): the
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       const int pl = qq / (LT / 8);
       const _Float16* base = (isv ? Vp : Kp) + (size_t)pl * ps + (size_t)t0 * kHeadDim;
       const uint32_t dst = (isv ? vs_lds : ks_lds) + (uint32_t)(((buf * 2 + pl) * PL + (qq % (LT / 8)) * 8 * kHeadDim) * 2);
-      dma16(base, voff_full[i], dst);
+      dma16_u(base, voff_full[i], dst);
     }
   };
 
@@ -502,7 +502,11 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
 
   // one 64-key softmax step over LDS rows off .. off+63 of the current buffer (off: element
   // offset buf*2*PL + sub*KT*kHeadDim, a compile-time constant in the main loop)
-  auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0) {
+  // mid(): called between the exponentials and the P split / PV MFMAs -- the LDS-DMA pieces of the
+  // next tile are issued there, in the step's VALU-only stretch, where a piece costs a fraction of
+  // its issue price among the score MFMAs (MI355X_MICROARCH.md, LDS-DMA piece issue cost)
+  // nmode: 0 none, 1 issue_full(nt0, nbuf), 2 issue(nt0, nbuf) -- the next tile's staging
+  auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0, int nmode, int nt0, int nbuf) {
     const int off = OFFc;
     constexpr bool MASK = decltype(MASKc)::value;
     constexpr bool EXACT = decltype(EXc)::value;
@@ -596,6 +600,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       }
       l_run[qt] += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
     }
+    if (nmode == 1) issue_full(__builtin_amdgcn_readfirstlane(nt0), __builtin_amdgcn_readfirstlane(nbuf));
+    else if (nmode == 2) issue(__builtin_amdgcn_readfirstlane(nt0), __builtin_amdgcn_readfirstlane(nbuf));
 #pragma unroll
     for (int p = 0; p < NKT / 2; ++p)
 #pragma unroll
@@ -638,15 +644,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   {                                                                                 \
     int t = 0;                                                                      \
     for (; t + 2 <= nfull; t += 2) {                                                \
-      issue_full((t + 1) * LT, 1); /* buffer 1 released by the barrier; t+1 < nfull */ \
-      body(IC0{}, NoMask{}, EXc, t * LT);                                           \
-      if constexpr (SUBS == 2) body(IC1{}, NoMask{}, EXc, t * LT + KT);             \
+      /* buffer 1 released by the barrier; t+1 < nfull */                           \
+      body(IC0{}, NoMask{}, EXc, t * LT, 1, (t + 1) * LT, 1);                       \
+      if constexpr (SUBS == 2) body(IC1{}, NoMask{}, EXc, t * LT + KT, 0, 0, 0);    \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
       __syncthreads();                                                              \
-      if (t + 2 < nfull) issue_full((t + 2) * LT, 0);                               \
-      else if (t + 2 < nlt) issue((t + 2) * LT, 0);                                 \
-      body(IC2{}, NoMask{}, EXc, (t + 1) * LT);                                     \
-      if constexpr (SUBS == 2) body(IC3{}, NoMask{}, EXc, (t + 1) * LT + KT);       \
+      body(IC2{}, NoMask{}, EXc, (t + 1) * LT, t + 2 < nfull ? 1 : (t + 2 < nlt ? 2 : 0), (t + 2) * LT, 0); \
+      if constexpr (SUBS == 2) body(IC3{}, NoMask{}, EXc, (t + 1) * LT + KT, 0, 0, 0); \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
       __syncthreads();                                                              \
     }                                                                               \
@@ -655,7 +659,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       if (t + 1 < nlt) issue((t + 1) * LT, buf ^ 1);                                \
       for (int sub = 0; sub < SUBS; ++sub) {                                        \
         const int s0 = t * LT + sub * KT;                                           \
-        if (s0 < Nk) body(buf * 2 * PL + sub * KT * kHeadDim, Mask{}, EXc, s0);     \
+        if (s0 < Nk) body(buf * 2 * PL + sub * KT * kHeadDim, Mask{}, EXc, s0, 0, 0, 0); \
       }                                                                             \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
       __syncthreads();                                                              \

@@ -285,6 +285,14 @@ __device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t 
                : "memory");
 }
 
+// dma16 from code the compiler cannot prove wave-uniform (e.g. inside a lambda called from another
+// lambda): the base and the LDS address are made scalar explicitly (they are uniform by construction)
+__device__ __forceinline__ void dma16_u(const void* base, uint32_t voff, uint32_t lds) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  dma16(reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo), voff, __builtin_amdgcn_readfirstlane(lds));
+}
+
 // the same copy with the non-temporal hint (operands streamed exactly once)
 __device__ __forceinline__ void dma16_nt(const void* base, uint32_t voff, uint32_t lds) {
   unsigned keep;

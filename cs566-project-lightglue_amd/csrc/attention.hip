@@ -90,7 +90,7 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
   if (S.act && !S.act[pb]) return;
   const int Nq = S.nq_cnt ? S.nq_cnt[pb] : NqS, Nk = S.nk_cnt ? S.nk_cnt[pb] : NkS;
   if (q_blk >= Nq || Nk <= 0) return;
-  const float* Q = S.q + (size_t)bh * NqS * kHeadDim;
+  const float* Q = static_cast<const float*>(S.q) + (size_t)bh * NqS * kHeadDim;
   const __bf16* Kp = static_cast<const __bf16*>(S.kp) + (size_t)bh * NkS * kHeadDim;
   const __bf16* Vp = static_cast<const __bf16*>(S.vp) + (size_t)bh * NkS * kHeadDim;
   const long long ps = S.pstride;
@@ -274,6 +274,27 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
 // (These numerics are shared by the production attention_h3g_kernel below; the first kernel
 // built on them, attention_h3_kernel, now lives in tools/attn_h3_legacy.hip.)
 // ----------------------------------------------------------------------------------------
+// 8 consecutive dims of a query row (element offset off from q, the head's [Nq][64] block):
+// fp32 rows or (QP) a plane image (plane stride ps), whose h + l 2^-11 is exact in fp32 (22 significant
+// bits), times 2^E of its range slot (qsc) -- the values the fp32 rows would hold
+template <bool QP>
+__device__ __forceinline__ void load_q8(const void* q, long long ps, size_t off, float qsc, f32x4& a, f32x4& b) {
+  if constexpr (QP) {
+    const _Float16* qp = static_cast<const _Float16*>(q) + off;
+    const f16x8 h = *reinterpret_cast<const f16x8*>(qp);
+    const f16x8 l = *reinterpret_cast<const f16x8*>(qp + ps);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] = ((float)h[e] + (float)l[e] * (1.f / kLoScale)) * qsc;
+      b[e] = ((float)h[e + 4] + (float)l[e + 4] * (1.f / kLoScale)) * qsc;
+    }
+  } else {
+    const float* qf = static_cast<const float*>(q) + off;
+    a = *reinterpret_cast<const f32x4*>(qf);
+    b = *reinterpret_cast<const f32x4*>(qf + 4);
+  }
+}
+
 __device__ __forceinline__ f16x4 tr_read_h(const _Float16* p) {
   const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
   return __builtin_bit_cast(f16x4, v);
@@ -339,7 +360,7 @@ __device__ __forceinline__ float sum_x16_32(float v) {
 // workgroup each; instead of the context the workgroup writes its unnormalised partial (O, the
 // softmax reference m, the 2^11-scaled sum l and the query's exponent factor c) and
 // attn_split_combine_kernel merges the ranges.
-template <int SUBS, int PRIO, int WAVES = 8, bool SPLIT = false>
+template <int SUBS, int PRIO, int WAVES = 8, bool SPLIT = false, bool QP = false>
 __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
                                                                 float scale_log2e, float* part = nullptr,
                                                                 int nsplit = 1, int lsplit = 0) {
@@ -383,7 +404,9 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
     }
     return;
   }
-  const float* Q = S.q + (size_t)bh * NqS * kHeadDim;
+  const void* Q = QP ? static_cast<const void*>(static_cast<const _Float16*>(S.q) + (size_t)bh * NqS * kHeadDim)
+                    : static_cast<const void*>(static_cast<const float*>(S.q) + (size_t)bh * NqS * kHeadDim);
+  const float qsc = QP ? ldexpf(1.f, range_slot_exp(S.rtab, S.k_slot)) : 1.f;  // QP: queries from planes
   const _Float16* Kp = static_cast<const _Float16*>(S.kp) + ((size_t)bh * NkS + k0) * kHeadDim;
   const _Float16* Vp = static_cast<const _Float16*>(S.vp) + ((size_t)bh * NkS + k0) * kHeadDim;
   const long long ps = S.pstride;
@@ -404,13 +427,12 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int qrow = min(q_blk + wave * 32 + qt * 16 + r16, Nq - 1);
-    const float* qr = Q + (size_t)qrow * kHeadDim + 8 * g;
+    const size_t qr = (size_t)qrow * kHeadDim + 8 * g;
     f32x4 x[2][2];
     float mx = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      x[ks][0] = *reinterpret_cast<const f32x4*>(qr + 32 * ks);
-      x[ks][1] = *reinterpret_cast<const f32x4*>(qr + 32 * ks + 4);
+      load_q8<QP>(Q, S.pstride, qr + 32 * ks, qsc, x[ks][0], x[ks][1]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[ks][0][e]), fabsf(x[ks][1][e])));
     }
@@ -780,7 +802,7 @@ __global__ __launch_bounds__(256) void attn_split_combine_kernel(AttnSet s0, Att
 
 template <int SUBS, int PRIO = 0, int WAVES = 8>
 static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st,
-                                       float* part = nullptr, int nsplit = 1) {
+                                       bool qp, float* part = nullptr, int nsplit = 1) {
   constexpr int QB = 32 * WAVES;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
   if (nq == 0 || B == 0) return hipSuccess;
@@ -791,8 +813,12 @@ static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int
     constexpr int LT = 64 * SUBS;  // keys per LDS tile
     const int nk = s0.Nk > s1.Nk ? s0.Nk : s1.Nk;
     const int lsplit = ((nk + nsplit - 1) / nsplit + LT - 1) / LT * LT;
-    hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES, true>), dim3(items * nsplit), dim3(64 * WAVES), 0, st, s0, s1,
-                       B, H, nqb, scale * 1.4426950408889634f, part, nsplit, lsplit);
+    if (qp)
+      hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES, true, true>), dim3(items * nsplit), dim3(64 * WAVES), 0, st,
+                         s0, s1, B, H, nqb, scale * 1.4426950408889634f, part, nsplit, lsplit);
+    else
+      hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES, true>), dim3(items * nsplit), dim3(64 * WAVES), 0, st, s0,
+                         s1, B, H, nqb, scale * 1.4426950408889634f, part, nsplit, lsplit);
     const size_t threads = (size_t)2 * B * H * nq * 8;
     const dim3 cg((unsigned)((threads + 255) / 256)), cb(256);
     switch (nsplit) {
@@ -802,8 +828,12 @@ static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int
     }
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
-                     scale * 1.4426950408889634f);
+  if (qp)
+    hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES, false, true>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B,
+                       H, nqb, scale * 1.4426950408889634f);
+  else
+    hipLaunchKernelGGL((attention_h3g_kernel<SUBS, PRIO, WAVES>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
+                       scale * 1.4426950408889634f);
   return hipGetLastError();
 }
 
@@ -826,7 +856,7 @@ static hipError_t attention_h3g_launch(const AttnSet& s0, const AttnSet& s1, int
 // LDS: K as in h3g (16-byte chunk c of row r at c ^ ((r >> 1) & 7): the 32x32 fragment reads hit
 // 16 distinct slots per lane group too); V rows with the two 32-dim halves swapped where key bit 1
 // is set (each transposed read's 4 rows then cover all 64 banks).
-template <int SUBS, int PRIO, int WAVES = 8>
+template <int SUBS, int PRIO, int WAVES = 8, bool QP = false>
 __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_kernel(AttnSet s0, AttnSet s1, int B, int H, int nqb,
                                                                 float scale_log2e) {
   constexpr int QB = 32 * WAVES;
@@ -850,7 +880,9 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
   if (S.act && !S.act[pb]) return;
   const int Nq = S.nq_cnt ? S.nq_cnt[pb] : NqS, Nk = S.nk_cnt ? S.nk_cnt[pb] : NkS;
   if (q_blk >= Nq || Nk <= 0) return;
-  const float* Q = S.q + (size_t)bh * NqS * kHeadDim;
+  const void* Q = QP ? static_cast<const void*>(static_cast<const _Float16*>(S.q) + (size_t)bh * NqS * kHeadDim)
+                    : static_cast<const void*>(static_cast<const float*>(S.q) + (size_t)bh * NqS * kHeadDim);
+  const float qsc = QP ? ldexpf(1.f, range_slot_exp(S.rtab, S.k_slot)) : 1.f;  // QP: queries from planes
   const _Float16* Kp = static_cast<const _Float16*>(S.kp) + (size_t)bh * NkS * kHeadDim;
   const _Float16* Vp = static_cast<const _Float16*>(S.vp) + (size_t)bh * NkS * kHeadDim;
   const long long ps = S.pstride;
@@ -869,13 +901,12 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
   bool big;
   {
     const int qrow = min(q_blk + wave * 32 + l32, Nq - 1);
-    const float* qr = Q + (size_t)qrow * kHeadDim + 8 * half;
+    const size_t qr = (size_t)qrow * kHeadDim + 8 * half;
     f32x4 x[4][2];
     float mx = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      x[ks][0] = *reinterpret_cast<const f32x4*>(qr + 16 * ks);
-      x[ks][1] = *reinterpret_cast<const f32x4*>(qr + 16 * ks + 4);
+      load_q8<QP>(Q, S.pstride, qr + 16 * ks, qsc, x[ks][0], x[ks][1]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[ks][0][e]), fabsf(x[ks][1][e])));
     }
@@ -1145,15 +1176,20 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
 }
 
 template <int SUBS, int PRIO = 0, int WAVES = 8>
-static hipError_t attention_h3m_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st) {
+static hipError_t attention_h3m_launch(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, hipStream_t st,
+                                       bool qp) {
   constexpr int QB = 32 * WAVES;
   const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
   if (nq == 0 || B == 0) return hipSuccess;
   if (s0.Nk <= 0 || s1.Nk <= 0) return hipErrorInvalidValue;
   const int nqb = (nq + QB - 1) / QB;
   const int items = nqb * B * H * 2;
-  hipLaunchKernelGGL((attention_h3m_kernel<SUBS, PRIO, WAVES>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
-                     scale * 1.4426950408889634f);
+  if (qp)
+    hipLaunchKernelGGL((attention_h3m_kernel<SUBS, PRIO, WAVES, true>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
+                       scale * 1.4426950408889634f);
+  else
+    hipLaunchKernelGGL((attention_h3m_kernel<SUBS, PRIO, WAVES>), dim3(items), dim3(64 * WAVES), 0, st, s0, s1, B, H, nqb,
+                       scale * 1.4426950408889634f);
   return hipGetLastError();
 }
 
@@ -1218,28 +1254,29 @@ size_t attention_split_floats(int B, int H, int nq, int nk) {
 }
 
 hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st,
-                         float* part, size_t part_floats) {
+                         float* part, size_t part_floats, bool q_planes) {
   if (prec == PREC_H3) {
-    if (!s0.op || !s1.op) return hipErrorInvalidValue;
+    if (!s0.op || !s1.op || !s0.q || !s1.q) return hipErrorInvalidValue;
     const int nq = s0.Nq > s1.Nq ? s0.Nq : s1.Nq;
     if (attention_use_h3m()) {
       switch (attention_waves(B, H, nq)) {
-        case 2: return attention_h3m_launch<2, 1, 2>(s0, s1, B, H, scale, st);
-        case 4: return attention_h3m_launch<2, 1, 4>(s0, s1, B, H, scale, st);
-        default: return attention_h3m_launch<2, 1, 8>(s0, s1, B, H, scale, st);
+        case 2: return attention_h3m_launch<2, 1, 2>(s0, s1, B, H, scale, st, q_planes);
+        case 4: return attention_h3m_launch<2, 1, 4>(s0, s1, B, H, scale, st, q_planes);
+        default: return attention_h3m_launch<2, 1, 8>(s0, s1, B, H, scale, st, q_planes);
       }
     }
     switch (attention_waves(B, H, nq)) {
-      case 2: return attention_h3g_launch<2, 1, 2>(s0, s1, B, H, scale, st);
+      case 2: return attention_h3g_launch<2, 1, 2>(s0, s1, B, H, scale, st, q_planes);
       case 4: {
         const int nk = s0.Nk > s1.Nk ? s0.Nk : s1.Nk;
         const int ns = attention_nsplit(B, H, nq, nk);
         const bool fits = part && part_floats >= attention_split_floats(B, H, nq, nk);
-        return attention_h3g_launch<2, 1, 4>(s0, s1, B, H, scale, st, fits ? part : nullptr, fits ? ns : 1);
+        return attention_h3g_launch<2, 1, 4>(s0, s1, B, H, scale, st, q_planes, fits ? part : nullptr, fits ? ns : 1);
       }
-      default: return attention_h3g_launch<2, 1, 8>(s0, s1, B, H, scale, st);
+      default: return attention_h3g_launch<2, 1, 8>(s0, s1, B, H, scale, st, q_planes);
     }
   }
+  if (q_planes || !s0.q || !s1.q) return hipErrorInvalidValue;  // bf16x6 reads fp32 queries
   return attention_x6_launch<LG_ATTN_CONFIG>(s0, s1, B, H, scale, st);
 }
 

@@ -642,7 +642,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     // load-time Wqkv row order puts rotary partners in one lane of the MFMA tile).  Written into
     // LDS at their natural dim, each lane then owns whole rotary pairs of one row.
     //   self  (EPI_QKV_ROT):   t0 -> q fp32 (rotary), t1 -> k planes (rotary), t2 -> v planes
-    //   cross (EPI_CROSS_QKV): t0 -> qk fp32 * scale^0.5 and qk planes,        t1 -> v planes
+    //   cross (EPI_CROSS_QKV): t0 -> qk planes * scale^0.5 (+ fp32 rows when hl.q is set), t1 -> v planes
+    //   (the attention reads the cross queries from the qk planes: attention_f32's q_planes)
     const HeadLayout& hl = g.hl;
     for (int r = tid; r < BM; r += BM * 4) {
       int base = 0, stride = 0;
@@ -654,7 +655,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
     const int cbase = n0 + wn0;
     const int t = cbase / kDim, head = (cbase % kDim) / kHeadDim;
     const bool rot = EPI == EPI_QKV_ROT && t < 2 && hl.cosb;  // no cos table: plain q/k/v (SuperGlue)
-    const bool to_q = t == 0;
+    const bool to_q = t == 0 && hl.q;
     const bool to_kp = EPI == EPI_QKV_ROT ? t == 1 : t == 0;
     const bool to_vp = EPI == EPI_QKV_ROT ? t == 2 : t == 1;
     const float sc = (EPI == EPI_CROSS_QKV && t == 0) ? hl.qk_scale : 1.f;

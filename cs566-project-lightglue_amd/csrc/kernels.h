@@ -165,7 +165,11 @@ hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipSt
 // Attention over head-major Q/K/V ([set][b][h][n][64]); O written row-major into ctx
 // [rows][256] at column h*64 (rows in GEMM order).  Two "sets" per launch (blockIdx.z).
 struct AttnSet {
-  const float* q;    // [B][H][Nq][64] fp32
+  // [B][H][Nq][64] fp32 rows; with attention_f32(..., q_planes) (PREC_H3) instead a plane image
+  // [planes][B][H][Nq][64] (plane stride pstride) holding q * 2^-E[k_slot] -- the cross block's
+  // qk, whose planes the key side needs anyway, so the QKV GEMM stores it once (the pieces the
+  // attention forms from them are the ones it forms from the fp32 rows)
+  const void* q;
   const void* kp;    // [planes][B][H][Nk][64] (plane stride pstride): 3 bf16 (X6) / 2 fp16 (H3)
   const void* vp;    // [planes][B][H][Nk][64]
   long long pstride;
@@ -187,8 +191,9 @@ struct AttnSet {
 };
 // part / part_floats (optional): scratch for the key-split partials of small batches
 // (attention_split_floats(B, H, max Nq, max Nk) floats; without it the launch does not split)
+// q_planes (PREC_H3): both sets' q point at plane images with the key planes' exponent (k_slot)
 hipError_t attention_f32(const AttnSet& s0, const AttnSet& s1, int B, int H, float scale, int prec, hipStream_t st,
-                         float* part = nullptr, size_t part_floats = 0);
+                         float* part = nullptr, size_t part_floats = 0, bool q_planes = false);
 size_t attention_split_floats(int B, int H, int nq, int nk);
 
 // Positional encoding: normalised keypoints -> cos/sin tables [rows][32].

@@ -703,9 +703,9 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     g.acc_scale = pl.unscale;
   };
   auto image = [&](_Float16* p, int K) { return PlaneRef{p, (long long)RP * K, RP}; };
-  auto attn = [&](const AttnSet& a0, const AttnSet& a1, float scale, bool cross) -> hipError_t {
+  auto attn = [&](const AttnSet& a0, const AttnSet& a1, float scale, bool cross, bool q_planes) -> hipError_t {
     const int p = h->prof_begin(LG_KERNEL_ATTENTION, st);
-    const hipError_t e = attention_f32(a0, a1, B, H, scale, prec, st, w.apart, w.apart_floats);
+    const hipError_t e = attention_f32(a0, a1, B, H, scale, prec, st, w.apart, w.apart_floats, q_planes);
     // self: 2 matmuls per image (QK^T, PV); cross: one shared sim + two PV (lightglue.py:236-242)
     const double hd = 64.0 * H * B;
     const double fl = cross ? 6.0 * a0.Nq * a0.Nk * hd : 4.0 * hd * ((double)a0.Nq * a0.Nk + (double)a1.Nq * a1.Nk);
@@ -840,7 +840,10 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       // QKV projection with fused rotary (self) / scale (cross) and head-major scatter
       HeadLayout hl;
       hl.B = B; hl.H = H; hl.M = M; hl.N = N; hl.cosb = w.cosb; hl.sinb = w.sinb;
-      hl.q = w.Q; hl.kp = w.KP; hl.vp = w.VP; hl.pstride = (long long)w.R * D;
+      // the cross block's qk goes out only as planes in fp16x3 (the attention reads its queries
+      // from them: attention_f32's q_planes); self q and every bf16x6 query stay fp32 rows
+      const bool q_planes = prec == PREC_H3 && blk == 1;
+      hl.q = q_planes ? nullptr : w.Q; hl.kp = w.KP; hl.vp = w.VP; hl.pstride = (long long)w.R * D;
       hl.qk_scale = std::sqrt(1.f / std::sqrt(64.f));  // scale**0.5 (lightglue.py:235)
       const int epi_qkv = blk == 0 ? EPI_QKV_ROT : EPI_CROSS_QKV;
       const lg_handle::BlockGain& gn = h->gains[(size_t)i * 2 + blk];
@@ -873,11 +876,15 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       if (blk == 0) {  // self: q/k/v of the same image, scale 1/sqrt(64) (SDPA default)
         a0 = {w.Q, w.KP, w.VP, ps, w.ctx, M, M, w.Cp, (long long)RP * D, RP, 0, rt, s_k, c0, c0, act};
         a1 = {w.Q + img1, kp1, vp1, ps, ctx1, N, N, w.Cp, (long long)RP * D, RP, B * M, rt, s_k, c1, c1, act};
-      } else {  // cross: qk fp32 in w.Q and as planes in w.KP, v planes in w.VP
+      } else {  // cross: qk as planes in w.KP (fp16x3: also the queries; bf16x6: fp32 in w.Q), v planes in w.VP
         a0 = {w.Q, kp1, vp1, ps, w.ctx, M, N, w.Cp, (long long)RP * D, RP, 0, rt, s_k, c0, c1, act};
         a1 = {w.Q + img1, w.KP, w.VP, ps, ctx1, N, M, w.Cp, (long long)RP * D, RP, B * M, rt, s_k, c1, c0, act};
+        if (q_planes) {  // the queries are the qk planes (the key planes of the other direction)
+          a0.q = w.KP;
+          a1.q = kp1;
+        }
       }
-      LG_HIP(attn(a0, a1, blk == 0 ? 0.125f : 1.0f, blk == 1));
+      LG_HIP(attn(a0, a1, blk == 0 ? 0.125f : 1.0f, blk == 1, q_planes));
       if (prec == PREC_H3) {
         // out projection (skipped when folded into ffn.0 at load time: ffn.0 then reads ctx)
         // the context planes carry the value planes' exponent (attention.hip)

@@ -463,7 +463,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   // with the source chunk that the swizzle puts there (rows past Nk repeat row Nk-1)
   const uint32_t ks_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)Ks);
   const uint32_t vs_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)Vs);
-  auto issue = [&](int t0, int buf) {
+  auto issue = [&](int t0, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
     const int c = isv ? cs ^ (((r >> 1) & 3) << 1) : cs ^ ((r >> 1) & 7);
     voff_full[i] = (uint32_t)(r * kHeadDim + c * 8) * 2u;
   }
-  auto issue_full = [&](int t0, int buf) {
+  auto issue_full = [&](int t0, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   // next tile are issued there, in the step's VALU-only stretch, where a piece costs a fraction of
   // its issue price among the score MFMAs (MI355X_MICROARCH.md, LDS-DMA piece issue cost)
   // nmode: 0 none, 1 issue_full(nt0, nbuf), 2 issue(nt0, nbuf) -- the next tile's staging
-  auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0, int nmode, int nt0, int nbuf) {
+  auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0, int nmode, int nt0, int nbuf) __attribute__((always_inline)) {
     const int off = OFFc;
     constexpr bool MASK = decltype(MASKc)::value;
     constexpr bool EXACT = decltype(EXc)::value;
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
   // half-swap swizzle (chunk cs of row r at cs ^ 4 ((r >> 1) & 1))
   const uint32_t ks_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)Ks);
   const uint32_t vs_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)Vs);
-  auto issue = [&](int t0, int buf) {
+  auto issue = [&](int t0, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;
@@ -961,7 +961,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
     const int c = isv ? cs ^ (((r >> 1) & 1) << 2) : cs ^ ((r >> 1) & 7);
     voff_full[i] = (uint32_t)(r * kHeadDim + c * 8) * 2u;
   }
-  auto issue_full = [&](int t0, int buf) {
+  auto issue_full = [&](int t0, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;
@@ -991,7 +991,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
   float thr = -INFINITY;  // raise test (lmax - m_use) c > 3 as one compare, kept with m_use
   const float inv3c = 3.f / c_lane;
 
-  auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0) {
+  auto body = [&](auto OFFc, auto MASKc, auto EXc, int t0) __attribute__((always_inline)) {
     const int off = OFFc;
     constexpr bool MASK = decltype(MASKc)::value;
     constexpr bool EXACT = decltype(EXc)::value;

@@ -258,7 +258,8 @@ __global__ __launch_bounds__(64 * WAVES) void attention_x6_kernel(AttnSet s0, At
 
 // ----------------------------------------------------------------------------------------
 // fp16x3 attention (PREC_H3, common.h): the bf16x6 tiling above with half the MFMAs.
-//  * K and V arrive as two fp16 planes (h, l*2^11) from the QKV GEMM epilogue.
+//  * K arrives as two fp16 planes (h, l*2^11), V as (h, l) (split2h_v, two-sided range exponent)
+//    from the QKV GEMM epilogue.
 //  * Each query row is scaled by 2^e (per lane: the query sits on the lane) so that
 //    max|q 2^e| lies in [8, 16); its pieces (h*2^11, l, h) stay in registers.  The S^T
 //    accumulator then holds 2^(11+e) q.k, and the per-lane factor scale*log2(e)*2^-(11+e)
@@ -628,20 +629,20 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
     for (int p = 0; p < NKT / 2; ++p)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        f16x8 ph, phs, pl;
+        // P pieces at scale 2^11: phs = fp16(e), pl = fp16(e - phs); the value planes' low piece is
+        // unscaled (split2h_v), so v_h phs + v_h pl + v_l phs = 2^11 (v_h p_h + v_h p_l + v_l p_h)
+        f16x8 phs, pl;
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
           const float e0 = sc[2 * p + (j >> 2)][qt][j & 3];
           const float e1 = sc[2 * p + (j >> 2)][qt][(j & 3) + 1];
           const f16x2 hs = {(_Float16)e0, (_Float16)e1};
-          const f16x2 h = hs * (f16x2){(_Float16)(1.f / kLoScale), (_Float16)(1.f / kLoScale)};
           const f16x2 lo = lo_pair(e0, e1, hs);
           phs[j] = hs[0]; phs[j + 1] = hs[1];
-          ph[j] = h[0]; ph[j + 1] = h[1];
           pl[j] = lo[0]; pl[j + 1] = lo[1];
         }
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt][qt] = mfma_h3_16(vf[p][dt][0], vf[p][dt][1], phs, pl, ph, o[dt][qt]);
+        for (int dt = 0; dt < 4; ++dt) o[dt][qt] = mfma_h3_16(vf[p][dt][0], vf[p][dt][1], phs, pl, phs, o[dt][qt]);
       }
   };
 
@@ -1084,19 +1085,17 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        f16x8 ph, phs, pl;
+        f16x8 phs, pl;  // as in attention_h3g_kernel: unscaled value low piece, no p_h copy
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
           const float e0 = sc[u][8 * ss + j], e1 = sc[u][8 * ss + j + 1];
           const f16x2 hs = {(_Float16)e0, (_Float16)e1};
-          const f16x2 h = hs * (f16x2){(_Float16)(1.f / kLoScale), (_Float16)(1.f / kLoScale)};
           const f16x2 lo = lo_pair(e0, e1, hs);
           phs[j] = hs[0]; phs[j + 1] = hs[1];
-          ph[j] = h[0]; ph[j + 1] = h[1];
           pl[j] = lo[0]; pl[j + 1] = lo[1];
         }
-        o0 = mfma_h3(vf[u][ss][0][0], vf[u][ss][0][1], phs, pl, ph, o0);
-        o1 = mfma_h3(vf[u][ss][1][0], vf[u][ss][1][1], phs, pl, ph, o1);
+        o0 = mfma_h3(vf[u][ss][0][0], vf[u][ss][0][1], phs, pl, phs, o0);
+        o1 = mfma_h3(vf[u][ss][1][0], vf[u][ss][1][1], phs, pl, phs, o1);
       }
   };
 

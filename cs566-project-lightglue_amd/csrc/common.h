@@ -170,6 +170,14 @@ __device__ __forceinline__ void split2h(float x, _Float16& h, _Float16& l) {
   h = (_Float16)x;
   l = (_Float16)((x - (float)h) * kLoScale);  // x - h is exact
 }
+// value planes (PREC_H3 V): the low piece at its own scale, x = h + l.  Small residuals become
+// fp16 subnormals (absolute error <= 2^-25 in plane units); the value planes' range exponent is
+// two-sided (kRangeTwoSided), so a plane's largest values sit near 2^15 and that error stays
+// ~2^-40 of them
+__device__ __forceinline__ void split2h_v(float x, _Float16& h, _Float16& l) {
+  h = (_Float16)x;
+  l = (_Float16)(x - (float)h);
+}
 
 __device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -232,7 +240,14 @@ __device__ __forceinline__ int range_exponent(const RO& r) {
   if (r.in0 >= 0) b += r.g0 * range_max(r.tab, r.in0);
   if (r.in1 >= 0) b += r.g1 * range_max(r.tab, r.in1);
   const float lim = ldexpf(kRangeLimit, -r.lshift);
-  if (!(b > lim) || !(b <= 3.0e38f)) return 0;  // in range, or non-finite data
+  if (!(b <= 3.0e38f)) return 0;  // non-finite data
+  if (r.track & 2) {  // kernels.h kRangeTwoSided
+    if (!(b > 0.f)) return 0;
+    int E;
+    (void)frexpf(b / lim, &E);  // 2^(E-1) < b / lim <= 2^E: the bound lands in (lim / 2, lim]
+    return max(E, -64);
+  }
+  if (!(b > lim)) return 0;  // in range
   int E;
   (void)frexpf(b / lim, &E);  // b / lim = m 2^E, m in [0.5, 1)  ->  2^E >= it
   return E;
@@ -248,7 +263,7 @@ __device__ __forceinline__ int range_slot_exp(const unsigned* tab, int slot) {
 template <class RO>
 __device__ __forceinline__ void range_commit_lds(const RO& r, float lane_max, int e, float* red, int nwaves = -1) {
   if (!r.tab) return;
-  if (!r.track) {  // E only: no reduction, no barrier (E != 0 is rare)
+  if (!(r.track & 1)) {  // kernels.h kRangeTrack clear: E only, no reduction, no barrier
     if (e != 0 && (threadIdx.x & 63) == 0) r.tab[r.out * kRangeStride + kRangeShards] = (unsigned)e;
     return;
   }

@@ -487,7 +487,7 @@ hipError_t remap_seg(const int64_t* m0c, const int64_t* m1c, const float* s0c, c
 // ----------------------------------------------------------------------------------------
 // Kernel-check helpers (lg_attention): fp32 -> operand planes, plane image -> fp32 rows.
 // ----------------------------------------------------------------------------------------
-__global__ void split_planes_kernel(const float* x, size_t n, void* planes, int prec, RangeOut ro) {
+__global__ void split_planes_kernel(const float* x, size_t n, void* planes, int prec, RangeOut ro, bool values) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int eo = prec == PREC_H3 ? range_exponent(ro) : 0;
   float wmax = 0.f;
@@ -495,7 +495,8 @@ __global__ void split_planes_kernel(const float* x, size_t n, void* planes, int 
     const float v = x[i];
     if (prec == PREC_H3) {
       _Float16 h, l;
-      split2h(ldexpf(v, -eo), h, l);
+      if (values) split2h_v(ldexpf(v, -eo), h, l);  // value planes (kernels.h HeadLayout)
+      else split2h(ldexpf(v, -eo), h, l);
       wmax = fabsf(v);
       static_cast<_Float16*>(planes)[i] = h;
       static_cast<_Float16*>(planes)[n + i] = l;
@@ -510,9 +511,9 @@ __global__ void split_planes_kernel(const float* x, size_t n, void* planes, int 
   if (prec == PREC_H3) range_commit(ro, wmax, eo);
 }
 
-hipError_t split_planes(const float* x, size_t n, void* planes, int prec, const RangeOut& ro, hipStream_t st) {
+hipError_t split_planes(const float* x, size_t n, void* planes, int prec, const RangeOut& ro, hipStream_t st, bool values) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, planes, prec, ro);
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, planes, prec, ro, values);
   return hipGetLastError();
 }
 

@@ -762,7 +762,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
           for (int e = 0; e < 8; ++e) {
             wmax = fmaxf(wmax, fabsf(x[e]));
             _Float16 a, c;
-            split2h(x[e] * so, a, c);
+            if (to_vp) split2h_v(x[e] * so, a, c);  // value planes: unscaled low piece (kernels.h HeadLayout)
+            else split2h(x[e] * so, a, c);
             h[e] = a;
             l[e] = c;
           }

@@ -72,10 +72,13 @@ struct RangeOut {
   int in0, in1;
   float g0, g1, add;
   int out;
-  int track;          // 1: record M[out] (only the residual stream's images need it; E is always kept)
+  int track;          // kRangeTrack: record M[out] (only the residual stream's images need it; E is
+                      // always kept); kRangeTwoSided: E may be negative -- small tensors are scaled
+                      // UP to the limit too (value planes, whose low piece is stored unscaled)
   int lshift;         // the bound is held to 2^(15 - lshift): 11 for images used as the "y" operand
                       // of an fp16x3 product (|y| <= 16, so y_h * 2^11 stays finite)
 };
+constexpr int kRangeTrack = 1, kRangeTwoSided = 2;
 inline RangeOut range_none() { return RangeOut{nullptr, -1, -1, 0.f, 0.f, 0.f, 0, 0}; }
 
 // Head-major destinations [set][b][h][n][64] for the QKV epilogues; set 0 = image 0 (B*M rows),
@@ -83,7 +86,8 @@ inline RangeOut range_none() { return RangeOut{nullptr, -1, -1, 0.f, 0.f, 0.f, 0
 //   q   fp32 queries (self) / qk (cross)
 //   kp  keys as operand planes (plane p at kp + p*pstride): k (self) / qk (cross)
 //       PREC_X6: three bf16 planes (h, m, l);  PREC_H3: two fp16 planes (h, l * 2^11)
-//   vp  values, same planes
+//   vp  values, same planes; PREC_H3: (h, l) with the low piece NOT scaled (split2h_v: the
+//       attention's P V product then needs no unscaled copy of P's high piece)
 struct HeadLayout {
   float* q;
   void* kp;
@@ -275,7 +279,9 @@ hipError_t split_weight_h3(const float* src, int rows, int K, float scale, _Floa
 
 // lg_attention (kernel-level checks): fp32 [n] -> operand planes of `prec` (plane stride n; PREC_H3
 // range-scaled by ro), and a plane image (K columns) -> fp32 rows, times 2^E[slot] of tab.
-hipError_t split_planes(const float* x, size_t n, void* planes, int prec, const RangeOut& ro, hipStream_t st);
+// values: PREC_H3 value planes (low piece unscaled, HeadLayout.vp)
+hipError_t split_planes(const float* x, size_t n, void* planes, int prec, const RangeOut& ro, hipStream_t st,
+                        bool values = false);
 hipError_t image_to_rows(const _Float16* planes, long long ps, int rows_pad, int K, float* out, int rows,
                          const unsigned* tab, int slot, hipStream_t st);
 // Load-time weight statistics for the range bounds: out[0] = max over rows of sum_k |W[r,k]|,

@@ -853,7 +853,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, bw.Wqkv); g.bias = Wb + bw.bqkv;
         g.rtab = rt; g.a0_slot = s_x; g.rm = live;
         g.ro = ro(s_x, gn.gK, -1, 0.f, gn.bK, s_k, 1);  // M[k]: the attention's exact-softmax test
-        g.ro_v = ro(s_x, gn.gV, -1, 0.f, gn.bV, s_v, h->fold ? 0 : 1);
+        g.ro_v = ro(s_x, gn.gV, -1, 0.f, gn.bV, s_v, kRangeTwoSided | (h->fold ? 0 : kRangeTrack));
         g.R = R; g.Nout = blk == 0 ? 3 * D : 2 * D; g.hl = hl;
         LG_HIP(gemmh(g, epi_qkv));
       } else {
@@ -1347,7 +1347,8 @@ int lg_attention(const float* q, const float* k, const float* v, int32_t B, int3
     LG_HIP(lg::range_absmax(v, n, rtab, 1, st));
   }
   LG_HIP(lg::split_planes(k, n, kp, prec, lg::RangeOut{h3 ? rtab : nullptr, 0, -1, 1.f, 0.f, 0.f, 2, 1}, st));
-  LG_HIP(lg::split_planes(v, n, vp, prec, lg::RangeOut{h3 ? rtab : nullptr, 1, -1, 1.f, 0.f, 0.f, 3, 1}, st));
+  LG_HIP(lg::split_planes(v, n, vp, prec, lg::RangeOut{h3 ? rtab : nullptr, 1, -1, 1.f, 0.f, 0.f, 3, lg::kRangeTrack | lg::kRangeTwoSided}, st,
+                          true));
   // one set; the second set is empty (Nq = 0: its workgroups exit at once)
   const lg::AttnSet s0{q, kp, vp, (long long)n, ctx, Nq, Nk, img, (long long)rp * 256, rp, 0, h3 ? rtab : nullptr, 2};
   lg::AttnSet s1 = s0;

@@ -524,7 +524,7 @@ int sg_forward(sg_handle_t* h, const sg_inputs_t* in, sg_outputs_t* out, void* w
       g.A0 = image(w.Xp, D); g.K0 = D; g.K = D; wplanes(g, ly.qkv);
       g.rtab = rt; g.a0_slot = s_x; g.a1_slot = -1;
       g.ro = ro(s_x, ly.gK, -1, 0.f, ly.bK, s_k, 1);
-      g.ro_v = ro(s_x, ly.gV, -1, 0.f, ly.bV, s_v, 1);  // M[v] bounds the context (mlp.0's input)
+      g.ro_v = ro(s_x, ly.gV, -1, 0.f, ly.bV, s_v, kRangeTrack | kRangeTwoSided);  // M[v] bounds the context (mlp.0's input)
       g.R = R; g.Nout = 3 * D; g.hl = hl;
       SG_HIP(gemm_h3(g, EPI_QKV_ROT, st));
     }

@@ -420,45 +420,71 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   f16x8 qh[2][2], qhs[2][2], ql[2][2];
   float c_lane[2];
   const int ek = range_slot_exp(S.rtab, S.k_slot);  // key planes hold k * 2^-ek (RangeOut)
-  // |scale q.k log2 e| <= 64 max|q_row| max|k| scale log2 e; beyond 2^21 the fused exponent
-  // argument fma(s, c, -(m c - 11)) loses its absolute accuracy (m c is rounded to fp32), so such
-  // waves form (s - m) first -- one more VALU per score, only for extreme data
+  // Query pieces, two forms (mfma_h3_16 computes x_l yh + x_h yl + x_h yhs, the key planes being
+  // x_h = fp16(k 2^-ek) and x_l = its residual * 2^11):
+  //  * common form: y = q scale log2(e) 2^ek split UNSCALED -- yhs = y_h, yl = fp16(y - y_h),
+  //    yh = y_h 2^-11 -- so the score accumulator IS the exponent argument in log2 units; each
+  //    tile's first MFMA takes C = 11 - m (m the query's softmax reference), so e = p 2^11 =
+  //    exp2(accumulator) with no VALU between the MFMA and the exponential.  Small components'
+  //    low pieces go subnormal: absolute error <= 2^-25 per component in log2-logit units per unit
+  //    of k, below the fp32 reference's own rounding of logits of order 10.
+  //  * exact form (extreme or tiny data, wave-uniform): |scale q.k log2 e| <= 64 max|q_row| max|k|
+  //    scale log2 e beyond 2^21, or a row's max|y| outside [2^-4, 2^14]: each row scaled by 2^ex into [8, 16), pieces
+  //    (h 2^11, l 2^11, h), the accumulator holds 2^(11+ex) q.k, and the exponent argument is
+  //    formed as (s - m) c + 11 in VALU with the per-lane factor c.
   const float kmax = S.rtab ? range_max(S.rtab, S.k_slot) : INFINITY;
+  const float ysc = ldexpf(scale_log2e, ek);
   bool big = false;
+  f32x4 xq[2][2][2];
+  int exq[2];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int qrow = min(q_blk + wave * 32 + qt * 16 + r16, Nq - 1);
     const size_t qr = (size_t)qrow * kHeadDim + 8 * g;
-    f32x4 x[2][2];
     float mx = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      load_q8<QP>(Q, S.pstride, qr + 32 * ks, qsc, x[ks][0], x[ks][1]);
+      load_q8<QP>(Q, S.pstride, qr + 32 * ks, qsc, xq[qt][ks][0], xq[qt][ks][1]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(x[ks][0][e]), fabsf(x[ks][1][e])));
+      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(xq[qt][ks][0][e]), fabsf(xq[qt][ks][1][e])));
     }
     mx = max_x16_32(mx);
-    big |= !(64.f * mx * kmax * scale_log2e <= 2097152.f);
+    // common form only for rows whose largest y is in [2^-4, 2^14]: the subnormal low pieces'
+    // error (<= 2^-25 sum|x|) then stays under 2^-21 of the row's logit scale (max|y| sum|x|)
+    big |= !(64.f * mx * kmax * scale_log2e <= 2097152.f) || !(mx * ysc <= 16384.f) || !(mx * ysc >= 0.0625f);
     int ex = 0;
     if (mx > 0.f && mx <= 3.0e38f) {
       int E;
       (void)frexpf(mx, &E);
       ex = min(max(4 - E, -100), 100);
     }
-    c_lane[qt] = ldexpf(scale_log2e, ek - (11 + ex));
+    exq[qt] = ex;
+  }
+  const bool exact = __builtin_amdgcn_readfirstlane((int)(__ballot(big) != 0ull)) != 0;  // wave-uniform
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    c_lane[qt] = exact ? ldexpf(scale_log2e, ek - (11 + exq[qt])) : 1.f;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
+        const float xv = xq[qt][ks][e >> 2][e & 3];
         _Float16 h, l;
-        split2h(ldexpf(x[ks][e >> 2][e & 3], ex), h, l);
-        qh[qt][ks][e] = h;
-        ql[qt][ks][e] = l;
-        qhs[qt][ks][e] = h * (_Float16)kLoScale;
+        if (exact) {
+          split2h(ldexpf(xv, exq[qt]), h, l);
+          qh[qt][ks][e] = h;
+          ql[qt][ks][e] = l;
+          qhs[qt][ks][e] = h * (_Float16)kLoScale;
+        } else {
+          const float y = xv * ysc;
+          h = (_Float16)y;
+          l = (_Float16)(y - (float)h);  // exact difference, rounded (subnormal when tiny)
+          qhs[qt][ks][e] = h;
+          ql[qt][ks][e] = l;
+          qh[qt][ks][e] = (_Float16)((float)h * (1.f / kLoScale));
+        }
       }
   }
-
-  const bool exact = __builtin_amdgcn_readfirstlane((int)(__ballot(big) != 0ull)) != 0;  // wave-uniform
   // LDS-DMA staging of one LDS tile (keys t0 .. t0+LT-1) into buffer buf: piece q (wave-uniform)
   // = 8 rows of one plane of K (q < PIECES/2) or V; lane i fills LDS slot (row i>>3, chunk i&7)
   // with the source chunk that the swizzle puts there (rows past Nk repeat row Nk-1)
@@ -517,11 +543,17 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   f32x4 o[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt][0] = o[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_use[2] = {-INFINITY, -INFINITY};
+  // softmax reference per query: exact form in accumulator units (m_use = -inf forces the first
+  // raise); common form in log2 units, starting at 0 with the first step always re-referencing
+  float m_use[2] = {exact ? -INFINITY : 0.f, exact ? -INFINITY : 0.f};
   float l_run[2] = {0.f, 0.f};
-  // raise test (lmax - m_use) c > 3 as one compare against m_use + 3 / c, updated with m_use
+  // exact form: raise test (lmax - m_use) c > 3 as one compare against m_use + 3 / c
   float thr[2] = {-INFINITY, -INFINITY};
   const float inv3c[2] = {3.f / c_lane[0], 3.f / c_lane[1]};
+  // common form: C operand of each score tile's first MFMA, 11 - m_use (so the accumulator holds
+  // s - m + 11 = log2(p 2^11)); raise when it exceeds 14 (s - m > 3, p > 8)
+  f32x4 cm[2] = {f32x4{11.f, 11.f, 11.f, 11.f}, f32x4{11.f, 11.f, 11.f, 11.f}};
+  bool first = true;  // wave-uniform: the first 64-key step sets every query's reference
 
   // one 64-key softmax step over LDS rows off .. off+63 of the current buffer (off: element
   // offset buf*2*PL + sub*KT*kHeadDim, a compile-time constant in the main loop)
@@ -552,7 +584,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        f32x4 a = EXACT ? f32x4{0.f, 0.f, 0.f, 0.f} : cm[qt];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) a = mfma_h3_16(kf[kt][ks][0], kf[kt][ks][1], qhs[qt][ks], ql[qt][ks], qh[qt][ks], a);
         sc[kt][qt] = a;
@@ -586,28 +618,52 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       const float lmax = fmaxf(max3f(m0, m1, m2), max3f(m3, m4, sc[3][qt][3]));
       // the lane-local max decides whether any query can need a raise; only then are the four
       // lanes of each query reduced (the raise itself is per query, exactly as in h3/h3m)
-      if (__ballot(lmax > thr[qt]) != 0ull) {
-        const float tmax = max_x16_32(lmax);
-        const bool need = (tmax - m_use[qt]) * c_lane[qt] > 3.f;
-        const float m_new = need ? tmax : m_use[qt];
-        const float alpha = __builtin_amdgcn_exp2f((m_use[qt] - m_new) * c_lane[qt]);
-        m_use[qt] = m_new;
-        thr[qt] = m_new + inv3c[qt];
-        l_run[qt] *= alpha;
+      if constexpr (EXACT) {
+        if (__ballot(lmax > thr[qt]) != 0ull) {
+          const float tmax = max_x16_32(lmax);
+          const bool need = (tmax - m_use[qt]) * c_lane[qt] > 3.f;
+          const float m_new = need ? tmax : m_use[qt];
+          const float alpha = __builtin_amdgcn_exp2f((m_use[qt] - m_new) * c_lane[qt]);
+          m_use[qt] = m_new;
+          thr[qt] = m_new + inv3c[qt];
+          l_run[qt] *= alpha;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
+          for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[dt][qt][r] *= alpha;
+            for (int r = 0; r < 4; ++r) o[dt][qt][r] *= alpha;
+        }
+      } else {
+        // accumulators hold s - m + 11: re-reference a query whose tile max passes 14 (and every
+        // query on the first step) by d = tmax - 11, shifting this step's accumulators, C and the
+        // running sums (exp2(-d) <= 1/8; nothing to rescale on the first step)
+        if (first || __ballot(lmax > 14.f) != 0ull) {
+          const float tmax = max_x16_32(lmax);
+          const float d = (first || tmax > 14.f) && tmax > -INFINITY ? tmax - 11.f : 0.f;
+          m_use[qt] += d;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cm[qt][r] -= d;
+#pragma unroll
+          for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sc[kt][qt][r] -= d;
+          if (!first) {
+            const float alpha = __builtin_amdgcn_exp2f(-d);
+            l_run[qt] *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[dt][qt][r] *= alpha;
+          }
+        }
       }
       // e = p 2^11
       float ps4[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (!EXACT) {
-        const float mb = fmaf(m_use[qt], c_lane[qt], -11.f);
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][qt][r], c_lane[qt], -mb));
+            const float e = __builtin_amdgcn_exp2f(sc[kt][qt][r]);
             sc[kt][qt][r] = e;
             ps4[r] += e;
           }
@@ -623,6 +679,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
       }
       l_run[qt] += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
     }
+    if constexpr (!EXACT) first = false;
     if (nmode == 1) issue_full(__builtin_amdgcn_readfirstlane(nt0), __builtin_amdgcn_readfirstlane(nbuf));
     else if (nmode == 2) issue(__builtin_amdgcn_readfirstlane(nt0), __builtin_amdgcn_readfirstlane(nbuf));
 #pragma unroll

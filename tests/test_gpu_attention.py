@@ -7,6 +7,8 @@ drive the kernel's own corner paths directly:
     O / l rescale) on every 64-key tile; decreasing order never raises after the first tile;
   * large logits (|scale q.k| up to ~90) where a stale reference would overflow exp;
   * ragged key counts (last tile partly masked, a single key) and query blocks;
+  * query rows at the smallest scale the h3g common (log2-unit, accumulator-seeded) form takes, and
+    waves mixing such rows with tiny ones (exact form);
   * both operand formats (fp16x3 "auto", bf16x6).
 Bar: |ctx - ref64| <= 2e-6 + 2^-21 * L * max|v|, L = max_{q,k} scale * sum_d |q_d k_d| -- twice the
 fp16x3 piece-truncation bound (2^-22 relative) carried by the largest logit; fp32
@@ -81,11 +83,23 @@ def case(name):
         return randn(B, H, 70, 64, seed=10), randn(B, H, 1, 64, seed=11), randn(B, H, 1, 64, seed=12), 0.125
     if name == "one_key_in_last_tile":
         return randn(B, H, 257, 64, seed=13), randn(B, H, 65, 64, seed=14), randn(B, H, 65, 64, seed=15), 0.125
+    if name == "small_queries":
+        # every row's max |q scale log2 e| just above 2^-4, the smallest the h3g common form takes
+        # (its unscaled low pieces are mostly fp16 subnormals there)
+        q = randn(B, H, 256, 64, seed=16)
+        q = q / q.abs().amax(-1, keepdim=True) * (0.07 / (0.125 * 1.4426950408889634))
+        return q, randn(B, H, 300, 64, seed=17), randn(B, H, 300, 64, seed=18), 0.125
+    if name == "mixed_row_scales":
+        # row scales from 1e-3 to 8 interleaved, so waves mix rows on both sides of the 2^-4
+        # threshold (such a wave runs the exact form)
+        q = randn(B, H, 256, 64, seed=19)
+        f = torch.logspace(-3, np.log10(8.0), 256)[torch.randperm(256, generator=torch.Generator().manual_seed(20))]
+        return q * f[None, None, :, None], randn(B, H, 320, 64, seed=21), randn(B, H, 320, 64, seed=22), 0.125
     raise KeyError(name)
 
 
 CASES = ["random_ragged", "increasing_scores", "decreasing_scores", "large_logits", "single_key",
-         "one_key_in_last_tile"]
+         "one_key_in_last_tile", "small_queries", "mixed_row_scales"]
 
 
 @pytest.mark.parametrize("kernel", ["h3m", "h3g"])

@@ -344,5 +344,29 @@ __device__ __forceinline__ float gelu_erf(float y) {
   const float h = 0.5f * t * __builtin_amdgcn_exp2f((p - z * z) * 1.4426950408889634f);
   return y >= 0.f ? fmaf(-y, h, y) : y * h;
 }
+// the same for two values with packed fp32 arithmetic (v_pk_fma_f32 / v_pk_mul_f32: two lanes per
+// issue, each lane the scalar form's operation sequence, so the results are bit-identical); for
+// epilogues with no MFMA beside them (MI355X_MICROARCH.md: packed fp32 only loses beside MFMAs)
+typedef float f32x2_ __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_ gelu_erf2(f32x2_ y) {
+  const f32x2_ z = __builtin_elementwise_abs(y) * 0.70710678118654752f;
+  const f32x2_ u = __builtin_elementwise_fma(f32x2_{0.5f, 0.5f}, z, f32x2_{1.f, 1.f});
+  const f32x2_ t = {__builtin_amdgcn_rcpf(u.x), __builtin_amdgcn_rcpf(u.y)};
+  auto fm = [&](f32x2_ p, float c) { return __builtin_elementwise_fma(p, t, f32x2_{c, c}); };
+  f32x2_ p = {0.17087277f, 0.17087277f};
+  p = fm(p, -0.82215223f);
+  p = fm(p, 1.48851587f);
+  p = fm(p, -1.13520398f);
+  p = fm(p, 0.27886807f);
+  p = fm(p, -0.18628806f);
+  p = fm(p, 0.09678418f);
+  p = fm(p, 0.37409196f);
+  p = fm(p, 1.00002368f);
+  p = fm(p, -1.26551223f);
+  const f32x2_ w = (p - z * z) * 1.4426950408889634f;
+  const f32x2_ h = 0.5f * t * f32x2_{__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)};
+  const f32x2_ pos = __builtin_elementwise_fma(-y, h, y), neg = y * h;
+  return f32x2_{y.x >= 0.f ? pos.x : neg.x, y.y >= 0.f ? pos.y : neg.y};
+}
 
 }  // namespace lg

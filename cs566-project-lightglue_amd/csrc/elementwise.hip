@@ -110,8 +110,9 @@ __global__ __launch_bounds__(256) void ln_gelu_kernel(float* x, const float* g, 
     for (int i = 0; i < 4; ++i) {
       float y0 = (v0[i] - mean) * rstd * g0[i] + b0[i];
       float y1 = (v1[i] - mean) * rstd * g1[i] + b1[i];
-      v0[i] = gelu_erf(y0);
-      v1[i] = gelu_erf(y1);
+      const f32x2_ z = gelu_erf2(f32x2_{y0, y1});  // packed: the same values as gelu_erf
+      v0[i] = z.x;
+      v1[i] = z.y;
     }
     if (!planes) {
       *reinterpret_cast<f32x4*>(xr + lane * 4) = v0;

@@ -464,16 +464,36 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       constexpr int jh = 0;  // WN == 64: one 64-column pass per row pass
-      visit(i, [&](int rr, int c, float v) {
-        const int lr = wm0 + i * 32 + rr;
-        const float y = (v - mean_s[lr]) * rstd_s[lr] * gj[c / LC] + bj[c / LC];
+      if constexpr (kMF16 && !(LG_LN_PROBE & 1)) {
+        // rows 4 (lane >> 4) + r, r = 0..3, of each 16-row block, column 16 j + (lane & 15): the
+        // normalisation and GELU run on row pairs (r, r + 1) with packed fp32 arithmetic
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int rp = 0; rp < 4; rp += 2) {
+            const int rr0 = a * 16 + (lane >> 4) * 4 + rp, lr0 = wm0 + i * 32 + rr0;
+            const f32x2_ m2 = {mean_s[lr0], mean_s[lr0 + 1]}, s2 = {rstd_s[lr0], rstd_s[lr0 + 1]};
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+              const int c = j * 16 + (lane & 15);
+              const f32x2_ v2 = {acc[2 * i + a][j][rp], acc[2 * i + a][j][rp + 1]};
+              const f32x2_ z2 = gelu_erf2((v2 - m2) * s2 * gj[j] + bj[j]);
+              ep[rr0 * 64 + (c ^ ((rr0 & 1) << 2))] = z2.x;
+              ep[(rr0 + 1) * 64 + (c ^ (((rr0 + 1) & 1) << 2))] = z2.y;
+            }
+          }
+      } else {
+        visit(i, [&](int rr, int c, float v) {
+          const int lr = wm0 + i * 32 + rr;
+          const float y = (v - mean_s[lr]) * rstd_s[lr] * gj[c / LC] + bj[c / LC];
 #if LG_LN_PROBE & 1
-        ep[rr * 64 + (c ^ ((rr & 1) << 2))] = y;
+          ep[rr * 64 + (c ^ ((rr & 1) << 2))] = y;
 #else
-        ep[rr * 64 + (c ^ ((rr & 1) << 2))] = gelu_erf(y);
+          ep[rr * 64 + (c ^ ((rr & 1) << 2))] = gelu_erf(y);
 #endif
-        return v;
-      });
+          return v;
+        });
+      }
       {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll

@@ -170,6 +170,28 @@ __device__ __forceinline__ void split2h(float x, _Float16& h, _Float16& l) {
   h = (_Float16)x;
   l = (_Float16)((x - (float)h) * kLoScale);  // x - h is exact
 }
+// split2h / split2h_v of 8 values v[e] * so, two per step: h = cvt_pk(y0, y1), and the low piece
+// as ONE v_fma_mix per value -- l = fp16(h * (-lsc) + v * (so * lsc)), lsc = 2^11 (split2h) or 1
+// (split2h_v): y * lsc - h * lsc is exact in fp32 before its single rounding, so the pieces equal
+// split2h's (the compiler's form of split2h takes 7 VALU per pair, this one 5)
+template <bool V = false>
+__device__ __forceinline__ void split2h_x8(const float (&v)[8], float so, f16x8& h, f16x8& l) {
+  typedef _Float16 f16x2_s __attribute__((ext_vector_type(2)));
+  const float lsc = V ? 1.f : kLoScale, nl = -lsc, sl = so * lsc;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float y0 = v[2 * p] * so, y1 = v[2 * p + 1] * so;
+    const f16x2_s hp = {(_Float16)y0, (_Float16)y1};
+    unsigned lo;
+    asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hp), "s"(nl), "v"(v[2 * p] * sl));
+    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hp), "s"(nl), "v"(v[2 * p + 1] * sl));
+    const f16x2_s lp = __builtin_bit_cast(f16x2_s, lo);
+    h[2 * p] = hp[0];
+    h[2 * p + 1] = hp[1];
+    l[2 * p] = lp[0];
+    l[2 * p + 1] = lp[1];
+  }
+}
 // value planes (PREC_H3 V): the low piece at its own scale, x = h + l.  Small residuals become
 // fp16 subnormals (absolute error <= 2^-25 in plane units); the value planes' range exponent is
 // two-sided (kRangeTwoSided), so a plane's largest values sit near 2^15 and that error stays

@@ -506,15 +506,13 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rr * 64 + ((cq + 4) ^ sw));
           if (!(LG_LN_PROBE & 2) && row < g.R && row_live(g.rm, row)) {
             f16x8 h, l;
+            float vv[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float v = e < 4 ? v0[e] : v1[e - 4];
-              wmax = fmaxf(wmax, fabsf(v));
-              _Float16 a, c;
-              split2h(v * so, a, c);
-              h[e] = a;
-              l[e] = c;
+              vv[e] = e < 4 ? v0[e] : v1[e - 4];
+              wmax = fmaxf(wmax, fabsf(vv[e]));
             }
+            split2h_x8(vv, so, h, l);
             const size_t off = plane_off(row, n0 + wn0 + jh * 64 + cq, g.yrows_pad);
             st_stream(reinterpret_cast<f16x8*>(g.Yp + off), h);
             st_stream(reinterpret_cast<f16x8*>(g.Yp + g.yps + off), l);
@@ -637,15 +635,13 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
               }
             }
             f16x8 h, l;
+            float vv[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float v = e < 4 ? v0[e] : v1[e - 4];
-              wmax = fmaxf(wmax, fabsf(v));
-              _Float16 a, c;
-              split2h(v * so, a, c);
-              h[e] = a;
-              l[e] = c;
+              vv[e] = e < 4 ? v0[e] : v1[e - 4];
+              wmax = fmaxf(wmax, fabsf(vv[e]));
             }
+            split2h_x8(vv, so, h, l);
             const size_t off = plane_off(row, n0 + wn0 + cq, g.yrows_pad);
             st_stream(reinterpret_cast<f16x8*>(g.Yp + off), h);
             st_stream(reinterpret_cast<f16x8*>(g.Yp + g.yps + off), l);
@@ -779,14 +775,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
           _Float16* base = static_cast<_Float16*>(to_kp ? hl.kp : hl.vp);
           f16x8 h, l;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            wmax = fmaxf(wmax, fabsf(x[e]));
-            _Float16 a, c;
-            if (to_vp) split2h_v(x[e] * so, a, c);  // value planes: unscaled low piece (kernels.h HeadLayout)
-            else split2h(x[e] * so, a, c);
-            h[e] = a;
-            l[e] = c;
-          }
+          for (int e = 0; e < 8; ++e) wmax = fmaxf(wmax, fabsf(x[e]));
+          if (to_vp) split2h_x8<true>(x, so, h, l);  // value planes: unscaled low piece (kernels.h HeadLayout)
+          else split2h_x8(x, so, h, l);
           st_stream(reinterpret_cast<f16x8*>(base + off), h);
           st_stream(reinterpret_cast<f16x8*>(base + hl.pstride + off), l);
         }

@@ -656,8 +656,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
           }
         }
       }
-      // e = p 2^11
-      float ps4[4] = {0.f, 0.f, 0.f, 0.f};
+      // e = p 2^11; the partial sums start from the first sub-tile's values (0 + e costs an add)
+      float ps4[4];
       if constexpr (!EXACT) {
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt)
@@ -665,7 +665,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
           for (int r = 0; r < 4; ++r) {
             const float e = __builtin_amdgcn_exp2f(sc[kt][qt][r]);
             sc[kt][qt][r] = e;
-            ps4[r] += e;
+            ps4[r] = kt == 0 ? e : ps4[r] + e;
           }
       } else {
 #pragma unroll
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
           for (int r = 0; r < 4; ++r) {
             const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][qt][r] - m_use[qt], c_lane[qt], 11.f));
             sc[kt][qt][r] = e;
-            ps4[r] += e;
+            ps4[r] = kt == 0 ? e : ps4[r] + e;
           }
       }
       l_run[qt] += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
@@ -1116,7 +1116,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
       }
     }
     // e = p 2^11
-    float ps8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float ps8[8];
     if constexpr (!EXACT) {
       const float mb = fmaf(m_use, c_lane, -11.f);
 #pragma unroll
@@ -1125,7 +1125,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
         for (int r = 0; r < 16; ++r) {
           const float e = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c_lane, -mb));
           sc[u][r] = e;
-          ps8[r & 7] += e;
+          ps8[r & 7] = u == 0 && r < 8 ? e : ps8[r & 7] + e;
         }
     } else {
 #pragma unroll
@@ -1134,7 +1134,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3m_
         for (int r = 0; r < 16; ++r) {
           const float e = __builtin_amdgcn_exp2f(fmaf(sc[u][r] - m_use, c_lane, 11.f));
           sc[u][r] = e;
-          ps8[r & 7] += e;
+          ps8[r & 7] = u == 0 && r < 8 ? e : ps8[r & 7] + e;
         }
     }
     l_run += ((ps8[0] + ps8[1]) + (ps8[2] + ps8[3])) + ((ps8[4] + ps8[5]) + (ps8[6] + ps8[7]));

@@ -340,6 +340,11 @@ __device__ __forceinline__ f16x2 lo_pair(float e0, float e1, f16x2 hs) {
   return __builtin_bit_cast(f16x2, l);
 }
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+// the common form's score max tree: llvm.maximum (v_maximum3_f32 on gfx950) takes the MFMA results
+// as they are, where fmaxf's maxnum first quiets each operand it cannot prove canonical (a
+// v_max_f32 x, x); the two differ only on NaN, which the exponentials propagate either way
+__device__ __forceinline__ float max2m(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float max3m(float a, float b, float c) { return max2m(max2m(a, b), c); }
 // op over the 4 lanes l, l^16, l^32, l^48 through v_permlane{16,32}_swap (no LDS round trip)
 __device__ __forceinline__ float max_x16_32(float v) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -610,12 +615,22 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
           for (int r = 0; r < 4; ++r)
             if (t0 + 16 * kt + 4 * g + r >= Nk) sc[kt][qt][r] = -INFINITY;
       }
-      const float m0 = max3f(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
-      const float m1 = max3f(sc[0][qt][3], sc[1][qt][0], sc[1][qt][1]);
-      const float m2 = max3f(sc[1][qt][2], sc[1][qt][3], sc[2][qt][0]);
-      const float m3 = max3f(sc[2][qt][1], sc[2][qt][2], sc[2][qt][3]);
-      const float m4 = max3f(sc[3][qt][0], sc[3][qt][1], sc[3][qt][2]);
-      const float lmax = fmaxf(max3f(m0, m1, m2), max3f(m3, m4, sc[3][qt][3]));
+      float lmax;
+      if constexpr (EXACT) {
+        const float m0 = max3f(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
+        const float m1 = max3f(sc[0][qt][3], sc[1][qt][0], sc[1][qt][1]);
+        const float m2 = max3f(sc[1][qt][2], sc[1][qt][3], sc[2][qt][0]);
+        const float m3 = max3f(sc[2][qt][1], sc[2][qt][2], sc[2][qt][3]);
+        const float m4 = max3f(sc[3][qt][0], sc[3][qt][1], sc[3][qt][2]);
+        lmax = fmaxf(max3f(m0, m1, m2), max3f(m3, m4, sc[3][qt][3]));
+      } else {
+        const float m0 = max3m(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
+        const float m1 = max3m(sc[0][qt][3], sc[1][qt][0], sc[1][qt][1]);
+        const float m2 = max3m(sc[1][qt][2], sc[1][qt][3], sc[2][qt][0]);
+        const float m3 = max3m(sc[2][qt][1], sc[2][qt][2], sc[2][qt][3]);
+        const float m4 = max3m(sc[3][qt][0], sc[3][qt][1], sc[3][qt][2]);
+        lmax = max2m(max3m(m0, m1, m2), max3m(m3, m4, sc[3][qt][3]));
+      }
       // the lane-local max decides whether any query can need a raise; only then are the four
       // lanes of each query reduced (the raise itself is per query, exactly as in h3/h3m)
       if constexpr (EXACT) {

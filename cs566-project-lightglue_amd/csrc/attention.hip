@@ -49,6 +49,15 @@ __device__ __forceinline__ int xcd_chunk(int id, int n) {
 // cached stores win (three same-box pairs: 1312 vs 1301 pairs/s)
 #define LG_ATTN_CTX_NT 0
 #endif
+// common-form lazy softmax reference (log2 units of the score accumulator, e = 2^acc): a query is
+// re-referenced when a score tile's max passes LG_ATTN_RAISE, to put that max at LG_ATTN_REF
+// (e <= 2^LG_ATTN_RAISE < 65504 keeps every e an fp16 for the P split)
+#ifndef LG_ATTN_RAISE
+#define LG_ATTN_RAISE 14
+#endif
+#ifndef LG_ATTN_REF
+#define LG_ATTN_REF 11
+#endif
 #ifndef LG_ATTN_REVERSE
 #define LG_ATTN_REVERSE 1  // configs[2] three same-box pairs: 1326 vs 1321 pairs/s, attention -0.6 %
 #endif
@@ -556,7 +565,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
   float thr[2] = {-INFINITY, -INFINITY};
   const float inv3c[2] = {3.f / c_lane[0], 3.f / c_lane[1]};
   // common form: C operand of each score tile's first MFMA, 11 - m_use (so the accumulator holds
-  // s - m + 11 = log2(p 2^11)); raise when it exceeds 14 (s - m > 3, p > 8)
+  // s - m + 11 = log2(p 2^11)); raise when it exceeds LG_ATTN_RAISE, re-referencing the query so
+  // that its largest accumulator becomes LG_ATTN_REF
   f32x4 cm[2] = {f32x4{11.f, 11.f, 11.f, 11.f}, f32x4{11.f, 11.f, 11.f, 11.f}};
   bool first = true;  // wave-uniform: the first 64-key step sets every query's reference
 
@@ -648,12 +658,12 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void attention_h3g_
             for (int r = 0; r < 4; ++r) o[dt][qt][r] *= alpha;
         }
       } else {
-        // accumulators hold s - m + 11: re-reference a query whose tile max passes 14 (and every
-        // query on the first step) by d = tmax - 11, shifting this step's accumulators, C and the
-        // running sums (exp2(-d) <= 1/8; nothing to rescale on the first step)
-        if (first || __ballot(lmax > 14.f) != 0ull) {
+        // accumulators hold s - m + 11: re-reference a query whose tile max passes LG_ATTN_RAISE
+        // (and every query on the first step) by d = tmax - LG_ATTN_REF, shifting this step's
+        // accumulators, C and the running sums (nothing to rescale on the first step)
+        if (first || __ballot(lmax > (float)LG_ATTN_RAISE) != 0ull) {
           const float tmax = max_x16_32(lmax);
-          const float d = (first || tmax > 14.f) && tmax > -INFINITY ? tmax - 11.f : 0.f;
+          const float d = (first || tmax > (float)LG_ATTN_RAISE) && tmax > -INFINITY ? tmax - (float)LG_ATTN_REF : 0.f;
           m_use[qt] += d;
 #pragma unroll
           for (int r = 0; r < 4; ++r) cm[qt][r] -= d;

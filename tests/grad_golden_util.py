@@ -1,0 +1,70 @@
+"""Gradient golden fixtures (tests/golden/make_grad_golden.py): loading, input regeneration and the
+float64 oracle gradients (oracle/lightglue_train_ref.py) they pin."""
+import glob
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+import lgamd  # noqa: F401
+from golden_util import HERE, sha
+
+sys.path.insert(0, HERE)
+from make_superglue_golden import ground_truth  # noqa: E402
+
+
+def grad_names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(HERE, "grad_*.npz")))
+
+
+def load_grad(name):
+    z = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
+    g = {k: z[k] for k in z.files if k != "meta_json"}
+    return g, json.loads(str(z["meta_json"]))
+
+
+def grad_case(meta):
+    """(conf, state dict, pair, gt) exactly as make_grad_golden.py built them (SHA-checked)."""
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = dict(meta["conf"])
+    sd = synthetic_state_dict(conf, **meta["weights"])
+    pkw = dict(meta["pair"])
+    pair = synthetic_pair(**pkw)
+    B, M = pkw["B"], pkw["M"]
+    if meta.get("scale_ori"):
+        rng = np.random.Generator(np.random.PCG64(pkw["seed"] + 1000))
+        pair.update({
+            "scales0": (rng.random((B, M)) * 2).astype(np.float32),
+            "oris0": (rng.random((B, M)) * 6.28 - 3.14).astype(np.float32),
+            "scales1": (rng.random((B, M)) * 2).astype(np.float32),
+            "oris1": (rng.random((B, M)) * 6.28 - 3.14).astype(np.float32),
+        })
+    gt = ground_truth(B, M, M, meta["gt_seed"])
+    assert sha(pair) == meta["inputs_sha256"], "input recipe drifted"
+    assert sha(sd) == meta["weights_sha256"], "weight recipe drifted"
+    assert sha(gt) == meta["gt_sha256"], "ground-truth recipe drifted"
+    return conf, sd, pair, gt
+
+
+def oracle_grads(conf, sd, pair, gt, dtype=torch.float64):
+    """d mean(total) / d (every parameter, descriptors0, descriptors1) of the oracle restatement."""
+    from oracle.lightglue_train_ref import train_loss
+
+    W = {k: torch.from_numpy(np.asarray(v)).to(dtype).requires_grad_() for k, v in sd.items()}
+    data = {k: torch.from_numpy(v).to(dtype) for k, v in pair.items() if not k.startswith("descriptors")}
+    d0 = torch.from_numpy(pair["descriptors0"]).to(dtype).requires_grad_()
+    d1 = torch.from_numpy(pair["descriptors1"]).to(dtype).requires_grad_()
+    data["descriptors0"], data["descriptors1"] = d0, d1
+    loss, losses = train_loss(W, data, gt, conf, dtype)
+    loss.backward()
+    g = {k: (w.grad if w.grad is not None else torch.zeros_like(w)).double().numpy() for k, w in W.items()}
+    return float(loss.detach()), g, d0.grad.double().numpy(), d1.grad.double().numpy()
+
+
+def golden_entries(g, name):
+    """(flat indices or None, float64 values) of parameter `name` in a gradient golden."""
+    idx = g.get(f"gidx:{name}")
+    return (None if idx is None else idx.astype(np.int64)), g[f"g64:{name}"]

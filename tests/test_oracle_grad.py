@@ -1,0 +1,35 @@
+"""Pin the float64 autograd gradients of the oracle's training loss (oracle/lightglue_train_ref.py)
+to the reference's own autograd gradients (tests/golden/grad_*.npz, make_grad_golden.py).
+
+Both sides are float64 torch-CPU autograd over the same algorithm with different op groupings, so
+the bar is tight: |d| <= 1e-9 * max|g| + 1e-12 per tensor -- except where the reference's double
+run itself rounds to float32: TokenConfidence.loss passes ``correct.float()`` targets
+(lightglue.py:117-120), so its BCE (the loss value, and the token Linear gradients) carries fp32
+rounding (measured 3e-8 relative): 1e-7 there.  ``posenc.condition_modulation`` gets an exactly
+zero gradient (a phase shift common to every point of an image cancels in q_rot . k_rot); both
+sides hold ~1e-17 of rounding.
+"""
+import numpy as np
+import pytest
+
+from grad_golden_util import golden_entries, grad_case, grad_names, load_grad, oracle_grads
+
+
+@pytest.mark.parametrize("name", grad_names())
+def test_oracle_gradients_match_reference(name):
+    g, meta = load_grad(name)
+    conf, sd, pair, gt = grad_case(meta)
+    loss, og, gd0, gd1 = oracle_grads(conf, sd, pair, gt)
+    assert abs(float(g["loss32"]) - loss) <= 1e-5 * abs(loss)  # the fp32 reference run, same loss
+    assert abs(loss - float(g["loss64"])) <= 1e-7 * abs(float(g["loss64"]))
+    assert list(og) == meta["names"]
+    for n in meta["names"]:
+        idx, ref = golden_entries(g, n)
+        got = og[n].reshape(-1)
+        got = got if idx is None else got[idx]
+        rel = 1e-7 if n.startswith("token_confidence.") else 1e-9
+        tol = rel * float(g[f"max64:{n}"]) + 1e-12
+        assert np.abs(got - ref).max() <= tol, n
+        assert abs(np.linalg.norm(og[n]) - float(g[f"norm64:{n}"])) <= rel * float(g[f"norm64:{n}"]) + 1e-12, n
+    for gd, key in ((gd0, "gdesc0"), (gd1, "gdesc1")):
+        assert np.abs(gd - g[key]).max() <= 1e-9 * np.abs(g[key]).max() + 1e-12, key

@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LIGHTGLUE_MI355X_LIB", os.path.join(_HERE, "liblightglue_mi355x.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE, LG_E_INTERNAL = 0, -1, -2, -3, -4, -5
 
@@ -34,6 +34,17 @@ EXPORTED_SYMBOLS = [
     "lg_attention",
     "lg_assignment_workspace_bytes",
     "lg_assignment_head",
+    # training (backward pass)
+    "lg_train_saved_bytes",
+    "lg_train_scratch_bytes",
+    "lg_train_forward",
+    "lg_train_backward",
+    "lg_head_scratch_bytes",
+    "lg_head_backward",
+    "lg_train_gemm_workspace_bytes",
+    "lg_train_gemm",
+    "lg_train_attention",
+    "lg_train_attention_backward",
     # SuperPoint extractor (include/superpoint_mi355x.h)
     "sp_create",
     "sp_destroy",
@@ -256,6 +267,26 @@ def load():
         ),
         "lg_assignment_workspace_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
         "lg_assignment_head": (ctypes.c_int, [_P, i32, _P, _P, i32, i32, i32, _P, _P, _P, _P, _P, sz, _P]),
+        "lg_train_saved_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_train_scratch_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_train_forward": (ctypes.c_int, [_P, _P, ctypes.POINTER(LGInputs), _P, _P, _P, sz, _P]),
+        "lg_train_backward": (ctypes.c_int, [_P, _P, ctypes.POINTER(LGInputs), _P, sz, _P, _P, _P, _P, _P, _P, sz, _P]),
+        "lg_head_scratch_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_head_backward": (
+            ctypes.c_int,
+            [_P, _P, i32, _P, _P, i32, i32, i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, sz, _P],
+        ),
+        "lg_train_gemm_workspace_bytes": (ctypes.c_int, [i32, i32, i32, i32, ctypes.POINTER(sz)]),
+        "lg_train_gemm": (
+            ctypes.c_int,
+            [_P, _P, _P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+             i32, i32, i32, i32, ctypes.c_float, ctypes.c_float, _P, i32, i32, _P, sz, _P],
+        ),
+        "lg_train_attention": (ctypes.c_int, [_P, _P, _P, i32, i32, i32, i32, ctypes.c_float, _P, _P, _P]),
+        "lg_train_attention_backward": (
+            ctypes.c_int,
+            [_P, _P, _P, _P, _P, _P, i32, i32, i32, i32, ctypes.c_float, _P, _P, _P, _P, _P],
+        ),
         "sp_create": (ctypes.c_int, [ctypes.POINTER(SPConfig), ctypes.c_int, ctypes.POINTER(_P)]),
         "sp_destroy": (ctypes.c_int, [_P]),
         "sp_weight_count": (ctypes.c_int, [_P]),

@@ -491,6 +491,19 @@ int lg_destroy(lg_handle_t* h) {
   delete h;
   return LG_OK;
 }
+}  // extern "C"
+
+// accessors for the training entry points (lightglue_train.cpp)
+namespace lg {
+const lg_config_t* handle_config(const lg_handle* h) { return &h->cfg; }
+int handle_device(const lg_handle* h) { return h->device; }
+int handle_weight_index(const lg_handle* h, const std::string& name) {
+  auto it = h->index.find(name);
+  return it == h->index.end() ? -1 : it->second;
+}
+}  // namespace lg
+
+extern "C" {
 
 int lg_weight_count(const lg_handle_t* h) { return h ? (int)h->schema.size() : 0; }
 const char* lg_weight_name(const lg_handle_t* h, int i) {

@@ -1,0 +1,628 @@
+// C-ABI of the LightGlue training path (include/lightglue_mi355x.h, "Training"): the
+// activation-saving training forward, its backward, and the assignment-head backward -- what
+// torch autograd computes in the reference (gluefactory/train.py:436-450 over
+// gluefactory/models/matchers/lightglue.py:444-579 and :614-663).  Kernels: train.hip.
+//
+// Row space: R = B (M + N) rows of 256 -- image-0 rows (pair-major, R0 = B M of them) then image-1
+// rows -- as in the eval forward.  Every activation is row-major fp32; head h of a projection is
+// columns [64h, 64h + 64).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/lightglue_mi355x.h"
+#include "kernels.h"
+#include "train.h"
+
+namespace lg {
+int api_fail(int code, const char* msg);
+const lg_config_t* handle_config(const lg_handle* h);
+int handle_device(const lg_handle* h);
+int handle_weight_index(const lg_handle* h, const std::string& name);
+}  // namespace lg
+
+namespace {
+
+using namespace lg;
+
+int fail(int code, const std::string& msg) { return api_fail(code, msg.c_str()); }
+
+#define TR_HIP(expr)                                                                                \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    if (_e != hipSuccess) return fail(LG_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+constexpr int D = 256;
+
+struct Dims {
+  int B, M, N, R, R0, din, L, H, m_in;
+  bool proj;
+};
+
+Dims dims_of(const lg_handle_t* h, int B, int M, int N) {
+  const lg_config_t& c = *handle_config(h);
+  Dims d;
+  d.B = B;
+  d.M = M;
+  d.N = N;
+  d.R0 = B * M;
+  d.R = B * (M + N);
+  d.din = c.input_dim;
+  d.L = c.n_layers;
+  d.H = c.num_heads;
+  d.m_in = c.add_scale_ori ? 4 : 2;
+  d.proj = c.input_dim != c.descriptor_dim;
+  return d;
+}
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  float* f(size_t n) {
+    char* p = base ? base + off : nullptr;
+    off += (n * sizeof(float) + 255) & ~size_t(255);
+    return reinterpret_cast<float*>(p);
+  }
+};
+
+struct Blk {
+  float *Q, *K, *V, *LSE, *O, *CAT, *H1, *ST, *G, *Y;
+};
+struct Saved {
+  float *X0, *Din, *PEX, *COS, *SIN, *SZ, *QKV;
+  std::vector<Blk> self, cross;
+  size_t bytes;
+};
+
+Saved carve_saved(char* base, const Dims& d) {
+  Carver c{base};
+  Saved s;
+  const size_t R = d.R;
+  s.X0 = c.f(R * D);
+  s.Din = d.proj ? c.f(R * d.din) : nullptr;
+  s.PEX = c.f(R * 4);
+  s.COS = c.f(R * 32);
+  s.SIN = c.f(R * 32);
+  s.SZ = c.f(4 * (size_t)d.B);
+  s.QKV = c.f(R * 3 * D);  // forward temporary
+  const size_t nl = (size_t)d.B * d.H * (d.M + d.N);
+  for (int l = 0; l < d.L; ++l) {
+    Blk b{};
+    b.Q = c.f(R * D);
+    b.K = c.f(R * D);
+    b.V = c.f(R * D);
+    b.LSE = c.f(nl);
+    b.O = c.f(R * D);
+    b.CAT = c.f(R * 2 * D);
+    b.H1 = c.f(R * 2 * D);
+    b.ST = c.f(R * 2);
+    b.G = c.f(R * 2 * D);
+    b.Y = c.f(R * D);
+    s.self.push_back(b);
+    Blk x{};
+    x.Q = c.f(R * D);  // qk
+    x.V = c.f(R * D);
+    x.LSE = c.f(nl);
+    x.O = c.f(R * D);
+    x.CAT = c.f(R * 2 * D);
+    x.H1 = c.f(R * 2 * D);
+    x.ST = c.f(R * 2);
+    x.G = c.f(R * 2 * D);
+    x.Y = c.f(R * D);  // the layer's output
+    s.cross.push_back(x);
+  }
+  s.bytes = c.off;
+  return s;
+}
+
+struct Scratch {
+  float *GX, *GY, *GG, *GH, *GC, *GO, *GQ, *GK, *GV, *GQKV, *DELTA, *GCOS, *GSIN, *WS, *PART;
+  size_t ws_floats, part_floats, bytes;
+};
+
+size_t gemm_ws_need(const Dims& d) {
+  size_t w = 0;
+  auto upd = [&](int M, int N, int K) { w = std::max(w, tgemm_ws_floats(M, N, K, 1)); };
+  upd(3 * D, D, d.R);
+  upd(D, D, d.R);
+  upd(2 * D, 2 * D, d.R);
+  upd(D, 2 * D, d.R);
+  if (d.proj) upd(D, d.din, d.R);
+  return w;
+}
+
+size_t part_need(const Dims& d) {
+  size_t p = colsum_part_floats(d.R, 3 * D);
+  p = std::max(p, lngelu_bwd_part_floats(d.R));
+  p = std::max(p, pe_bwd_part_floats(d.R));
+  return p;
+}
+
+Scratch carve_scratch(char* base, const Dims& d) {
+  Carver c{base};
+  Scratch s;
+  const size_t R = d.R;
+  s.GX = c.f(R * D);
+  s.GY = c.f(R * D);
+  s.GG = c.f(R * 2 * D);
+  s.GH = c.f(R * 2 * D);
+  s.GC = c.f(R * 2 * D);
+  s.GO = c.f(R * D);
+  s.GQ = c.f(R * D);
+  s.GK = c.f(R * D);
+  s.GV = c.f(R * D);
+  s.GQKV = c.f(R * 3 * D);
+  s.DELTA = c.f((size_t)d.B * d.H * (d.M + d.N));
+  s.GCOS = c.f(R * 32);
+  s.GSIN = c.f(R * 32);
+  s.ws_floats = gemm_ws_need(d);
+  s.WS = c.f(s.ws_floats + 64);
+  s.part_floats = part_need(d);
+  s.PART = c.f(s.part_floats + 64);
+  s.bytes = c.off;
+  return s;
+}
+
+// Parameter lookup by reference name.
+struct Params {
+  const lg_handle_t* h;
+  const float* const* p;
+  float* const* g;
+  const float* w(const std::string& n) const { return p[handle_weight_index(h, n)]; }
+  float* gr(const std::string& n) const { return g ? g[handle_weight_index(h, n)] : nullptr; }
+};
+
+struct Ctx {
+  hipStream_t st;
+  float* ws;
+  size_t ws_floats;
+  float* part;
+};
+
+// y[M,N] = alpha (x[M,K] W[N,K]^T + b) + beta y
+hipError_t linear(const Ctx& c, const float* x, long long ldx, int rows, int K, const float* W, const float* b, int N,
+                  float* y, long long ldy, float beta = 0.f, float alpha = 1.f) {
+  TGemm g{x, W, y, ldx, K, ldy, 0, 0, 0, rows, N, K, 1, alpha, beta, b};
+  return tgemm(g, false, true, c.ws, c.ws_floats, c.st);
+}
+// dx[M,K] (+)= dy[M,N] W[N,K]
+hipError_t linear_dgrad(const Ctx& c, const float* dy, long long lddy, int rows, int N, const float* W, int K, float* dx,
+                        long long lddx, float beta = 0.f) {
+  TGemm g{dy, W, dx, lddy, K, lddx, 0, 0, 0, rows, K, N, 1, 1.f, beta, nullptr};
+  return tgemm(g, false, false, c.ws, c.ws_floats, c.st);
+}
+// dW[N,K] = dy[rows,N]^T x[rows,K]; db[N] = colsum(dy)
+hipError_t linear_wgrad(const Ctx& c, const float* dy, long long lddy, const float* x, long long ldx, int rows, int N,
+                        int K, float* dW, float* db) {
+  if (dW) {
+    TGemm g{dy, x, dW, lddy, ldx, K, 0, 0, 0, N, K, rows, 1, 1.f, 0.f, nullptr};
+    hipError_t e = tgemm(g, true, false, c.ws, c.ws_floats, c.st);
+    if (e != hipSuccess) return e;
+  }
+  if (db) return colsum(dy, lddy, rows, N, nullptr, c.part, db, c.st);
+  return hipSuccess;
+}
+
+TAttn attn_args(const float* Q, const float* K, const float* V, float* O, float* lse, int B, int H, int Nq, int Nk,
+                float scale) {
+  TAttn a{};
+  a.Q = Q;
+  a.K = K;
+  a.V = V;
+  a.O = O;
+  a.lse = lse;
+  a.ldq = a.ldk = a.ldv = a.ldo = D;
+  a.B = B;
+  a.H = H;
+  a.Nq = Nq;
+  a.Nk = Nk;
+  a.scale = scale;
+  return a;
+}
+
+// FFN + residual of a block (lightglue.py:171-176,191,246-248): CAT[:, 256:] holds the message
+hipError_t ffn_forward(const Ctx& c, const Params& P, const std::string& pre, const float* X, Blk& b, int R) {
+  hipError_t e;
+  if ((e = hipMemcpy2DAsync(b.CAT, 2 * D * sizeof(float), X, D * sizeof(float), D * sizeof(float), R,
+                            hipMemcpyDeviceToDevice, c.st)) != hipSuccess)
+    return e;
+  if ((e = linear(c, b.CAT, 2 * D, R, 2 * D, P.w(pre + ".ffn.0.weight"), P.w(pre + ".ffn.0.bias"), 2 * D, b.H1, 2 * D)) !=
+      hipSuccess)
+    return e;
+  if ((e = lngelu_fwd(b.H1, P.w(pre + ".ffn.1.weight"), P.w(pre + ".ffn.1.bias"), R, b.G, b.ST, c.st)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(b.Y, X, (size_t)R * D * sizeof(float), hipMemcpyDeviceToDevice, c.st)) != hipSuccess) return e;
+  return linear(c, b.G, 2 * D, R, 2 * D, P.w(pre + ".ffn.3.weight"), P.w(pre + ".ffn.3.bias"), D, b.Y, D, 1.f);
+}
+
+// FFN backward: Gout = d/d(block output); writes gX = Gout + d/d(x through the ffn input) and
+// leaves d/d(message) in GC[:, 256:]
+hipError_t ffn_backward(const Ctx& c, const Params& P, const std::string& pre, const Blk& b, const float* Gout,
+                        float* gX, Scratch& s, int R) {
+  hipError_t e;
+  if ((e = linear_wgrad(c, Gout, D, b.G, 2 * D, R, D, 2 * D, P.gr(pre + ".ffn.3.weight"), P.gr(pre + ".ffn.3.bias"))) !=
+      hipSuccess)
+    return e;
+  if ((e = linear_dgrad(c, Gout, D, R, D, P.w(pre + ".ffn.3.weight"), 2 * D, s.GG, 2 * D)) != hipSuccess) return e;
+  if ((e = lngelu_bwd(s.GG, b.H1, b.ST, P.w(pre + ".ffn.1.weight"), P.w(pre + ".ffn.1.bias"), R, s.GH, s.PART,
+                      P.gr(pre + ".ffn.1.weight"), P.gr(pre + ".ffn.1.bias"), c.st)) != hipSuccess)
+    return e;
+  if ((e = linear_wgrad(c, s.GH, 2 * D, b.CAT, 2 * D, R, 2 * D, 2 * D, P.gr(pre + ".ffn.0.weight"),
+                        P.gr(pre + ".ffn.0.bias"))) != hipSuccess)
+    return e;
+  if ((e = linear_dgrad(c, s.GH, 2 * D, R, 2 * D, P.w(pre + ".ffn.0.weight"), 2 * D, s.GC, 2 * D)) != hipSuccess) return e;
+  return add_rows256(Gout, D, s.GC, 2 * D, gX, D, R, c.st);
+}
+
+int check_shape(const lg_handle_t* h, int B, int M, int N) {
+  if (!h) return fail(LG_E_INVALID, "null handle");
+  if (B <= 0) return fail(LG_E_INVALID, "batch must be >= 1");
+  if (M <= 0 || N <= 0) return fail(LG_E_INVALID, "empty keypoint set");
+  if ((long long)B * (M + N) > (1ll << 30) / 1024) return fail(LG_E_INVALID, "row count too large");
+  return LG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lg_train_saved_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (int e = check_shape(h, B, M, N)) return e;
+  if (!bytes) return fail(LG_E_INVALID, "null argument");
+  *bytes = carve_saved(nullptr, dims_of(h, B, M, N)).bytes;
+  return LG_OK;
+}
+
+int lg_train_scratch_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (int e = check_shape(h, B, M, N)) return e;
+  if (!bytes) return fail(LG_E_INVALID, "null argument");
+  *bytes = carve_scratch(nullptr, dims_of(h, B, M, N)).bytes;
+  return LG_OK;
+}
+
+int lg_train_forward(lg_handle_t* h, const float* const* params, const lg_inputs_t* in, float* layer_descriptors0,
+                     float* layer_descriptors1, void* saved, size_t saved_bytes, void* stream) {
+  if (!in || !params || !saved) return fail(LG_E_INVALID, "null argument");
+  if (int e = check_shape(h, in->B, in->M, in->N)) return e;
+  if (!in->keypoints0 || !in->keypoints1 || !in->descriptors0 || !in->descriptors1)
+    return fail(LG_E_INVALID, "null input tensor");
+  const Dims d = dims_of(h, in->B, in->M, in->N);
+  if (d.m_in == 4 && (!in->scales0 || !in->oris0 || !in->scales1 || !in->oris1))
+    return fail(LG_E_INVALID, "add_scale_ori needs scales0/1 and oris0/1");
+  Saved s = carve_saved((char*)saved, d);
+  if (saved_bytes < s.bytes) return fail(LG_E_WORKSPACE, "saved buffer too small: need " + std::to_string(s.bytes));
+  TR_HIP(hipSetDevice(handle_device(h)));
+  const Ctx c{(hipStream_t)stream, nullptr, 0, nullptr};
+  const Params P{h, params, nullptr};
+  const int B = d.B, M = d.M, N = d.N, R = d.R, R0 = d.R0, H = d.H;
+  // positional encoding (lightglue.py:452-456,490-494); no image_size: min/max extent (:25-26)
+  if (in->image_size0) TR_HIP(hipMemcpyAsync(s.SZ, in->image_size0, 2 * B * sizeof(float), hipMemcpyDeviceToDevice, c.st));
+  else TR_HIP(kpt_extent(in->keypoints0, B, M, s.SZ, c.st));
+  if (in->image_size1)
+    TR_HIP(hipMemcpyAsync(s.SZ + 2 * B, in->image_size1, 2 * B * sizeof(float), hipMemcpyDeviceToDevice, c.st));
+  else TR_HIP(kpt_extent(in->keypoints1, B, N, s.SZ + 2 * B, c.st));
+  for (int img = 0; img < 2; ++img) {
+    TPE p{};
+    p.kpts = img ? in->keypoints1 : in->keypoints0;
+    p.size = s.SZ + 2 * B * img;
+    p.scales = img ? in->scales1 : in->scales0;
+    p.oris = img ? in->oris1 : in->oris0;
+    p.Wr = P.w("posenc.Wr.weight");
+    p.Wc = P.w("posenc.condition_modulation.weight");
+    p.bc = P.w("posenc.condition_modulation.bias");
+    p.B = B;
+    p.n = img ? N : M;
+    p.m_in = d.m_in;
+    const size_t r0 = img ? R0 : 0;
+    p.x = s.PEX + r0 * 4;
+    p.cosb = s.COS + r0 * 32;
+    p.sinb = s.SIN + r0 * 32;
+    TR_HIP(pe_train(p, c.st));
+  }
+  // input descriptors (input_proj, :370-373,486-487)
+  if (d.proj) {
+    TR_HIP(hipMemcpyAsync(s.Din, in->descriptors0, (size_t)R0 * d.din * 4, hipMemcpyDeviceToDevice, c.st));
+    TR_HIP(hipMemcpyAsync(s.Din + (size_t)R0 * d.din, in->descriptors1, (size_t)(R - R0) * d.din * 4,
+                          hipMemcpyDeviceToDevice, c.st));
+    TR_HIP(linear(c, s.Din, d.din, R, d.din, P.w("input_proj.weight"), P.w("input_proj.bias"), D, s.X0, D));
+  } else {
+    TR_HIP(hipMemcpyAsync(s.X0, in->descriptors0, (size_t)R0 * D * 4, hipMemcpyDeviceToDevice, c.st));
+    TR_HIP(hipMemcpyAsync(s.X0 + (size_t)R0 * D, in->descriptors1, (size_t)(R - R0) * D * 4, hipMemcpyDeviceToDevice, c.st));
+  }
+  const float scale = 0.125f;  // head_dim ** -0.5 (:146-149; cross: (s^0.5)^2, :235-236)
+  const size_t lse1 = (size_t)B * H * M;
+  for (int l = 0; l < d.L; ++l) {
+    const std::string sp = "transformers." + std::to_string(l) + ".self_attn";
+    const std::string cp = "transformers." + std::to_string(l) + ".cross_attn";
+    const float* X = l == 0 ? s.X0 : s.cross[l - 1].Y;
+    // SelfBlock (:178-191) on both images (shared weights, :270-271)
+    Blk& sb = s.self[l];
+    TR_HIP(linear(c, X, D, R, D, P.w(sp + ".Wqkv.weight"), P.w(sp + ".Wqkv.bias"), 3 * D, s.QKV, 3 * D));
+    TR_HIP(rotary_split(s.QKV, s.COS, s.SIN, R, H, sb.Q, sb.K, sb.V, c.st));
+    TR_HIP(tattn_forward(attn_args(sb.Q, sb.K, sb.V, sb.O, sb.LSE, B, H, M, M, scale), c.st));
+    TR_HIP(tattn_forward(attn_args(sb.Q + (size_t)R0 * D, sb.K + (size_t)R0 * D, sb.V + (size_t)R0 * D, sb.O + (size_t)R0 * D,
+                                   sb.LSE + lse1, B, H, N, N, scale),
+                         c.st));
+    TR_HIP(linear(c, sb.O, D, R, D, P.w(sp + ".out_proj.weight"), P.w(sp + ".out_proj.bias"), D, sb.CAT + D, 2 * D));
+    TR_HIP(ffn_forward(c, P, sp, X, sb, R));
+    // CrossBlock (:220-249)
+    Blk& cb = s.cross[l];
+    TR_HIP(linear(c, sb.Y, D, R, D, P.w(cp + ".to_qk.weight"), P.w(cp + ".to_qk.bias"), D, cb.Q, D));
+    TR_HIP(linear(c, sb.Y, D, R, D, P.w(cp + ".to_v.weight"), P.w(cp + ".to_v.bias"), D, cb.V, D));
+    // m0 = softmax_j(sim) v1 (image-0 queries), m1 = softmax_i(sim)^T v0 (image-1 queries)
+    TR_HIP(tattn_forward(attn_args(cb.Q, cb.Q + (size_t)R0 * D, cb.V + (size_t)R0 * D, cb.O, cb.LSE, B, H, M, N, scale), c.st));
+    TR_HIP(tattn_forward(
+        attn_args(cb.Q + (size_t)R0 * D, cb.Q, cb.V, cb.O + (size_t)R0 * D, cb.LSE + lse1, B, H, N, M, scale), c.st));
+    TR_HIP(linear(c, cb.O, D, R, D, P.w(cp + ".to_out.weight"), P.w(cp + ".to_out.bias"), D, cb.CAT + D, 2 * D));
+    TR_HIP(ffn_forward(c, P, cp, sb.Y, cb, R));
+    // ref_descriptors*[:, l] (:521-524,572)
+    if (layer_descriptors0)
+      TR_HIP(hipMemcpy2DAsync(layer_descriptors0 + (size_t)l * M * D, (size_t)d.L * M * D * 4, cb.Y, (size_t)M * D * 4,
+                              (size_t)M * D * 4, B, hipMemcpyDeviceToDevice, c.st));
+    if (layer_descriptors1)
+      TR_HIP(hipMemcpy2DAsync(layer_descriptors1 + (size_t)l * N * D, (size_t)d.L * N * D * 4, cb.Y + (size_t)R0 * D,
+                              (size_t)N * D * 4, (size_t)N * D * 4, B, hipMemcpyDeviceToDevice, c.st));
+  }
+  return LG_OK;
+}
+
+int lg_train_backward(lg_handle_t* h, const float* const* params, const lg_inputs_t* in, const void* saved,
+                      size_t saved_bytes, const float* grad_layer_descriptors0, const float* grad_layer_descriptors1,
+                      float* const* grads, float* grad_desc0, float* grad_desc1, void* scratch, size_t scratch_bytes,
+                      void* stream) {
+  if (!in || !params || !saved || !scratch) return fail(LG_E_INVALID, "null argument");
+  if (int e = check_shape(h, in->B, in->M, in->N)) return e;
+  const Dims d = dims_of(h, in->B, in->M, in->N);
+  Saved s = carve_saved((char*)saved, d);
+  if (saved_bytes < s.bytes) return fail(LG_E_WORKSPACE, "saved buffer too small");
+  Scratch w = carve_scratch((char*)scratch, d);
+  if (scratch_bytes < w.bytes) return fail(LG_E_WORKSPACE, "scratch too small: need " + std::to_string(w.bytes));
+  TR_HIP(hipSetDevice(handle_device(h)));
+  const Ctx c{(hipStream_t)stream, w.WS, w.ws_floats, w.PART};
+  const Params P{h, params, grads};
+  const int B = d.B, M = d.M, N = d.N, R = d.R, R0 = d.R0, H = d.H;
+  const float scale = 0.125f;
+  const size_t lse1 = (size_t)B * H * M;
+  const size_t o1 = (size_t)R0 * D;
+  TR_HIP(hipMemsetAsync(w.GX, 0, (size_t)R * D * 4, c.st));
+  TR_HIP(hipMemsetAsync(w.GCOS, 0, (size_t)R * 32 * 4, c.st));
+  TR_HIP(hipMemsetAsync(w.GSIN, 0, (size_t)R * 32 * 4, c.st));
+  for (int l = d.L - 1; l >= 0; --l) {
+    const std::string sp = "transformers." + std::to_string(l) + ".self_attn";
+    const std::string cp = "transformers." + std::to_string(l) + ".cross_attn";
+    const Blk& sb = s.self[l];
+    const Blk& cb = s.cross[l];
+    const float* X = l == 0 ? s.X0 : s.cross[l - 1].Y;
+    // d/d(layer output) += the heads' gradient of ref_descriptors*[:, l]
+    TR_HIP(add_layer_rows(w.GX, grad_layer_descriptors0, grad_layer_descriptors1, B, M, N, d.L, l, c.st));
+    // ---- CrossBlock backward: GX -> GY (d/d self-block output sb.Y)
+    TR_HIP(ffn_backward(c, P, cp, cb, w.GX, w.GY, w, R));
+    const float* gmsg = w.GC + D;
+    TR_HIP(linear_wgrad(c, gmsg, 2 * D, cb.O, D, R, D, D, P.gr(cp + ".to_out.weight"), P.gr(cp + ".to_out.bias")));
+    TR_HIP(linear_dgrad(c, gmsg, 2 * D, R, D, P.w(cp + ".to_out.weight"), D, w.GO, D));
+    TR_HIP(attn_delta(cb.O, w.GO, D, B, H, M, w.DELTA, c.st));
+    TR_HIP(attn_delta(cb.O + o1, w.GO + o1, D, B, H, N, w.DELTA + lse1, c.st));
+    TR_HIP(hipMemsetAsync(w.GQ + o1, 0, (size_t)(R - R0) * D * 4, c.st));
+    {  // path 1 (image-1 queries over image-0 keys): dQ -> gqk1 (atomics), dK -> gqk0, dV -> gv0
+      TAttn a = attn_args(cb.Q + o1, cb.Q, cb.V, cb.O + o1, cb.LSE + lse1, B, H, N, M, scale);
+      a.dO = w.GO + o1;
+      a.delta = w.DELTA + lse1;
+      a.dQ = w.GQ + o1;
+      a.dK = w.GQ;
+      a.dV = w.GV;
+      a.accum_kv = 0;
+      TR_HIP(tattn_backward(a, c.st));
+    }
+    {  // path 0 (image-0 queries over image-1 keys): dQ -> gqk0 (+= onto path 1's dK), dK += gqk1
+      TAttn a = attn_args(cb.Q, cb.Q + o1, cb.V + o1, cb.O, cb.LSE, B, H, M, N, scale);
+      a.dO = w.GO;
+      a.delta = w.DELTA;
+      a.dQ = w.GQ;
+      a.dK = w.GQ + o1;
+      a.dV = w.GV + o1;
+      a.accum_kv = 1;
+      TR_HIP(hipMemsetAsync(w.GV + o1, 0, (size_t)(R - R0) * D * 4, c.st));
+      TR_HIP(tattn_backward(a, c.st));
+    }
+    TR_HIP(linear_wgrad(c, w.GQ, D, sb.Y, D, R, D, D, P.gr(cp + ".to_qk.weight"), P.gr(cp + ".to_qk.bias")));
+    TR_HIP(linear_wgrad(c, w.GV, D, sb.Y, D, R, D, D, P.gr(cp + ".to_v.weight"), P.gr(cp + ".to_v.bias")));
+    TR_HIP(linear_dgrad(c, w.GQ, D, R, D, P.w(cp + ".to_qk.weight"), D, w.GY, D, 1.f));
+    TR_HIP(linear_dgrad(c, w.GV, D, R, D, P.w(cp + ".to_v.weight"), D, w.GY, D, 1.f));
+    // ---- SelfBlock backward: GY -> GX (d/d layer input X)
+    TR_HIP(ffn_backward(c, P, sp, sb, w.GY, w.GX, w, R));
+    TR_HIP(linear_wgrad(c, gmsg, 2 * D, sb.O, D, R, D, D, P.gr(sp + ".out_proj.weight"), P.gr(sp + ".out_proj.bias")));
+    TR_HIP(linear_dgrad(c, gmsg, 2 * D, R, D, P.w(sp + ".out_proj.weight"), D, w.GO, D));
+    TR_HIP(attn_delta(sb.O, w.GO, D, B, H, M, w.DELTA, c.st));
+    TR_HIP(attn_delta(sb.O + o1, w.GO + o1, D, B, H, N, w.DELTA + lse1, c.st));
+    TR_HIP(hipMemsetAsync(w.GQ, 0, (size_t)R * D * 4, c.st));
+    for (int img = 0; img < 2; ++img) {
+      const size_t off = img ? o1 : 0;
+      const int n = img ? N : M;
+      TAttn a = attn_args(sb.Q + off, sb.K + off, sb.V + off, sb.O + off, sb.LSE + (img ? lse1 : 0), B, H, n, n, scale);
+      a.dO = w.GO + off;
+      a.delta = w.DELTA + (img ? lse1 : 0);
+      a.dQ = w.GQ + off;
+      a.dK = w.GK + off;
+      a.dV = w.GV + off;
+      TR_HIP(tattn_backward(a, c.st));
+    }
+    TR_HIP(rotary_split_bwd(w.GQ, w.GK, w.GV, sb.Q, sb.K, s.COS, s.SIN, R, H, w.GQKV, w.GCOS, w.GSIN, c.st));
+    TR_HIP(linear_wgrad(c, w.GQKV, 3 * D, X, D, R, 3 * D, D, P.gr(sp + ".Wqkv.weight"), P.gr(sp + ".Wqkv.bias")));
+    TR_HIP(linear_dgrad(c, w.GQKV, 3 * D, R, 3 * D, P.w(sp + ".Wqkv.weight"), D, w.GX, D, 1.f));
+  }
+  // GX = d/d(X0): input_proj (:486-487) and the input descriptors
+  if (d.proj) {
+    TR_HIP(linear_wgrad(c, w.GX, D, s.Din, d.din, R, D, d.din, P.gr("input_proj.weight"), P.gr("input_proj.bias")));
+    if (grad_desc0) TR_HIP(linear_dgrad(c, w.GX, D, R0, D, P.w("input_proj.weight"), d.din, grad_desc0, d.din));
+    if (grad_desc1) TR_HIP(linear_dgrad(c, w.GX + o1, D, R - R0, D, P.w("input_proj.weight"), d.din, grad_desc1, d.din));
+  } else {
+    if (grad_desc0) TR_HIP(hipMemcpyAsync(grad_desc0, w.GX, o1 * 4, hipMemcpyDeviceToDevice, c.st));
+    if (grad_desc1) TR_HIP(hipMemcpyAsync(grad_desc1, w.GX + o1, (size_t)(R - R0) * D * 4, hipMemcpyDeviceToDevice, c.st));
+  }
+  // posenc (:63-77): d/d(Wr, condition_modulation) from the rotary's cos / sin gradients
+  float* gWr = P.gr("posenc.Wr.weight");
+  float* gWc = P.gr("posenc.condition_modulation.weight");
+  float* gbc = P.gr("posenc.condition_modulation.bias");
+  if (gWr && gWc && gbc)
+    TR_HIP(pe_backward(s.PEX, s.COS, s.SIN, w.GCOS, w.GSIN, R, R0, (float)M, (float)N, d.m_in, w.PART, gWr, gWc, gbc, c.st));
+  return LG_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ assignment head backward
+namespace {
+struct HeadScratch {
+  float *X, *MD, *GMD, *SIM, *Z, *GZ, *LSER, *LSEC, *RS, *GD, *GT, *WS, *PART;
+  size_t ws_floats, bytes;
+};
+HeadScratch carve_head_scratch(char* base, int B, int M, int N) {
+  Carver c{base};
+  HeadScratch s;
+  const size_t R = (size_t)B * (M + N);
+  s.X = c.f(R * D);
+  s.MD = c.f(R * D);
+  s.GMD = c.f(R * D);
+  s.SIM = c.f((size_t)B * M * N);
+  s.Z = c.f(R);
+  s.GZ = c.f(R);
+  s.LSER = c.f((size_t)B * M);
+  s.LSEC = c.f((size_t)B * N);
+  s.RS = c.f(R);  // row sums (image-0 rows) then column sums (image-1 rows)
+  s.GD = c.f(R);  // dustbin-column entries then dustbin-row entries
+  s.GT = c.f(R);
+  s.ws_floats = std::max({tgemm_ws_floats(D, D, (int)R, 1), tgemm_ws_floats(M, D, N, B), tgemm_ws_floats(N, D, M, B)});
+  s.WS = c.f(s.ws_floats + 64);
+  s.PART = c.f(colsum_part_floats((int)R, D) + 64);
+  s.bytes = c.off;
+  return s;
+}
+}  // namespace
+
+extern "C" {
+
+int lg_head_scratch_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (int e = check_shape(h, B, M, N)) return e;
+  if (!bytes) return fail(LG_E_INVALID, "null argument");
+  *bytes = carve_head_scratch(nullptr, B, M, N).bytes;
+  return LG_OK;
+}
+
+int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, const float* desc0, const float* desc1,
+                     int32_t B, int32_t M, int32_t N, const float* la_grad, const float* s_in, const float* s_dust,
+                     const float* grad_similarity, const float* grad_token0, const float* grad_token1,
+                     float* const* grads, float* grad_desc0, float* grad_desc1, void* scratch, size_t scratch_bytes,
+                     void* stream) {
+  if (!params || !desc0 || !desc1 || !la_grad || !scratch) return fail(LG_E_INVALID, "null argument");
+  if (int e = check_shape(h, B, M, N)) return e;
+  const int L = handle_config(h)->n_layers;
+  if (layer < 0) layer += L;
+  if (layer < 0 || layer >= L) return fail(LG_E_INVALID, "layer index out of range");
+  if ((grad_token0 || grad_token1) && layer >= L - 1)
+    return fail(LG_E_INVALID, "token_confidence exists for layers 0..n_layers-2 only (lightglue.py:395-397)");
+  HeadScratch s = carve_head_scratch((char*)scratch, B, M, N);
+  if (scratch_bytes < s.bytes) return fail(LG_E_WORKSPACE, "scratch too small: need " + std::to_string(s.bytes));
+  TR_HIP(hipSetDevice(handle_device(h)));
+  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART};
+  const Params P{h, params, grads};
+  const std::string a = "log_assignment." + std::to_string(layer);
+  const int R0 = B * M, R = B * (M + N);
+  const size_t o1 = (size_t)R0 * D;
+  const float* Wf = P.w(a + ".final_proj.weight");
+  const float* wm = P.w(a + ".matchability.weight");
+  // recompute: md = final_proj(desc) / 4, z = matchability(desc), sim = md0 md1^T (:306-315)
+  TR_HIP(hipMemcpyAsync(s.X, desc0, o1 * 4, hipMemcpyDeviceToDevice, c.st));
+  TR_HIP(hipMemcpyAsync(s.X + o1, desc1, (size_t)(R - R0) * D * 4, hipMemcpyDeviceToDevice, c.st));
+  TR_HIP(linear(c, s.X, D, R, D, Wf, P.w(a + ".final_proj.bias"), D, s.MD, D, 0.f, 0.25f));
+  TR_HIP(gemv256(s.X, R, wm, P.w(a + ".matchability.bias"), s.Z, c.st));
+  {
+    TGemm g{s.MD, s.MD + o1, s.SIM, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B, 1.f, 0.f, nullptr};
+    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st));
+  }
+  TR_HIP(sim_lse(s.SIM, B, M, N, s.LSER, s.LSEC, c.st));
+  // sigmoid_log_double_softmax backward (:284-296)
+  TR_HIP(la_grad_sums(la_grad, s_in, s_dust, B, M, N, s.RS, s.RS + R0, s.GD, s.GD + R0, c.st));
+  TR_HIP(la_grad_sim(s.SIM, la_grad, s_in, s.LSER, s.LSEC, s.RS, s.RS + R0, grad_similarity, B, M, N, c.st));
+  TR_HIP(la_grad_z(s.Z, s.RS, s.GD, R, s.GZ, c.st));
+  // d/d(final_proj output) = d/d(md) / 4: gmd0 = gsim md1, gmd1 = gsim^T md0
+  {
+    TGemm g{s.SIM, s.MD + o1, s.GMD, N, D, D, (long long)M * N, (long long)N * D, (long long)M * D, M, D, N, B, 0.25f, 0.f, nullptr};
+    TR_HIP(tgemm(g, false, false, c.ws, c.ws_floats, c.st));
+  }
+  {
+    TGemm g{s.SIM, s.MD, s.GMD + o1, N, D, D, (long long)M * N, (long long)M * D, (long long)N * D, N, D, M, B, 0.25f, 0.f, nullptr};
+    TR_HIP(tgemm(g, true, false, c.ws, c.ws_floats, c.st));
+  }
+  TR_HIP(linear_wgrad(c, s.GMD, D, s.X, D, R, D, D, P.gr(a + ".final_proj.weight"), P.gr(a + ".final_proj.bias")));
+  if (float* g = P.gr(a + ".matchability.weight")) TR_HIP(colsum(s.X, D, R, D, s.GZ, c.part, g, c.st));
+  if (float* g = P.gr(a + ".matchability.bias")) TR_HIP(colsum(s.GZ, 1, R, 1, nullptr, c.part, g, c.st));
+  if (grad_desc0) {
+    TR_HIP(linear_dgrad(c, s.GMD, D, R0, D, Wf, D, grad_desc0, D));
+    TR_HIP(rank1_add256(grad_desc0, R0, s.GZ, wm, c.st));
+  }
+  if (grad_desc1) {
+    TR_HIP(linear_dgrad(c, s.GMD + o1, D, R - R0, D, Wf, D, grad_desc1, D));
+    TR_HIP(rank1_add256(grad_desc1, R - R0, s.GZ + R0, wm, c.st));
+  }
+  // TokenConfidence (:108-122): logits = token(desc.detach()) -> gradients of the token Linear only
+  if (grad_token0 || grad_token1) {
+    const std::string t = "token_confidence." + std::to_string(layer) + ".token.0";
+    if (grad_token0) TR_HIP(hipMemcpyAsync(s.GT, grad_token0, (size_t)R0 * 4, hipMemcpyDeviceToDevice, c.st));
+    else TR_HIP(hipMemsetAsync(s.GT, 0, (size_t)R0 * 4, c.st));
+    if (grad_token1) TR_HIP(hipMemcpyAsync(s.GT + R0, grad_token1, (size_t)(R - R0) * 4, hipMemcpyDeviceToDevice, c.st));
+    else TR_HIP(hipMemsetAsync(s.GT + R0, 0, (size_t)(R - R0) * 4, c.st));
+    if (float* g = P.gr(t + ".weight")) TR_HIP(colsum(s.X, D, R, D, s.GT, c.part, g, c.st));
+    if (float* g = P.gr(t + ".bias")) TR_HIP(colsum(s.GT, 1, R, 1, nullptr, c.part, g, c.st));
+  }
+  return LG_OK;
+}
+
+// ------------------------------------------------------------------ kernel-level entries (tests)
+int lg_train_gemm_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t batch, size_t* bytes) {
+  if (!bytes || M < 0 || N < 0 || K < 0 || batch < 0) return fail(LG_E_INVALID, "bad argument");
+  *bytes = tgemm_ws_floats(M, N, K, batch) * sizeof(float);
+  return LG_OK;
+}
+
+int lg_train_gemm(const float* A, const float* Bm, float* C, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA,
+                  int64_t sB, int64_t sC, int32_t M, int32_t N, int32_t K, int32_t batch, float alpha, float beta,
+                  const float* bias, int32_t ta, int32_t tb, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!A || !Bm || !C || M < 0 || N < 0 || K < 0 || batch < 0) return fail(LG_E_INVALID, "bad argument");
+  TGemm g{A, Bm, C, lda, ldb, ldc, sA, sB, sC, M, N, K, batch, alpha, beta, bias};
+  TR_HIP(tgemm(g, ta != 0, tb != 0, (float*)workspace, workspace_bytes / sizeof(float), (hipStream_t)stream));
+  TR_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return LG_OK;
+}
+
+int lg_train_attention(const float* q, const float* k, const float* v, int32_t B, int32_t H, int32_t Nq, int32_t Nk,
+                       float scale, float* o, float* lse, void* stream) {
+  if (!q || !k || !v || !o || !lse || B < 0 || H <= 0 || H * 64 != D || Nq < 0 || Nk <= 0)
+    return fail(LG_E_INVALID, "bad argument");
+  TR_HIP(tattn_forward(attn_args(q, k, v, o, lse, B, H, Nq, Nk, scale), (hipStream_t)stream));
+  TR_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return LG_OK;
+}
+
+int lg_train_attention_backward(const float* q, const float* k, const float* v, const float* o, const float* lse,
+                                const float* grad_o, int32_t B, int32_t H, int32_t Nq, int32_t Nk, float scale,
+                                float* grad_q, float* grad_k, float* grad_v, float* delta_ws, void* stream) {
+  if (!q || !k || !v || !o || !lse || !grad_o || !grad_q || !grad_k || !grad_v || !delta_ws || B < 0 || H <= 0 ||
+      H * 64 != D || Nq < 0 || Nk <= 0)
+    return fail(LG_E_INVALID, "bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  TR_HIP(attn_delta(o, grad_o, D, B, H, Nq, delta_ws, st));
+  TR_HIP(hipMemsetAsync(grad_q, 0, (size_t)B * Nq * D * 4, st));
+  TAttn a = attn_args(q, k, v, (float*)o, (float*)lse, B, H, Nq, Nk, scale);
+  a.dO = grad_o;
+  a.delta = delta_ws;
+  a.dQ = grad_q;
+  a.dK = grad_k;
+  a.dV = grad_v;
+  TR_HIP(tattn_backward(a, st));
+  TR_HIP(hipStreamSynchronize(st));
+  return LG_OK;
+}
+
+}  // extern "C"

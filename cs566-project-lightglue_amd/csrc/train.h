@@ -1,0 +1,130 @@
+// Host-visible launch wrappers of the training (autograd) kernels in train.hip (internal to
+// liblightglue_mi355x.so).  Every kernel computes in fp32: the products run on the f32-input
+// matrix cores (v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation, full fp32 range, so
+// gradients of any magnitude need no range scaling); reductions are deterministic (fixed-order
+// partial sums) except the attention backward's dQ, which is summed with float atomics.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace lg {
+
+// C[b] = alpha * (op(A[b]) op(B[b]) + bias) + beta * C[b]    (b < batch; bias [N] or null)
+//   op(A)(m,k) = ta ? A[k*lda + m] : A[m*lda + k]      (M x K)
+//   op(B)(k,n) = tb ? B[n*ldb + k] : B[k*ldb + n]      (K x N)
+// A linear layer y = x W^T + b is (ta=0, tb=1); its input gradient dx = dy W is (0, 0); its weight
+// gradient dW = dy^T x is (1, 0) -- K = rows, split over workgroups when the output has few tiles
+// (fixed-order partial sums in `ws`, tgemm_ws_floats).
+struct TGemm {
+  const float* A;
+  const float* B;
+  float* C;
+  long long lda, ldb, ldc;
+  long long sA, sB, sC;  // batch strides (elements)
+  int M, N, K, batch;
+  float alpha, beta;
+  const float* bias;
+};
+size_t tgemm_ws_floats(int M, int N, int K, int batch);
+hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st);
+
+// Attention on row-major fp32 tensors (row stride ld*, head h at columns [64h, 64h+64)); item
+// (b, h): queries rows [b*Nq, (b+1)*Nq) of Q, keys / values rows [b*Nk, (b+1)*Nk) of K / V.
+//   forward:  O = softmax(scale Q K^T) V, lse = log2 sum exp2(c Q K^T) per (item, query), c = scale log2 e
+//   backward: with delta = rowsum(dO * O) per (item, query) (attn_delta):
+//             dQ += scale dS K (float atomics: dQ must hold its initial value),
+//             dK (+)= scale dS^T Q, dV (+)= P^T dO (accum_kv: add to what dK / dV hold)
+struct TAttn {
+  const float* Q;
+  const float* K;
+  const float* V;
+  float* O;
+  float* lse;  // [B*H][Nq]
+  const float* dO;
+  const float* delta;  // [B*H][Nq]
+  float* dQ;
+  float* dK;
+  float* dV;
+  int ldq, ldk, ldv, ldo;
+  int B, H, Nq, Nk;
+  float scale;
+  int accum_kv;
+};
+hipError_t tattn_forward(const TAttn& a, hipStream_t st);
+hipError_t tattn_backward(const TAttn& a, hipStream_t st);
+// delta[(b*H + h)*Nq + q] = sum_d dO[(b*Nq+q)*ldo + 64h + d] * O[same]
+hipError_t attn_delta(const float* O, const float* dO, int ldo, int B, int H, int Nq, float* delta, hipStream_t st);
+
+// SelfBlock qkv split + rotary (lightglue.py:184-188): qkv [R][768] in the reference layout
+// (column h*192 + d*3 + t, :185) -> Q, K rotated by (cos, sin) [R][32], V; [R][256] each.
+hipError_t rotary_split(const float* qkv, const float* cosb, const float* sinb, int R, int H, float* Q, float* K,
+                        float* V, hipStream_t st);
+// its backward: gQKV [R][768] from gQ, gK, gV and the rotated Q, K; gcos / gsin [R][32] +=.
+hipError_t rotary_split_bwd(const float* gQ, const float* gK, const float* gV, const float* Q, const float* K,
+                            const float* cosb, const float* sinb, int R, int H, float* gQKV, float* gcos, float* gsin,
+                            hipStream_t st);
+
+// Positional encoding of one image set (lightglue.py:21-33,63-77): x [rows][4] (normalised
+// position, scale, ori) and cos / sin [rows][32]; `size` [B][2] (w, h) is required (callers run
+// kpt_extent for the min/max fallback).
+struct TPE {
+  const float* kpts;
+  const float* size;
+  const float* scales;
+  const float* oris;
+  const float* Wr;  // [32][m_in]
+  const float* Wc;  // [32]
+  const float* bc;  // [32]
+  int B, n, m_in;
+  float* x;
+  float* cosb;
+  float* sinb;
+};
+hipError_t pe_train(const TPE& p, hipStream_t st);
+// d(loss)/d(Wr, Wc, bc) from gcos / gsin [R][32] over both image sets (rows < R0 have count n0,
+// the rest n1): partial sums per row block in `part` (pe_bwd_part_floats), then one ordered pass.
+size_t pe_bwd_part_floats(int R);
+hipError_t pe_backward(const float* x, const float* cosb, const float* sinb, const float* gcos, const float* gsin,
+                       int R, int R0, float n0, float n1, int m_in, float* part, float* gWr, float* gWc, float* gbc,
+                       hipStream_t st);
+
+// ffn.1 LayerNorm(512, eps 1e-5) + ffn.2 GELU(erf) (lightglue.py:171-176): out = GELU(LN(h));
+// stats [R][2] = (mean, rstd).  Backward: gh from gout; dgamma / dbeta through per-block partials.
+hipError_t lngelu_fwd(const float* h, const float* gamma, const float* beta, int R, float* out, float* stats,
+                      hipStream_t st);
+size_t lngelu_bwd_part_floats(int R);
+hipError_t lngelu_bwd(const float* gout, const float* h, const float* stats, const float* gamma, const float* beta,
+                      int R, float* gh, float* part, float* dgamma, float* dbeta, hipStream_t st);
+
+// out[c] = sum_r s[r] * G[r*ld + c] (s null: 1), c < cols; fixed-order two-pass reduction.
+size_t colsum_part_floats(int rows, int cols);
+hipError_t colsum(const float* G, long long ld, int rows, int cols, const float* s, float* part, float* out,
+                  hipStream_t st);
+
+// y[r] = x[r] . w + b (256 wide; Linear(256 -> 1), matchability / token confidence)
+hipError_t gemv256(const float* x, int rows, const float* w, const float* b, float* y, hipStream_t st);
+// G[r][c] += s[r] * w[c] (256 wide)
+hipError_t rank1_add256(float* G, int rows, const float* s, const float* w, hipStream_t st);
+// C[i] = A[i] + B[i] over rows x 256 with row strides lda / ldb / ldc
+hipError_t add_rows256(const float* A, long long lda, const float* B, long long ldb, float* C, long long ldc, int rows,
+                       hipStream_t st);
+
+// GX rows += the layer-`layer` slices of g0 [B][L][M][256] (image-0 rows) / g1 [B][L][N][256]
+hipError_t add_layer_rows(float* GX, const float* g0, const float* g1, int B, int M, int N, int L, int layer,
+                          hipStream_t st);
+
+// ---- assignment head backward (MatchAssignment + sigmoid_log_double_softmax, lightglue.py:284-315)
+// sim [B][M][N]: lser [B*M], lsec [B*N] natural-log row / column logsumexp
+hipError_t sim_lse(const float* sim, int B, int M, int N, float* lser, float* lsec, hipStream_t st);
+// Gradient of the log assignment T [B][M+1][N+1] scaled per pair (s_in for the inner block,
+// s_dust for the dustbins; null = 1): rs [B*M] / cs [B*N] = scaled inner row / column sums,
+// gd0 [B*M] / gd1 [B*N] = scaled dustbin entries.
+hipError_t la_grad_sums(const float* T, const float* s_in, const float* s_dust, int B, int M, int N, float* rs,
+                        float* cs, float* gd0, float* gd1, hipStream_t st);
+// In place: sim -> d(loss)/d(sim) = 2 g - softmax_row * rs - softmax_col * cs (+ gsim_ext);
+// gz0 [B*M] / gz1 [B*N] = d/d(matchability logits).
+hipError_t la_grad_sim(float* sim, const float* T, const float* s_in, const float* lser, const float* lsec,
+                       const float* rs, const float* cs, const float* gsim_ext, int B, int M, int N, hipStream_t st);
+hipError_t la_grad_z(const float* z, const float* rs, const float* gd, int rows, float* gz, hipStream_t st);
+
+}  // namespace lg

@@ -1,0 +1,1068 @@
+// Training (autograd) kernels for gfx950: the LightGlue backward pass (reference
+// gluefactory/models/matchers/lightglue.py:159-315 differentiated by torch autograd in
+// gluefactory/train.py:450) and the activation-saving training forward it needs.
+//
+// Arithmetic: fp32 throughout.  The matrix products use v_mfma_f32_32x32x2_f32 (exact fp32
+// products, fp32 accumulation in k order; MI355X_MICROARCH.md / cdna_hip_programming.md
+// "FP32-input MFMA"), so a gradient of any magnitude is represented as fp32 represents it: no
+// range scaling, no split operands.  Lane map (common.h row32): A[l&31][l>>5], B[l>>5][l&31],
+// accumulator register r of lane l = C[row32(r, l>>5)][l&31].
+#include <algorithm>
+#include <cmath>
+
+#include "common.h"
+#include "train.h"
+
+namespace lg {
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// ============================================================================ GEMM
+// 128 x 128 x 32 block tile, 4 waves of 64 x 64 (2 x 2 tiles of 32 x 32).  Both operands are
+// staged in LDS k-major ([k][128 + 32]): a lane reads column (tile base + lane&31) of k-row
+// 2s + (lane>>5); the 160-float row pitch puts the two lane halves on disjoint bank halves.
+// Operands stored the other way round (m-major in memory) are transposed on the LDS write.
+constexpr int TG_BM = 128, TG_BN = 128, TG_BK = 32, TG_P = 160;
+
+struct TGemmK {
+  TGemm g;
+  int ksplit, kchunk;
+  int vecA, vecB;
+  float* part;  // [batch][ksplit][M][N] when ksplit > 1
+};
+
+// X(i, k) for i in [i0, i0 + 128), k in [k0, k0 + 32): KMAJ -> X[k*ld + i], else X[i*ld + k]
+template <bool KMAJ>
+__device__ __forceinline__ void tg_load(const float* X, long long ld, int i0, int D, int k0, int kend, int vec, int t,
+                                        f32x4 (&r)[4]) {
+  if (KMAJ) {
+    const int kr = t >> 5, i = i0 + (t & 31) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k0 + kr + 8 * q;
+      if (vec && k < kend && i + 3 < D) {
+        r[q] = *reinterpret_cast<const f32x4*>(X + (long long)k * ld + i);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[q][e] = (k < kend && i + e < D) ? X[(long long)k * ld + i + e] : 0.f;
+      }
+    }
+  } else {
+    const int ir = t >> 3, k = k0 + (t & 7) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + ir + 32 * q;
+      if (vec && i < D && k + 3 < kend) {
+        r[q] = *reinterpret_cast<const f32x4*>(X + (long long)i * ld + k);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[q][e] = (i < D && k + e < kend) ? X[(long long)i * ld + k + e] : 0.f;
+      }
+    }
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ void tg_store(float* S, int t, const f32x4 (&r)[4]) {
+  if (KMAJ) {
+    const int kr = t >> 5, i4 = (t & 31) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(S + (kr + 8 * q) * TG_P + i4) = r[q];
+  } else {
+    const int ir = t >> 3, k4 = (t & 7) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) S[(k4 + e) * TG_P + ir + 32 * q] = r[q][e];
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void tgemm_kernel(TGemmK p) {
+  __shared__ __attribute__((aligned(16))) float As[2][TG_BK * TG_P];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TG_BK * TG_P];
+  const TGemm& g = p.g;
+  const int t = threadIdx.x;
+  const int z = blockIdx.z, bat = z / p.ksplit, ks = z - bat * p.ksplit;
+  const float* A = g.A + bat * g.sA;
+  const float* B = g.B + bat * g.sB;
+  const int m0 = blockIdx.x * TG_BM, n0 = blockIdx.y * TG_BN;
+  const int kbeg = ks * p.kchunk, kend = min(g.K, kbeg + p.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + TG_BK - 1) / TG_BK : 0;
+  const int w = t >> 6, l = t & 63, h = l >> 5, l32 = l & 31;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+  f32x4 ra[4], rb[4];
+  if (nk > 0) {
+    tg_load<TA>(A, g.lda, m0, g.M, kbeg, kend, p.vecA, t, ra);
+    tg_load<!TB>(B, g.ldb, n0, g.N, kbeg, kend, p.vecB, t, rb);
+    tg_store<TA>(As[0], t, ra);
+    tg_store<!TB>(Bs[0], t, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      const int k0 = kbeg + (kt + 1) * TG_BK;
+      tg_load<TA>(A, g.lda, m0, g.M, k0, kend, p.vecA, t, ra);
+      tg_load<!TB>(B, g.ldb, n0, g.N, k0, kend, p.vecB, t, rb);
+    }
+    const float* as = As[cur] + wm + l32;
+    const float* bs = Bs[cur] + wn + l32;
+#pragma unroll
+    for (int s = 0; s < TG_BK / 2; ++s) {
+      const int kk = (2 * s + h) * TG_P;
+      const float a0 = as[kk], a1 = as[kk + 32], b0 = bs[kk], b1 = bs[kk + 32];
+      acc[0][0] = mfma32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32(a1, b1, acc[1][1]);
+    }
+    if (kt + 1 < nk) {
+      tg_store<TA>(As[cur ^ 1], t, ra);
+      tg_store<!TB>(Bs[cur ^ 1], t, rb);
+    }
+    __syncthreads();
+  }
+  float* C = g.C + bat * g.sC;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + l32;
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + row32(r, h);
+        if (row >= g.M) continue;
+        const float v = acc[i][j][r];
+        if (p.ksplit > 1) {
+          p.part[((long long)z * g.M + row) * g.N + col] = v;
+        } else {
+          float o = g.alpha * (g.bias ? v + g.bias[col] : v);
+          float* cp = C + (long long)row * g.ldc + col;
+          if (g.beta != 0.f) o = fmaf(g.beta, *cp, o);
+          *cp = o;
+        }
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void tgemm_reduce_kernel(TGemmK p) {
+  const TGemm& g = p.g;
+  const long long MN = (long long)g.M * g.N;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= MN * g.batch) return;
+  const int bat = (int)(idx / MN);
+  const long long e = idx - bat * MN;
+  const int row = (int)(e / g.N), col = (int)(e - (long long)row * g.N);
+  const float* src = p.part + (long long)bat * p.ksplit * MN + e;
+  float v = 0.f;
+  for (int s = 0; s < p.ksplit; ++s) v += src[s * MN];
+  float o = g.alpha * (g.bias ? v + g.bias[col] : v);
+  float* cp = g.C + bat * g.sC + (long long)row * g.ldc + col;
+  if (g.beta != 0.f) o = fmaf(g.beta, *cp, o);
+  *cp = o;
+}
+
+int tgemm_split(int M, int N, int K, int batch, int& kchunk) {
+  const long long tiles = (long long)((M + TG_BM - 1) / TG_BM) * ((N + TG_BN - 1) / TG_BN) * batch;
+  int ks = 1;
+  if (tiles < 512 && K >= 1024) {
+    ks = (int)std::min<long long>((1024 + tiles - 1) / tiles, K / 512);
+    ks = std::max(ks, 1);
+    // bound the partial buffer (32 Mi floats)
+    while (ks > 1 && (long long)ks * M * N * batch > (32ll << 20)) --ks;
+  }
+  kchunk = ((K + ks - 1) / ks + TG_BK - 1) / TG_BK * TG_BK;
+  ks = (K + kchunk - 1) / kchunk;
+  return std::max(ks, 1);
+}
+
+// ============================================================================ attention
+// Forward: a workgroup = 4 waves x 32 queries of one (pair, head); the query sits on the MFMA
+// lane (S^T = K Q^T), so the online softmax runs in-register per lane (the two lane halves hold
+// different keys of the same query: one v_permlane32_swap per max) and P^T is directly the B
+// operand of O^T = V^T P^T (the permuted key order row32 on both operands).  K / V tiles of 64
+// keys double-buffered in LDS (pitches 66 / 72: conflict-free for the two read patterns).
+constexpr int TA_KP = 66, TA_VP = 72;
+
+__device__ __forceinline__ void load_head_row_frag(const float* row, int h, float (&f)[32]) {
+  // f[s] = row[2s + h], s < 32, from 16 float4 loads of the 64-float head row
+#pragma unroll
+  for (int s4 = 0; s4 < 16; ++s4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(row + 4 * s4);
+    f[2 * s4] = h ? v[1] : v[0];
+    f[2 * s4 + 1] = h ? v[3] : v[2];
+  }
+}
+
+__global__ __launch_bounds__(256) void tattn_fwd_kernel(TAttn a) {
+  __shared__ __attribute__((aligned(16))) float Ks[2][64 * TA_KP];
+  __shared__ __attribute__((aligned(16))) float Vs[2][64 * TA_VP];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, l32 = l & 31;
+  const int item = blockIdx.y, b = item / a.H, hd = item - b * a.H;
+  const float* Q = a.Q + (long long)b * a.Nq * a.ldq + hd * 64;
+  const float* K = a.K + (long long)b * a.Nk * a.ldk + hd * 64;
+  const float* V = a.V + (long long)b * a.Nk * a.ldv + hd * 64;
+  const int qrow = blockIdx.x * 128 + w * 32 + l32;
+  const bool qv = qrow < a.Nq;
+  const float c = a.scale * kLog2e;
+  float qf[32];
+  if (qv) {
+    load_head_row_frag(Q + (long long)qrow * a.ldq, h, qf);
+#pragma unroll
+    for (int s = 0; s < 32; ++s) qf[s] *= c;
+  } else {
+#pragma unroll
+    for (int s = 0; s < 32; ++s) qf[s] = 0.f;
+  }
+  // K / V tile staging: 64 rows x 64 floats; thread t -> rows (t>>4) + 16q, columns 4(t&15)..+3
+  const int sr = t >> 4, sc = (t & 15) * 4;
+  f32x4 rk[4], rv[4];
+  auto load_kv = [&](int kt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int key = kt * 64 + sr + 16 * q;
+      if (key < a.Nk) {
+        rk[q] = *reinterpret_cast<const f32x4*>(K + (long long)key * a.ldk + sc);
+        rv[q] = *reinterpret_cast<const f32x4*>(V + (long long)key * a.ldv + sc);
+      } else {
+        rk[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        rv[q] = rk[q];
+      }
+    }
+  };
+  auto store_kv = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float* kp = Ks[st] + (sr + 16 * q) * TA_KP + sc;
+      *reinterpret_cast<f32x2*>(kp) = f32x2{rk[q][0], rk[q][1]};
+      *reinterpret_cast<f32x2*>(kp + 2) = f32x2{rk[q][2], rk[q][3]};
+      *reinterpret_cast<f32x4*>(Vs[st] + (sr + 16 * q) * TA_VP + sc) = rv[q];
+    }
+  };
+  const int nkt = (a.Nk + 63) / 64;
+  float m = -INFINITY, lsum = 0.f;
+  f32x16 ot[2] = {zero16(), zero16()};
+  load_kv(0);
+  store_kv(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) load_kv(kt + 1);
+    const float* ks = Ks[cur];
+    f32x16 st[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const float k0 = ks[l32 * TA_KP + 2 * s + h];
+      const float k1 = ks[(32 + l32) * TA_KP + 2 * s + h];
+      st[0] = mfma32(k0, qf[s], st[0]);
+      st[1] = mfma32(k1, qf[s], st[1]);
+    }
+    if (kt * 64 + 64 > a.Nk) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kt * 64 + 32 * tt + row32(r, h) >= a.Nk) st[tt][r] = -INFINITY;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[tt][r]);
+    mx = max_xor32(mx);
+    const float mn = fmaxf(m, mx);
+    const float base = mn == -INFINITY ? 0.f : mn;
+    const float f = exp2f(m - base);
+    lsum *= f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      ot[0][r] *= f;
+      ot[1][r] *= f;
+    }
+    m = mn;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = exp2f(st[tt][r] - base);
+        st[tt][r] = pv;
+        lsum += pv;
+      }
+    const float* vs = Vs[cur];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float* vr = vs + (32 * tt + row32(r, h)) * TA_VP + l32;
+        ot[0] = mfma32(vr[0], st[tt][r], ot[0]);
+        ot[1] = mfma32(vr[32], st[tt][r], ot[1]);
+      }
+    if (kt + 1 < nkt) store_kv(cur ^ 1);
+    __syncthreads();
+  }
+  lsum = sum_xor32(lsum);
+  if (!qv) return;
+  const float inv = 1.f / lsum;
+  float* O = a.O + ((long long)b * a.Nq + qrow) * a.ldo + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = ot[dt][4 * g4 + e] * inv;
+      *reinterpret_cast<f32x4*>(O + 32 * dt + 8 * g4 + 4 * h) = v;
+    }
+  if (h == 0) a.lse[(long long)item * a.Nq + qrow] = m + log2f(lsum);
+}
+
+// Backward: a workgroup = 4 waves x 32 keys of one (pair, head); the key sits on the lane, so S
+// and dP come out with their columns = keys and are directly the B operands of dV^T += dO^T P and
+// dK^T += Q^T dS (permuted query order row32 on both operands).  Row constants seed the
+// accumulators (S' = Q (cK)^T - lse, dP' = dO V^T - delta), so p = exp2(S') and dS = p * dP'
+// need no further VALU.  dQ: dS crosses LDS once, each wave multiplies a 32 x 32 quarter of the
+// (32 queries x 64 dims) tile over 64 of the workgroup's 128 keys, and adds it with float
+// atomics (two 128-B row segments per instruction: the full atomic rate).
+constexpr int TB_QP = 66, TB_KP = 66, TB_DP = 136;
+
+__global__ __launch_bounds__(256) void tattn_bwd_kernel(TAttn a) {
+  __shared__ __attribute__((aligned(16))) float Qs[2][32 * TB_QP];
+  __shared__ __attribute__((aligned(16))) float dOs[2][32 * TB_QP];
+  __shared__ __attribute__((aligned(16))) float Kall[128 * TB_KP];
+  __shared__ __attribute__((aligned(16))) float dSs[32 * TB_DP];
+  __shared__ float lse_s[2][32], del_s[2][32];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, l32 = l & 31;
+  const int item = blockIdx.y, b = item / a.H, hd = item - b * a.H;
+  const float* Q = a.Q + (long long)b * a.Nq * a.ldq + hd * 64;
+  const float* dO = a.dO + (long long)b * a.Nq * a.ldo + hd * 64;
+  const float* K = a.K + (long long)b * a.Nk * a.ldk + hd * 64;
+  const float* V = a.V + (long long)b * a.Nk * a.ldv + hd * 64;
+  const float* lse = a.lse + (long long)item * a.Nq;
+  const float* del = a.delta + (long long)item * a.Nq;
+  const int kb0 = blockIdx.x * 128;
+  const int key = kb0 + w * 32 + l32;
+  const bool kv = key < a.Nk;
+  const float c = a.scale * kLog2e;
+  float kf[32], vf[32];
+  if (kv) {
+    load_head_row_frag(K + (long long)key * a.ldk, h, kf);
+    load_head_row_frag(V + (long long)key * a.ldv, h, vf);
+#pragma unroll
+    for (int s = 0; s < 32; ++s) kf[s] *= c;
+  } else {
+#pragma unroll
+    for (int s = 0; s < 32; ++s) kf[s] = vf[s] = 0.f;
+  }
+  // the workgroup's 128 keys (unscaled) for dQ: thread t -> rows (t>>4) + 16q, q < 8
+  {
+    const int sr = t >> 4, sc = (t & 15) * 4;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = kb0 + sr + 16 * q;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (k < a.Nk) v = *reinterpret_cast<const f32x4*>(K + (long long)k * a.ldk + sc);
+      float* kp = Kall + (sr + 16 * q) * TB_KP + sc;
+      *reinterpret_cast<f32x2*>(kp) = f32x2{v[0], v[1]};
+      *reinterpret_cast<f32x2*>(kp + 2) = f32x2{v[2], v[3]};
+    }
+  }
+  // query tiles: 32 rows x 64 floats of Q and dO; thread t -> rows (t>>4) + 16q, q < 2
+  const int sr = t >> 4, sc = (t & 15) * 4;
+  f32x4 rq[2], rd[2];
+  float rl = 0.f, rdl = 0.f;
+  auto load_q = [&](int qt) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int qi = qt * 32 + sr + 16 * q;
+      if (qi < a.Nq) {
+        rq[q] = *reinterpret_cast<const f32x4*>(Q + (long long)qi * a.ldq + sc);
+        rd[q] = *reinterpret_cast<const f32x4*>(dO + (long long)qi * a.ldo + sc);
+      } else {
+        rq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        rd[q] = rq[q];
+      }
+    }
+    if (t < 32) {
+      const int qi = qt * 32 + t;
+      rl = qi < a.Nq ? lse[qi] : INFINITY;  // padded queries: p = exp2(-inf) = 0
+      rdl = qi < a.Nq ? del[qi] : 0.f;
+    }
+  };
+  auto store_q = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float* qp = Qs[st] + (sr + 16 * q) * TB_QP + sc;
+      float* dp = dOs[st] + (sr + 16 * q) * TB_QP + sc;
+      *reinterpret_cast<f32x2*>(qp) = f32x2{rq[q][0], rq[q][1]};
+      *reinterpret_cast<f32x2*>(qp + 2) = f32x2{rq[q][2], rq[q][3]};
+      *reinterpret_cast<f32x2*>(dp) = f32x2{rd[q][0], rd[q][1]};
+      *reinterpret_cast<f32x2*>(dp + 2) = f32x2{rd[q][2], rd[q][3]};
+    }
+    if (t < 32) {
+      lse_s[st][t] = rl;
+      del_s[st][t] = rdl;
+    }
+  };
+  f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
+  const int nqt = (a.Nq + 31) / 32;
+  const int qdt = w & 1, qkh = w >> 1;  // this wave's dQ quarter: dims 32*qdt.., keys 64*qkh..
+  float* dQ = a.dQ + (long long)b * a.Nq * a.ldq + hd * 64 + 32 * qdt + l32;
+  load_q(0);
+  store_q(0);
+  __syncthreads();
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int cur = qt & 1;
+    if (qt + 1 < nqt) load_q(qt + 1);
+    const float* qs = Qs[cur];
+    const float* dos = dOs[cur];
+    f32x16 sacc, pacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sacc[r] = -lse_s[cur][row32(r, h)];
+      pacc[r] = -del_s[cur][row32(r, h)];
+    }
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      sacc = mfma32(qs[l32 * TB_QP + 2 * s + h], kf[s], sacc);
+      pacc = mfma32(dos[l32 * TB_QP + 2 * s + h], vf[s], pacc);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = kv ? exp2f(sacc[r]) : 0.f;
+      sacc[r] = p;
+      pacc[r] *= p;  // dS (w.r.t. the scaled scores)
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = row32(r, h) * TB_QP + 32 * dt + l32;
+        dvt[dt] = mfma32(dos[qr], sacc[r], dvt[dt]);
+        dkt[dt] = mfma32(qs[qr], pacc[r], dkt[dt]);
+      }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dSs[row32(r, h) * TB_DP + w * 32 + l32] = pacc[r];
+    __syncthreads();
+    f32x16 qacc = zero16();
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const int kl = qkh * 64 + 2 * s + h;
+      qacc = mfma32(dSs[l32 * TB_DP + kl], Kall[kl * TB_KP + 32 * qdt + l32], qacc);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = qt * 32 + row32(r, h);
+      if (qi < a.Nq) atomicAdd(dQ + (long long)qi * a.ldq, qacc[r] * a.scale);
+    }
+    if (qt + 1 < nqt) store_q(cur ^ 1);
+    __syncthreads();
+  }
+  if (!kv) return;
+  float* dK = a.dK + ((long long)b * a.Nk + key) * a.ldk + hd * 64;
+  float* dV = a.dV + ((long long)b * a.Nk + key) * a.ldv + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * dt + 8 * g4 + 4 * h;
+      f32x4 vk, vv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        vk[e] = dkt[dt][4 * g4 + e] * a.scale;
+        vv[e] = dvt[dt][4 * g4 + e];
+      }
+      if (a.accum_kv) {
+        vk += *reinterpret_cast<const f32x4*>(dK + d0);
+        vv += *reinterpret_cast<const f32x4*>(dV + d0);
+      }
+      *reinterpret_cast<f32x4*>(dK + d0) = vk;
+      *reinterpret_cast<f32x4*>(dV + d0) = vv;
+    }
+}
+
+// one wave per query row: lanes 16h'..16h'+15 hold head h' (4 columns each)
+__global__ __launch_bounds__(256) void attn_delta_kernel(const float* O, const float* dO, int ldo, int B, int H, int Nq,
+                                                         float* delta) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (row >= B * Nq) return;
+  const int b = row / Nq, q = row - b * Nq;
+  float s = 0.f;
+  if (4 * l < 64 * H) {
+    const f32x4 o = *reinterpret_cast<const f32x4*>(O + (long long)row * ldo + 4 * l);
+    const f32x4 d = *reinterpret_cast<const f32x4*>(dO + (long long)row * ldo + 4 * l);
+    s = (o[0] * d[0] + o[1] * d[1]) + (o[2] * d[2] + o[3] * d[3]);
+  }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  const int hh = l >> 4;
+  if ((l & 15) == 0 && hh < H) delta[((long long)b * H + hh) * Nq + q] = s;
+}
+
+// ============================================================================ rotary
+// thread per (row, head, frequency f): dims 2f, 2f+1 of q, k, v are 6 consecutive floats of the
+// reference layout (column h*192 + d*3 + t)
+__global__ __launch_bounds__(256) void rotary_split_kernel(const float* qkv, const float* cosb, const float* sinb,
+                                                           int R, int H, float* Q, float* K, float* V) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (long long)R * H * 32) return;
+  const int f = (int)(id & 31);
+  const long long rh = id >> 5;
+  const int hd = (int)(rh % H);
+  const long long row = rh / H;
+  const float* x = qkv + row * (192ll * H) + hd * 192 + 6 * f;
+  const float c = cosb[row * 32 + f], s = sinb[row * 32 + f];
+  const float q0 = x[0], k0 = x[1], v0 = x[2], q1 = x[3], k1 = x[4], v1 = x[5];
+  const long long o = row * (64ll * H) + hd * 64 + 2 * f;
+  // t * cos + rotate_half(t) * sin (lightglue.py:36-43), unfused like the reference's ATen ops
+  *reinterpret_cast<f32x2*>(Q + o) = f32x2{__fadd_rn(__fmul_rn(q0, c), __fmul_rn(-q1, s)), __fadd_rn(__fmul_rn(q1, c), __fmul_rn(q0, s))};
+  *reinterpret_cast<f32x2*>(K + o) = f32x2{__fadd_rn(__fmul_rn(k0, c), __fmul_rn(-k1, s)), __fadd_rn(__fmul_rn(k1, c), __fmul_rn(k0, s))};
+  *reinterpret_cast<f32x2*>(V + o) = f32x2{v0, v1};
+}
+
+// thread per (row, f), looping over heads: gQKV and the encoding gradients (no atomics)
+__global__ __launch_bounds__(256) void rotary_split_bwd_kernel(const float* gQ, const float* gK, const float* gV,
+                                                               const float* Q, const float* K, const float* cosb,
+                                                               const float* sinb, int R, int H, float* gQKV,
+                                                               float* gcos, float* gsin) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (long long)R * 32) return;
+  const int f = (int)(id & 31);
+  const long long row = id >> 5;
+  const float c = cosb[id], s = sinb[id];
+  float gc = 0.f, gs = 0.f;
+  for (int hd = 0; hd < H; ++hd) {
+    const long long o = row * (64ll * H) + hd * 64 + 2 * f;
+    const f32x2 gq = *reinterpret_cast<const f32x2*>(gQ + o), gk = *reinterpret_cast<const f32x2*>(gK + o);
+    const f32x2 gv = *reinterpret_cast<const f32x2*>(gV + o);
+    const f32x2 qr = *reinterpret_cast<const f32x2*>(Q + o), kr = *reinterpret_cast<const f32x2*>(K + o);
+    // pre-rotation values t = R(-theta) out
+    const float q0 = qr[0] * c + qr[1] * s, q1 = qr[1] * c - qr[0] * s;
+    const float k0 = kr[0] * c + kr[1] * s, k1 = kr[1] * c - kr[0] * s;
+    gc += gq[0] * q0 + gq[1] * q1 + gk[0] * k0 + gk[1] * k1;
+    gs += gq[1] * q0 - gq[0] * q1 + gk[1] * k0 - gk[0] * k1;
+    float* x = gQKV + row * (192ll * H) + hd * 192 + 6 * f;
+    x[0] = gq[0] * c + gq[1] * s;
+    x[1] = gk[0] * c + gk[1] * s;
+    x[2] = gv[0];
+    x[3] = gq[1] * c - gq[0] * s;
+    x[4] = gk[1] * c - gk[0] * s;
+    x[5] = gv[1];
+  }
+  gcos[id] += gc;
+  gsin[id] += gs;
+}
+
+// ============================================================================ positional encoding
+__global__ __launch_bounds__(256) void pe_train_kernel(TPE p) {
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  const int f = gid & 31, pt = gid >> 5;
+  if (pt >= p.B * p.n) return;
+  const int b = pt / p.n;
+  const float w = p.size[b * 2], hh = p.size[b * 2 + 1];
+  const float scale = __fdiv_rn(fmaxf(w, hh), 2.f);  // normalize_keypoints (lightglue.py:29-32)
+  float x[4];
+  x[0] = __fdiv_rn(__fsub_rn(p.kpts[(long long)pt * 2], __fdiv_rn(w, 2.f)), scale);
+  x[1] = __fdiv_rn(__fsub_rn(p.kpts[(long long)pt * 2 + 1], __fdiv_rn(hh, 2.f)), scale);
+  x[2] = p.m_in == 4 ? p.scales[pt] : 0.f;
+  x[3] = p.m_in == 4 ? p.oris[pt] : 0.f;
+  const float* wr = p.Wr + f * p.m_in;
+  float pr = __fmul_rn(x[0], wr[0]);
+  for (int k = 1; k < p.m_in; ++k) pr = __fmaf_rn(x[k], wr[k], pr);
+  pr = __fadd_rn(pr, __fadd_rn(__fmul_rn((float)p.n, p.Wc[f]), p.bc[f]));  // + Lin(relu(n)) (:70-74)
+  p.cosb[(long long)pt * 32 + f] = cosf(pr);
+  p.sinb[(long long)pt * 32 + f] = sinf(pr);
+  if (f < 4) p.x[(long long)pt * 4 + f] = x[f];
+}
+
+constexpr int PE_ROWS = 256;  // rows per partial block
+// block: 256 threads = 8 row groups x 32 frequencies; partial [blk][32][6] = (gWr[0..3], gWc, gbc)
+__global__ __launch_bounds__(256) void pe_bwd_part_kernel(const float* x, const float* cosb, const float* sinb,
+                                                          const float* gcos, const float* gsin, int R, int R0, float n0,
+                                                          float n1, float* part) {
+  __shared__ float red[8][32][6];
+  const int f = threadIdx.x & 31, g = threadIdx.x >> 5;
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int r0 = blockIdx.x * PE_ROWS;
+  for (int r = r0 + g; r < min(R, r0 + PE_ROWS); r += 8) {
+    const long long i = (long long)r * 32 + f;
+    const float gp = cosb[i] * gsin[i] - sinb[i] * gcos[i];  // d/dproj of (cos proj, sin proj)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += gp * x[(long long)r * 4 + k];
+    acc[4] += gp * (r < R0 ? n0 : n1);
+    acc[5] += gp;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) red[g][f][k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < 32 * 6) {
+    const int ff = threadIdx.x / 6, k = threadIdx.x - ff * 6;
+    float s = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < 8; ++gg) s += red[gg][ff][k];
+    part[((long long)blockIdx.x * 32 + ff) * 6 + k] = s;
+  }
+}
+
+__global__ void pe_bwd_final_kernel(const float* part, int nblk, int m_in, float* gWr, float* gWc, float* gbc) {
+  const int id = threadIdx.x;  // 32 x 6
+  if (id >= 32 * 6) return;
+  const int f = id / 6, k = id - f * 6;
+  float s = 0.f;
+  for (int i = 0; i < nblk; ++i) s += part[((long long)i * 32 + f) * 6 + k];
+  if (k < m_in) gWr[f * m_in + k] = s;
+  else if (k == 4) gWc[f] = s;
+  else if (k == 5) gbc[f] = s;
+}
+
+// ============================================================================ LayerNorm + GELU
+__device__ __forceinline__ float gelu_exact(float y) { return 0.5f * y * (1.f + erff(y * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float y) {
+  return 0.5f * (1.f + erff(y * 0.70710678118654752f)) + y * 0.3989422804014327f * expf(-0.5f * y * y);
+}
+
+// one wave per row; lane holds columns [4l, 4l+4) and [256+4l, 256+4l+4)
+__global__ __launch_bounds__(256) void lngelu_fwd_kernel(const float* hin, const float* gamma, const float* beta,
+                                                         int R, float* out, float* stats) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (row >= R) return;
+  const float* x = hin + (long long)row * 512;
+  const f32x4 v0 = *reinterpret_cast<const f32x4*>(x + 4 * l), v1 = *reinterpret_cast<const f32x4*>(x + 256 + 4 * l);
+  const float mean = wave_sum((v0[0] + v0[1]) + (v0[2] + v0[3]) + (v1[0] + v1[1]) + (v1[2] + v1[3])) * (1.f / 512.f);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q += (v0[i] - mean) * (v0[i] - mean) + (v1[i] - mean) * (v1[i] - mean);
+  const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / 512.f) + 1e-5f);
+  const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + 4 * l), g1 = *reinterpret_cast<const f32x4*>(gamma + 256 + 4 * l);
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + 4 * l), b1 = *reinterpret_cast<const f32x4*>(beta + 256 + 4 * l);
+  f32x4 o0, o1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o0[i] = gelu_exact((v0[i] - mean) * rstd * g0[i] + b0[i]);
+    o1[i] = gelu_exact((v1[i] - mean) * rstd * g1[i] + b1[i]);
+  }
+  float* y = out + (long long)row * 512;
+  *reinterpret_cast<f32x4*>(y + 4 * l) = o0;
+  *reinterpret_cast<f32x4*>(y + 256 + 4 * l) = o1;
+  if (l == 0) *reinterpret_cast<f32x2*>(stats + 2ll * row) = f32x2{mean, rstd};
+}
+
+constexpr int LN_ROWS = 64;  // rows per workgroup (16 per wave) in the backward
+__global__ __launch_bounds__(256) void lngelu_bwd_kernel(const float* gout, const float* hin, const float* stats,
+                                                         const float* gamma, const float* beta, int R, float* gh,
+                                                         float* part) {
+  __shared__ float red[4][2][512];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + 4 * l), g1 = *reinterpret_cast<const f32x4*>(gamma + 256 + 4 * l);
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + 4 * l), b1 = *reinterpret_cast<const f32x4*>(beta + 256 + 4 * l);
+  f32x4 dg0 = {0.f, 0.f, 0.f, 0.f}, dg1 = dg0, db0 = dg0, db1 = dg0;
+  const int r0 = blockIdx.x * LN_ROWS + w * (LN_ROWS / 4);
+  for (int row = r0; row < min(R, r0 + LN_ROWS / 4); ++row) {
+    const float* x = hin + (long long)row * 512;
+    const float* go = gout + (long long)row * 512;
+    const f32x2 st = *reinterpret_cast<const f32x2*>(stats + 2ll * row);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(x + 4 * l), v1 = *reinterpret_cast<const f32x4*>(x + 256 + 4 * l);
+    const f32x4 o0 = *reinterpret_cast<const f32x4*>(go + 4 * l), o1 = *reinterpret_cast<const f32x4*>(go + 256 + 4 * l);
+    f32x4 xh0, xh1, gx0, gx1;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xh0[i] = (v0[i] - st[0]) * st[1];
+      xh1[i] = (v1[i] - st[0]) * st[1];
+      const float gy0 = o0[i] * gelu_grad(xh0[i] * g0[i] + b0[i]);
+      const float gy1 = o1[i] * gelu_grad(xh1[i] * g1[i] + b1[i]);
+      dg0[i] += gy0 * xh0[i];
+      dg1[i] += gy1 * xh1[i];
+      db0[i] += gy0;
+      db1[i] += gy1;
+      gx0[i] = gy0 * g0[i];
+      gx1[i] = gy1 * g1[i];
+      s1 += gx0[i] + gx1[i];
+      s2 += gx0[i] * xh0[i] + gx1[i] * xh1[i];
+    }
+    s1 = wave_sum(s1) * (1.f / 512.f);
+    s2 = wave_sum(s2) * (1.f / 512.f);
+    f32x4 r0v, r1v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      r0v[i] = st[1] * (gx0[i] - s1 - xh0[i] * s2);
+      r1v[i] = st[1] * (gx1[i] - s1 - xh1[i] * s2);
+    }
+    float* y = gh + (long long)row * 512;
+    *reinterpret_cast<f32x4*>(y + 4 * l) = r0v;
+    *reinterpret_cast<f32x4*>(y + 256 + 4 * l) = r1v;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    red[w][0][4 * l + i] = dg0[i];
+    red[w][0][256 + 4 * l + i] = dg1[i];
+    red[w][1][4 * l + i] = db0[i];
+    red[w][1][256 + 4 * l + i] = db1[i];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 1024; i += 256) {
+    const int k = i >> 9, cidx = i & 511;
+    part[((long long)blockIdx.x * 2 + k) * 512 + cidx] = (red[0][k][cidx] + red[1][k][cidx]) + (red[2][k][cidx] + red[3][k][cidx]);
+  }
+}
+
+// ============================================================================ column sums
+constexpr int CS_BLOCKS = 256;
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* G, long long ld, int rows, int cols,
+                                                          const float* s, int rpb, float* part) {
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    float acc = 0.f;
+    for (int r = r0; r < r1; ++r) {
+      const float v = G[(long long)r * ld + c];
+      acc = s ? fmaf(s[r], v, acc) : acc + v;
+    }
+    part[(long long)blockIdx.x * cols + c] = acc;
+  }
+}
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nblk, int cols, float* out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float acc = 0.f;
+  for (int i = 0; i < nblk; ++i) acc += part[(long long)i * cols + c];
+  out[c] = acc;
+}
+
+// ============================================================================ small row ops
+__global__ __launch_bounds__(256) void gemv256_kernel(const float* x, int rows, const float* w, const float* b,
+                                                      float* y) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (row >= rows) return;
+  const f32x4 v = *reinterpret_cast<const f32x4*>(x + (long long)row * 256 + 4 * l);
+  const f32x4 u = *reinterpret_cast<const f32x4*>(w + 4 * l);
+  const float s = wave_sum((v[0] * u[0] + v[1] * u[1]) + (v[2] * u[2] + v[3] * u[3]));
+  if (l == 0) y[row] = s + b[0];
+}
+
+__global__ __launch_bounds__(256) void rank1_add256_kernel(float* G, int rows, const float* s, const float* w) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (long long)rows * 64) return;
+  const long long row = id >> 6;
+  const int c4 = (int)(id & 63) * 4;
+  f32x4* p = reinterpret_cast<f32x4*>(G + row * 256 + c4);
+  const f32x4 u = *reinterpret_cast<const f32x4*>(w + c4);
+  const float sv = s[row];
+  f32x4 v = *p;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = fmaf(sv, u[e], v[e]);
+  *p = v;
+}
+
+__global__ __launch_bounds__(256) void add_rows256_kernel(const float* A, long long lda, const float* B, long long ldb,
+                                                          float* C, long long ldc, int rows) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (long long)rows * 64) return;
+  const long long row = id >> 6;
+  const int c4 = (int)(id & 63) * 4;
+  const f32x4 a = *reinterpret_cast<const f32x4*>(A + row * lda + c4);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(B + row * ldb + c4);
+  *reinterpret_cast<f32x4*>(C + row * ldc + c4) = a + b;
+}
+
+// ============================================================================ assignment head
+// row logsumexp: one wave per (pair, row)
+__global__ __launch_bounds__(256) void sim_lse_row_kernel(const float* sim, int rows, int N, float* lser) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* s = sim + (long long)row * N;
+  float m = -INFINITY;
+  for (int j = l; j < N; j += 64) m = fmaxf(m, s[j]);
+  m = wave_max(m);
+  float acc = 0.f;
+  for (int j = l; j < N; j += 64) acc += expf(s[j] - m);
+  acc = wave_sum(acc);
+  if (l == 0) lser[row] = m + logf(acc);
+}
+// column logsumexp: a thread per (pair, column) walks the rows (coalesced across the block)
+__global__ __launch_bounds__(256) void sim_lse_col_kernel(const float* sim, int B, int M, int N, float* lsec) {
+  const int j = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (j >= N) return;
+  const float* s = sim + (long long)b * M * N + j;
+  float m = -INFINITY;
+  for (int i = 0; i < M; ++i) m = fmaxf(m, s[(long long)i * N]);
+  float acc = 0.f;
+  for (int i = 0; i < M; ++i) acc += expf(s[(long long)i * N] - m);
+  lsec[(long long)b * N + j] = m + logf(acc);
+}
+
+__global__ __launch_bounds__(256) void la_row_sums_kernel(const float* T, const float* s_in, const float* s_dust, int B,
+                                                          int M, int N, float* rs, float* gd0) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (row >= B * M) return;
+  const int b = row / M, i = row - b * M;
+  const float* t = T + ((long long)b * (M + 1) + i) * (N + 1);
+  float acc = 0.f;
+  for (int j = l; j < N; j += 64) acc += t[j];
+  acc = wave_sum(acc);
+  if (l == 0) {
+    rs[row] = acc * (s_in ? s_in[b] : 1.f);
+    gd0[row] = t[N] * (s_dust ? s_dust[b] : 1.f);
+  }
+}
+__global__ __launch_bounds__(256) void la_col_sums_kernel(const float* T, const float* s_in, const float* s_dust, int B,
+                                                          int M, int N, float* cs, float* gd1) {
+  const int j = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (j >= N) return;
+  const float* t = T + (long long)b * (M + 1) * (N + 1) + j;
+  float acc = 0.f;
+  for (int i = 0; i < M; ++i) acc += t[(long long)i * (N + 1)];
+  cs[(long long)b * N + j] = acc * (s_in ? s_in[b] : 1.f);
+  gd1[(long long)b * N + j] = t[(long long)M * (N + 1)] * (s_dust ? s_dust[b] : 1.f);
+}
+
+__global__ __launch_bounds__(256) void la_grad_sim_kernel(float* sim, const float* T, const float* s_in,
+                                                          const float* lser, const float* lsec, const float* rs,
+                                                          const float* cs, const float* gext, int B, int M, int N) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long MN = (long long)M * N;
+  if (id >= MN * B) return;
+  const int b = (int)(id / MN);
+  const long long e = id - b * MN;
+  const int i = (int)(e / N), j = (int)(e - (long long)i * N);
+  const float g = T[((long long)b * (M + 1) + i) * (N + 1) + j] * (s_in ? s_in[b] : 1.f);
+  const float s = sim[id];
+  const long long ri = (long long)b * M + i, cj = (long long)b * N + j;
+  // la = s - lse_row + s - lse_col + ...  (lightglue.py:288-293)
+  float v = 2.f * g - expf(s - lser[ri]) * rs[ri] - expf(s - lsec[cj]) * cs[cj];
+  if (gext) v += gext[id];
+  sim[id] = v;
+}
+
+// d/dz of logsigmoid(z) (inner entries, summed: rs) and logsigmoid(-z) (the dustbin entry gd)
+__global__ __launch_bounds__(256) void la_grad_z_kernel(const float* z, const float* rs, const float* gd, int rows,
+                                                        float* gz) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows) return;
+  const float sp = 1.f / (1.f + expf(-z[i]));  // sigmoid(z)
+  gz[i] = (1.f - sp) * rs[i] - sp * gd[i];
+}
+
+// GX[r] += G_layer[pair][layer][point] for the layer-descriptor gradients [B][L][M or N][256]
+__global__ __launch_bounds__(256) void add_layer_rows_kernel(float* GX, const float* g0, const float* g1, int B, int M,
+                                                             int N, int L, int layer) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long R0 = (long long)B * M;
+  if (id >= (R0 + (long long)B * N) * 64) return;
+  const long long row = id >> 6;
+  const int c4 = (int)(id & 63) * 4;
+  const float* src;
+  if (row < R0) {
+    if (!g0) return;
+    const long long b = row / M, n = row - b * M;
+    src = g0 + ((b * L + layer) * M + n) * 256;
+  } else {
+    if (!g1) return;
+    const long long r2 = row - R0, b = r2 / N, n = r2 - b * N;
+    src = g1 + ((b * L + layer) * N + n) * 256;
+  }
+  f32x4* d = reinterpret_cast<f32x4*>(GX + row * 256 + c4);
+  *d = *d + *reinterpret_cast<const f32x4*>(src + c4);
+}
+
+inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace
+
+// ============================================================================ launchers
+size_t tgemm_ws_floats(int M, int N, int K, int batch) {
+  int kc = 0;
+  const int ks = tgemm_split(M, N, K, batch, kc);
+  return ks > 1 ? (size_t)ks * M * N * batch : 0;
+}
+
+hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return hipSuccess;
+  TGemmK p{};
+  p.g = g;
+  int kc = 0;
+  p.ksplit = tgemm_split(g.M, g.N, std::max(g.K, 1), g.batch, kc);
+  p.kchunk = kc;
+  if (p.ksplit > 1 && (!ws || (size_t)p.ksplit * g.M * g.N * g.batch > ws_floats)) {
+    p.ksplit = 1;
+    p.kchunk = std::max(g.K, 1);
+  }
+  p.part = ws;
+  auto aligned = [](const float* ptr, long long ld, long long sb) {
+    return ((uintptr_t)ptr % 16 == 0) && ld % 4 == 0 && sb % 4 == 0;
+  };
+  p.vecA = aligned(g.A, g.lda, g.sA);
+  p.vecB = aligned(g.B, g.ldb, g.sB);
+  const dim3 grid(cdiv(g.M, TG_BM), cdiv(g.N, TG_BN), g.batch * p.ksplit);
+  if (!ta && !tb) hipLaunchKernelGGL((tgemm_kernel<false, false>), grid, dim3(256), 0, st, p);
+  else if (!ta && tb) hipLaunchKernelGGL((tgemm_kernel<false, true>), grid, dim3(256), 0, st, p);
+  else if (ta && !tb) hipLaunchKernelGGL((tgemm_kernel<true, false>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((tgemm_kernel<true, true>), grid, dim3(256), 0, st, p);
+  if (p.ksplit > 1)
+    hipLaunchKernelGGL(tgemm_reduce_kernel, dim3(cdiv((long long)g.M * g.N * g.batch, 256)), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t tattn_forward(const TAttn& a, hipStream_t st) {
+  if (a.B * a.H == 0 || a.Nq == 0) return hipSuccess;
+  hipLaunchKernelGGL(tattn_fwd_kernel, dim3(cdiv(a.Nq, 128), a.B * a.H), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t tattn_backward(const TAttn& a, hipStream_t st) {
+  if (a.B * a.H == 0 || a.Nk == 0) return hipSuccess;
+  hipLaunchKernelGGL(tattn_bwd_kernel, dim3(cdiv(a.Nk, 128), a.B * a.H), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t attn_delta(const float* O, const float* dO, int ldo, int B, int H, int Nq, float* delta, hipStream_t st) {
+  if (B * Nq == 0) return hipSuccess;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv((long long)B * Nq, 4)), dim3(256), 0, st, O, dO, ldo, B, H, Nq, delta);
+  return hipGetLastError();
+}
+
+hipError_t rotary_split(const float* qkv, const float* cosb, const float* sinb, int R, int H, float* Q, float* K,
+                        float* V, hipStream_t st) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(rotary_split_kernel, dim3(cdiv((long long)R * H * 32, 256)), dim3(256), 0, st, qkv, cosb, sinb, R, H, Q,
+                     K, V);
+  return hipGetLastError();
+}
+
+hipError_t rotary_split_bwd(const float* gQ, const float* gK, const float* gV, const float* Q, const float* K,
+                            const float* cosb, const float* sinb, int R, int H, float* gQKV, float* gcos, float* gsin,
+                            hipStream_t st) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(rotary_split_bwd_kernel, dim3(cdiv((long long)R * 32, 256)), dim3(256), 0, st, gQ, gK, gV, Q, K, cosb,
+                     sinb, R, H, gQKV, gcos, gsin);
+  return hipGetLastError();
+}
+
+hipError_t pe_train(const TPE& p, hipStream_t st) {
+  if (p.B * p.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(pe_train_kernel, dim3(cdiv((long long)p.B * p.n * 32, 256)), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+size_t pe_bwd_part_floats(int R) { return (size_t)cdiv(std::max(R, 1), PE_ROWS) * 32 * 6; }
+
+hipError_t pe_backward(const float* x, const float* cosb, const float* sinb, const float* gcos, const float* gsin,
+                       int R, int R0, float n0, float n1, int m_in, float* part, float* gWr, float* gWc, float* gbc,
+                       hipStream_t st) {
+  const int nblk = (int)cdiv(std::max(R, 1), PE_ROWS);
+  hipLaunchKernelGGL(pe_bwd_part_kernel, dim3(nblk), dim3(256), 0, st, x, cosb, sinb, gcos, gsin, R, R0, n0, n1, part);
+  hipLaunchKernelGGL(pe_bwd_final_kernel, dim3(1), dim3(256), 0, st, part, nblk, m_in, gWr, gWc, gbc);
+  return hipGetLastError();
+}
+
+hipError_t lngelu_fwd(const float* h, const float* gamma, const float* beta, int R, float* out, float* stats,
+                      hipStream_t st) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(lngelu_fwd_kernel, dim3(cdiv(R, 4)), dim3(256), 0, st, h, gamma, beta, R, out, stats);
+  return hipGetLastError();
+}
+
+size_t lngelu_bwd_part_floats(int R) { return (size_t)cdiv(std::max(R, 1), LN_ROWS) * 2 * 512; }
+
+hipError_t lngelu_bwd(const float* gout, const float* h, const float* stats, const float* gamma, const float* beta,
+                      int R, float* gh, float* part, float* dgamma, float* dbeta, hipStream_t st) {
+  const int nblk = (int)cdiv(std::max(R, 1), LN_ROWS);
+  hipLaunchKernelGGL(lngelu_bwd_kernel, dim3(nblk), dim3(256), 0, st, gout, h, stats, gamma, beta, R, gh, part);
+  // dgamma = sum of the even partial rows, dbeta of the odd ones: [blk][2][512] read as [blk*2][512]
+  if (dgamma)
+    hipLaunchKernelGGL(colsum_part_kernel, dim3(1), dim3(256), 0, st, part, 1024ll, nblk, 512, (const float*)nullptr, nblk,
+                       dgamma);
+  if (dbeta)
+    hipLaunchKernelGGL(colsum_part_kernel, dim3(1), dim3(256), 0, st, part + 512, 1024ll, nblk, 512, (const float*)nullptr,
+                       nblk, dbeta);
+  return hipGetLastError();
+}
+
+size_t colsum_part_floats(int rows, int cols) { return (size_t)CS_BLOCKS * std::max(cols, 1); }
+
+hipError_t colsum(const float* G, long long ld, int rows, int cols, const float* s, float* part, float* out,
+                  hipStream_t st) {
+  if (cols == 0) return hipSuccess;
+  const int rpb = std::max(1, (int)cdiv(std::max(rows, 1), CS_BLOCKS));
+  const int nblk = (int)cdiv(std::max(rows, 1), rpb);
+  hipLaunchKernelGGL(colsum_part_kernel, dim3(nblk), dim3(256), 0, st, G, ld, rows, cols, s, rpb, part);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, st, part, nblk, cols, out);
+  return hipGetLastError();
+}
+
+hipError_t gemv256(const float* x, int rows, const float* w, const float* b, float* y, hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(gemv256_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, rows, w, b, y);
+  return hipGetLastError();
+}
+
+hipError_t rank1_add256(float* G, int rows, const float* s, const float* w, hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(rank1_add256_kernel, dim3(cdiv((long long)rows * 64, 256)), dim3(256), 0, st, G, rows, s, w);
+  return hipGetLastError();
+}
+
+hipError_t add_rows256(const float* A, long long lda, const float* B, long long ldb, float* C, long long ldc, int rows,
+                       hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(add_rows256_kernel, dim3(cdiv((long long)rows * 64, 256)), dim3(256), 0, st, A, lda, B, ldb, C, ldc,
+                     rows);
+  return hipGetLastError();
+}
+
+hipError_t add_layer_rows(float* GX, const float* g0, const float* g1, int B, int M, int N, int L, int layer,
+                          hipStream_t st) {
+  const long long n = (long long)B * (M + N) * 64;
+  if (n == 0 || (!g0 && !g1)) return hipSuccess;
+  hipLaunchKernelGGL(add_layer_rows_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, GX, g0, g1, B, M, N, L, layer);
+  return hipGetLastError();
+}
+
+hipError_t sim_lse(const float* sim, int B, int M, int N, float* lser, float* lsec, hipStream_t st) {
+  if (B * M == 0 || N == 0) return hipSuccess;
+  hipLaunchKernelGGL(sim_lse_row_kernel, dim3(cdiv((long long)B * M, 4)), dim3(256), 0, st, sim, B * M, N, lser);
+  hipLaunchKernelGGL(sim_lse_col_kernel, dim3(cdiv(N, 256), B), dim3(256), 0, st, sim, B, M, N, lsec);
+  return hipGetLastError();
+}
+
+hipError_t la_grad_sums(const float* T, const float* s_in, const float* s_dust, int B, int M, int N, float* rs,
+                        float* cs, float* gd0, float* gd1, hipStream_t st) {
+  if (B == 0) return hipSuccess;
+  if (M > 0)
+    hipLaunchKernelGGL(la_row_sums_kernel, dim3(cdiv((long long)B * M, 4)), dim3(256), 0, st, T, s_in, s_dust, B, M, N, rs,
+                       gd0);
+  if (N > 0)
+    hipLaunchKernelGGL(la_col_sums_kernel, dim3(cdiv(N, 256), B), dim3(256), 0, st, T, s_in, s_dust, B, M, N, cs, gd1);
+  return hipGetLastError();
+}
+
+hipError_t la_grad_sim(float* sim, const float* T, const float* s_in, const float* lser, const float* lsec,
+                       const float* rs, const float* cs, const float* gsim_ext, int B, int M, int N, hipStream_t st) {
+  const long long n = (long long)B * M * N;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(la_grad_sim_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, sim, T, s_in, lser, lsec, rs, cs, gsim_ext,
+                     B, M, N);
+  return hipGetLastError();
+}
+
+hipError_t la_grad_z(const float* z, const float* rs, const float* gd, int rows, float* gz, hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(la_grad_z_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, st, z, rs, gd, rows, gz);
+  return hipGetLastError();
+}
+
+}  // namespace lg

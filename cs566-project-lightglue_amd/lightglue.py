@@ -20,6 +20,14 @@ Deliberate behaviour differences from the reference:
 * with pruning and B > 1, ``log_assignment`` and ``ref_descriptors*`` are per-pair LISTS (pair b's
   kept block; the reference asserts B == 1, :528,533); ``kept0/1`` and ``stop_layer`` give the
   per-pair counts.
+
+Training (the reference differentiates this module with torch autograd, gluefactory/train.py:450):
+in training mode with gradients enabled, ``forward`` runs the activation-saving training forward
+of the HIP library (``lg_train_forward``) inside a ``torch.autograd.Function`` whose backward is
+the hand-written HIP backward (``lg_train_backward``); every ``MatchAssignment`` head is another
+Function (``lg_assignment_head`` forward, ``lg_head_backward`` backward), and :meth:`loss` fuses
+the NLL of each head into its head's backward (no dense d(loss)/d(log_assignment) is formed).
+Gradients reach every parameter and both descriptor inputs.
 """
 import ctypes
 import warnings
@@ -120,6 +128,154 @@ def _ptr(t):
 # [B, M, N] as pred["similarity"] (MatchAssignment's second output, lightglue.py:311,315; the input
 # of a Sinkhorn assignment head, configs[4]).
 EXTENSION_CONF = {"precision": "auto", "return_similarity": False}
+
+
+def _trunk_param(name):
+    return name.startswith(("input_proj.", "posenc.", "transformers."))
+
+
+class _TrainTrunk(torch.autograd.Function):
+    """LightGlue.forward in training mode (lightglue.py:444-579, :502-503 gating) up to the
+    per-layer descriptors ``ref_descriptors0/1`` [B, L, M, 256]; backward = lg_train_backward."""
+
+    @staticmethod
+    def forward(ctx, model, inputs, d0, d1, *params):
+        lib = model._ensure_handle(d0.device)
+        ctx.model, ctx.inputs = model, inputs
+        b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
+        L, dd = int(model.conf.n_layers), int(model.conf.descriptor_dim)
+        nb = ctypes.c_size_t()
+        _lib.check(lib.lg_train_saved_bytes(model._handle, b, m, n, ctypes.byref(nb)), "lg_train_saved_bytes")
+        saved = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=d0.device)
+        rd0 = torch.empty((b, L, m, dd), dtype=torch.float32, device=d0.device)
+        rd1 = torch.empty((b, L, n, dd), dtype=torch.float32, device=d0.device)
+        inp = model._lg_inputs(inputs, d0, d1)
+        stream = torch.cuda.current_stream(d0.device).cuda_stream
+        _lib.check(lib.lg_train_forward(model._handle, model._param_array(params), ctypes.byref(inp), _ptr(rd0), _ptr(rd1),
+                                        _ptr(saved), nb.value, ctypes.c_void_p(stream)), "lg_train_forward")
+        ctx.saved_buf = saved
+        ctx.save_for_backward(d0, d1, *params)
+        return rd0, rd1
+
+    @staticmethod
+    def backward(ctx, g_rd0, g_rd1):
+        model = ctx.model
+        d0, d1, *params = ctx.saved_tensors
+        lib = model._ensure_handle(d0.device)
+        b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
+        names = model._schema_names()
+        grads = [torch.empty_like(p) if (_trunk_param(nm) and ctx.needs_input_grad[4 + i]) else None
+                 for i, (nm, p) in enumerate(zip(names, params))]
+        gd0 = torch.empty_like(d0) if ctx.needs_input_grad[2] else None
+        gd1 = torch.empty_like(d1) if ctx.needs_input_grad[3] else None
+        nb = ctypes.c_size_t()
+        _lib.check(lib.lg_train_scratch_bytes(model._handle, b, m, n, ctypes.byref(nb)), "lg_train_scratch_bytes")
+        scratch = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=d0.device)
+        g_rd0 = None if g_rd0 is None else g_rd0.contiguous()
+        g_rd1 = None if g_rd1 is None else g_rd1.contiguous()
+        inp = model._lg_inputs(ctx.inputs, d0, d1)
+        stream = torch.cuda.current_stream(d0.device).cuda_stream
+        _lib.check(lib.lg_train_backward(model._handle, model._param_array(params), ctypes.byref(inp), _ptr(ctx.saved_buf),
+                                         ctx.saved_buf.numel(), _ptr(g_rd0), _ptr(g_rd1), model._param_array(grads),
+                                         _ptr(gd0), _ptr(gd1), _ptr(scratch), nb.value, ctypes.c_void_p(stream)),
+                   "lg_train_backward")
+        ctx.saved_buf = None
+        return (None, None, gd0, gd1, *grads)
+
+
+def _head_backward(model, layer, d0, d1, params, needs, la_grad, s_in, s_dust, g_sim, g_t0, g_t1):
+    """lg_head_backward for head ``layer``: (gd0, gd1, per-parameter grads or None)."""
+    lib = model._ensure_handle(d0.device)
+    b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
+    L = int(model.conf.n_layers)
+    li = layer % L
+    own = (f"log_assignment.{li}.",) + ((f"token_confidence.{li}.",) if (g_t0 is not None or g_t1 is not None) else ())
+    names = model._schema_names()
+    grads = [torch.empty_like(p) if (nm.startswith(own) and needs[i]) else None
+             for i, (nm, p) in enumerate(zip(names, params))]
+    gd0 = torch.empty_like(d0) if needs[-2] else None
+    gd1 = torch.empty_like(d1) if needs[-1] else None
+    nb = ctypes.c_size_t()
+    _lib.check(lib.lg_head_scratch_bytes(model._handle, b, m, n, ctypes.byref(nb)), "lg_head_scratch_bytes")
+    scratch = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=d0.device)
+    stream = torch.cuda.current_stream(d0.device).cuda_stream
+    c = lambda t: None if t is None else t.float().contiguous()  # noqa: E731
+    la_grad, s_in, s_dust, g_sim, g_t0, g_t1 = map(c, (la_grad, s_in, s_dust, g_sim, g_t0, g_t1))
+    _lib.check(lib.lg_head_backward(model._handle, model._param_array(params), int(li), _ptr(d0), _ptr(d1), b, m, n,
+                                    _ptr(la_grad), _ptr(s_in), _ptr(s_dust), _ptr(g_sim), _ptr(g_t0), _ptr(g_t1),
+                                    model._param_array(grads), _ptr(gd0), _ptr(gd1), _ptr(scratch), nb.value,
+                                    ctypes.c_void_p(stream)), "lg_head_backward")
+    return gd0, gd1, grads
+
+
+class _Head(torch.autograd.Function):
+    """``log_assignment[layer](desc0, desc1)`` (MatchAssignment + sigmoid_log_double_softmax,
+    lightglue.py:284-315) -> (log_assignment, similarity, token logits 0, token logits 1); the
+    token logits are TokenConfidence's Linear before its sigmoid (:109-110, detached inputs)."""
+
+    @staticmethod
+    def forward(ctx, model, layer, tokens, d0, d1, *params):
+        d0c, d1c = d0.float().contiguous(), d1.float().contiguous()
+        out = model.assignment_head(layer, d0c, d1c, token_logits=tokens)
+        la, sim = out[0], out[1]
+        t0, t1 = (out[2], out[3]) if tokens else (la.new_zeros(0), la.new_zeros(0))
+        ctx.model, ctx.layer, ctx.tokens = model, layer, tokens
+        ctx.save_for_backward(d0c, d1c, *params)
+        return la, sim, t0, t1
+
+    @staticmethod
+    def backward(ctx, g_la, g_sim, g_t0, g_t1):
+        d0, d1, *params = ctx.saved_tensors
+        if g_la is None:
+            b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
+            g_la = torch.zeros((b, m + 1, n + 1), device=d0.device)
+        if not ctx.tokens:
+            g_t0 = g_t1 = None
+        needs = list(ctx.needs_input_grad[5:]) + [ctx.needs_input_grad[3], ctx.needs_input_grad[4]]
+        gd0, gd1, grads = _head_backward(ctx.model, ctx.layer, d0, d1, params, needs, g_la, None, None, g_sim, g_t0, g_t1)
+        return (None, None, None, gd0, gd1, *grads)
+
+
+class _HeadNLL(torch.autograd.Function):
+    """One term of LightGlue.loss (lightglue.py:614-640): the NLL (losses.py:6-58) of head
+    ``layer`` on (desc0, desc1) with the ground-truth weights of losses.py:62-73.  Outputs (nll,
+    nll_pos, nll_neg, num_pos, num_neg, log_assignment, token logits 0, token logits 1); the loss is
+    linear in the log assignment, so the backward hands lg_head_backward the weights and two per-pair
+    scales instead of a dense gradient."""
+
+    @staticmethod
+    def forward(ctx, model, layer, data, balancing, tokens, d0, d1, *params):
+        from .superglue import _nll, nll_weights
+
+        d0c, d1c = d0.float().contiguous(), d1.float().contiguous()
+        out = model.assignment_head(layer, d0c, d1c, token_logits=tokens)
+        la = out[0]
+        t0, t1 = (out[2], out[3]) if tokens else (la.new_zeros(0), la.new_zeros(0))
+        terms = _nll(la, data, 1, float(balancing))  # [5, B]: nll, nll_pos, nll_neg, num_pos, num_neg
+        w = nll_weights(la, data)
+        ctx.model, ctx.layer, ctx.tokens, ctx.bal = model, layer, tokens, float(balancing)
+        ctx.save_for_backward(d0c, d1c, w, terms[3].clone(), terms[4].clone(), *params)
+        ctx.mark_non_differentiable(la)
+        nll, pos, neg, npos, nneg = (terms[i].clone() for i in range(5))
+        ctx.mark_non_differentiable(npos, nneg)
+        return nll, pos, neg, npos, nneg, la, t0, t1
+
+    @staticmethod
+    def backward(ctx, g_nll, g_pos, g_neg, _g_npos, _g_nneg, _g_la, g_t0, g_t1):
+        d0, d1, w, npos, nneg, *params = ctx.saved_tensors
+        b = d0.shape[0]
+        z = torch.zeros(b, device=d0.device)
+        g_nll = z if g_nll is None else g_nll
+        gp = ctx.bal * g_nll + (z if g_pos is None else g_pos)
+        gn = (1.0 - ctx.bal) * g_nll + (z if g_neg is None else g_neg)
+        # nll_pos = -sum(w la)_inner / num_pos, nll_neg = -sum(w la)_dustbins / (num_neg0 + num_neg1)
+        s_in = -gp / npos
+        s_dust = -gn / (2.0 * nneg)
+        if not ctx.tokens:
+            g_t0 = g_t1 = None
+        needs = list(ctx.needs_input_grad[7:]) + [ctx.needs_input_grad[5], ctx.needs_input_grad[6]]
+        gd0, gd1, grads = _head_backward(ctx.model, ctx.layer, d0, d1, params, needs, w, s_in, s_dust, None, g_t0, g_t1)
+        return (None, None, None, None, None, gd0, gd1, *grads)
 
 
 class LightGlue(nn.Module):
@@ -352,17 +508,76 @@ class LightGlue(nn.Module):
             sc0, o0 = per_point(data["scales0"]), per_point(data["oris0"])
             sc1, o1 = per_point(data["scales1"]), per_point(data["oris1"])
 
-        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                "lightglue_amd: the HIP forward has no autograd; training is out of scope (SURVEY.md §2). "
-                "Use torch.no_grad() or .eval()"
-            )
+        if self.training and torch.is_grad_enabled() and (
+                d0.requires_grad or d1.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return self._forward_train((k0, k1, s0, s1, sc0, o0, sc1, o1), d0, d1)
         inputs = (k0, k1, d0, d1, s0, s1, sc0, o0, sc1, o1)
         pruning = (c.width_confidence > 0 or c.depth_confidence > 0) and not self.training
         if self._graphs is not None and not pruning and not self.training:
             key = (str(device),) + tuple(None if t is None else tuple(t.shape) for t in inputs)
             return self._graph_forward(inputs, key)
         return self._forward_native(*inputs)
+
+    # ------------------------------------------------------------ training forward (autograd)
+    def _schema_names(self):
+        """State-dict names in the library's schema order (lg_weight_name)."""
+        if getattr(self, "_schema_for", None) is not self._handle:
+            lib = _lib.load()
+            n = lib.lg_weight_count(self._handle)
+            self._schema_list = [lib.lg_weight_name(self._handle, i).decode() for i in range(n)]
+            self._schema_for = self._handle
+        return self._schema_list
+
+    def _schema_params(self, device):
+        self._ensure_handle(device)
+        named = dict(self.named_parameters())
+        params = []
+        for nm in self._schema_names():
+            p = named[nm]
+            if p.device != device or p.dtype != torch.float32 or not p.is_contiguous():
+                raise RuntimeError(f"lightglue_amd: parameter {nm} must be a contiguous fp32 tensor on {device}")
+            params.append(p)
+        return params
+
+    @staticmethod
+    def _param_array(tensors):
+        arr = (ctypes.c_void_p * len(tensors))(*[None if t is None else t.data_ptr() for t in tensors])
+        return ctypes.cast(arr, ctypes.c_void_p)
+
+    def _lg_inputs(self, inputs, d0, d1):
+        k0, k1, s0, s1, sc0, o0, sc1, o1 = inputs
+        return _lib.LGInputs(d0.shape[0], d0.shape[1], d1.shape[1],
+                             *[_ptr(t) for t in (k0, k1, d0, d1, s0, s1, sc0, o0, sc1, o1)], _lib.LG_FWD_TRAINING_GATE)
+
+    def _forward_train(self, inputs, d0, d1):
+        """Training-mode forward with autograd (lightglue.py:444-579 with :502-503 gating): the HIP
+        training forward keeps its activations for the HIP backward; the final head is a
+        differentiable MatchAssignment; matches come from the detached log assignment."""
+        from .assignment import filter_matches
+
+        c = self.conf
+        device = d0.device
+        b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
+        if m == 0 or n == 0:
+            raise IndexError("max(): Expected reduction dim to have non-zero size (empty keypoint set)")
+        L = int(c.n_layers)
+        params = self._schema_params(device)
+        rd0, rd1 = _TrainTrunk.apply(self, inputs, d0, d1, *params)
+        la, _, _, _ = _Head.apply(self, -1, False, rd0[:, -1], rd1[:, -1], *params)
+        m0, m1, ms0, ms1 = filter_matches(la.detach(), float(c.filter_threshold))
+        self.last_precision_used = "fp32"
+        return {
+            "matches0": m0,
+            "matches1": m1,
+            "matching_scores0": ms0,
+            "matching_scores1": ms1,
+            "ref_descriptors0": rd0,
+            "ref_descriptors1": rd1,
+            "log_assignment": la,
+            "prune0": torch.full((b, m), float(L), device=device),
+            "prune1": torch.full((b, n), float(L), device=device),
+            "stop_layer": torch.full((b,), L - 1, dtype=torch.int64),
+        }
 
     def _forward_native(self, k0, k1, d0, d1, s0, s1, sc0, o0, sc1, o1):
         """One lg_forward call on prepared (fp32, contiguous, on-device) inputs."""
@@ -496,42 +711,44 @@ class LightGlue(nn.Module):
         return (la, sim, t0, t1) if token_logits else (la, sim)
 
     def loss(self, pred, data):
-        """LightGlue.loss (lightglue.py:614-663), forward values (no backward): the NLL of every
-        layer's assignment head on that layer's descriptors (``pred["ref_descriptors*"]`` is
-        [B, L, M, 256] in training mode, [B, 1, M, 256] in eval mode, so eval evaluates the last
-        head only), weighted by ``gamma ** (L - i - 1)``; the token-confidence BCE of layers
+        """LightGlue.loss (lightglue.py:614-663): the NLL of every layer's assignment head on that
+        layer's descriptors (``pred["ref_descriptors*"]`` is [B, L, M, 256] in training mode,
+        [B, 1, M, 256] in eval mode, so eval evaluates the last head only), weighted by
+        ``gamma ** (L - i - 1)`` (or ``i + 1`` when gamma <= 0); the token-confidence BCE of layers
         0..L-2 (:108-122; added to ``total`` in training mode); ``row_norm``; and, in eval mode,
-        ``matcher_metrics`` (models/utils/metrics.py).  The heads and the NLL sums run in the HIP
-        library (``lg_assignment_head``, ``sg_nll_loss``); what stays in torch is the reference's
-        per-point glue (argmax agreement, BCE on [B, M] logits, metric ratios)."""
-        from .superglue import NLLLoss
-
+        ``matcher_metrics`` (models/utils/metrics.py).  Differentiable: each head + NLL term is one
+        autograd Function (:class:`_HeadNLL`) whose backward runs in the HIP library; what stays in
+        torch is the reference's per-point glue (argmax agreement, BCE on [B, M] logits, the
+        gamma-weighted sum, metric ratios)."""
         lconf = self.conf.loss
         if lconf.get("fn", "nll") != "nll":
             raise NotImplementedError(f"loss fn {lconf.fn!r} (the reference defines only 'nll')")
-        loss_fn = NLLLoss({"nll_balancing": lconf.nll_balancing})
+        bal = float(lconf.nll_balancing)
         rd0, rd1 = pred["ref_descriptors0"], pred["ref_descriptors1"]
         N = rd0.shape[1]
-        la_last, _ = self.assignment_head(-1, rd0[:, -1], rd1[:, -1])
-        nll, gt_weights, loss_metrics = loss_fn({"log_assignment": la_last}, data)
+        params = self._schema_params(rd0.device)
+
+        def head(i, tokens):
+            return _HeadNLL.apply(self, i, data, bal, tokens, rd0[:, i], rd1[:, i], *params)
+
+        nll, nll_pos, nll_neg, num_pos, num_neg, _, _, _ = head(-1, False)
+        losses = {"total": nll, "last": nll.clone().detach(), "assignment_nll": nll, "nll_pos": nll_pos,
+                  "nll_neg": nll_neg, "num_matchable": num_pos, "num_unmatchable": num_neg}
         sum_weights = 1.0
-        losses = {"total": nll, "last": nll.clone().detach(), **loss_metrics}
         if self.training:
             losses["confidence"] = 0.0
-        losses["row_norm"] = pred["log_assignment"].exp()[:, :-1].sum(2).mean(1)
-        la_final = pred["log_assignment"]
+        la_final = pred["log_assignment"].detach()
+        losses["row_norm"] = la_final.exp()[:, :-1].sum(2).mean(1)
+        bce = torch.nn.functional.binary_cross_entropy_with_logits
         for i in range(N - 1):
-            la_i, _, lg0, lg1 = self.assignment_head(i, rd0[:, i], rd1[:, i], token_logits=True)
-            nll_i, _, _ = loss_fn({"log_assignment": la_i}, data, weights=gt_weights)
+            nll_i, _, _, _, _, la_i, lg0, lg1 = head(i, True)
             weight = lconf.gamma ** (N - i - 1) if lconf.gamma > 0.0 else i + 1
             sum_weights += weight
             losses["total"] = losses["total"] + nll_i * weight
             # TokenConfidence.loss (:108-122): does layer i already pick the final argmax?
-            correct0 = la_final[:, :-1, :].max(-1).indices == la_i[:, :-1, :].max(-1).indices
-            correct1 = la_final[:, :, :-1].max(-2).indices == la_i[:, :, :-1].max(-2).indices
-            bce = torch.nn.functional.binary_cross_entropy_with_logits
-            tok = (bce(lg0, correct0.float(), reduction="none").mean(-1)
-                   + bce(lg1, correct1.float(), reduction="none").mean(-1)) / 2.0
+            hit0 = (la_final[:, :-1, :].max(-1).indices == la_i[:, :-1, :].max(-1).indices).float()
+            hit1 = (la_final[:, :, :-1].max(-2).indices == la_i[:, :, :-1].max(-2).indices).float()
+            tok = (bce(lg0, hit0, reduction="none").mean(-1) + bce(lg1, hit1, reduction="none").mean(-1)) / 2.0
             losses["confidence"] = losses.get("confidence", 0.0) + tok / (N - 1)
         losses["total"] = losses["total"] / sum_weights
         if self.training:
@@ -542,41 +759,32 @@ class LightGlue(nn.Module):
 
 @torch.no_grad()
 def matcher_metrics(pred, data, prefix="", prefix_gt=None):
-    """gluefactory/models/utils/metrics.py: match recall / precision / accuracy and the ranking AP
-    of ``matches0`` against ``gt_matches0`` (per-pair ratios over [B, M] index tensors)."""
+    """models/utils/metrics.py:4-50 (match recall / precision / accuracy / ranking AP of
+    ``matches0`` against ``gt_matches0``), restated as ratios of per-pair counts over [B, M].
+    The reference's ranking AP sums the consecutive steps of the score-sorted recall curve times the
+    curve's LAST precision point (``p_pts[:, None, -1]``): the sum telescopes to
+    precision * (recall - recall point of the best-scoring keypoint), computed here without the
+    sort (ties for the best score resolve to the first index)."""
+    pg = prefix if prefix_gt is None else prefix_gt
+    m = pred[f"{prefix}matches0"]
+    gt = data[f"gt_{pg}matches0"].to(m.device)
+    hit = (m == gt).float()
+    labelled = (gt >= -1).float()
+    matchable = (gt > -1).float()
+    claimed = ((m > -1) & (gt >= -1)).float()
+    eps = 1e-8
 
-    def recall(m, gt_m):
-        mask = (gt_m > -1).float()
-        return ((m == gt_m) * mask).sum(1) / (1e-8 + mask.sum(1))
+    def rate(mask):
+        return (hit * mask).sum(1) / (eps + mask.sum(1))
 
-    def accuracy(m, gt_m):
-        mask = (gt_m >= -1).float()
-        return ((m == gt_m) * mask).sum(1) / (1e-8 + mask.sum(1))
-
-    def precision(m, gt_m):
-        mask = ((m > -1) & (gt_m >= -1)).float()
-        return ((m == gt_m) * mask).sum(1) / (1e-8 + mask.sum(1))
-
-    def ranking_ap(m, gt_m, scores):
-        p_mask = ((m > -1) & (gt_m >= -1)).float()
-        r_mask = (gt_m > -1).float()
-        order = torch.argsort(-scores)
-        sp = torch.gather(p_mask, -1, order)
-        sr = torch.gather(r_mask, -1, order)
-        tp = torch.gather(m == gt_m, -1, order)
-        p_pts = torch.cumsum(tp * sp, -1) / (1e-8 + torch.cumsum(sp, -1))
-        r_pts = torch.cumsum(tp * sr, -1) / (1e-8 + sr.sum(-1)[:, None])
-        return torch.sum((r_pts[..., 1:] - r_pts[..., :-1]) * p_pts[:, None, -1], dim=-1)
-
-    if prefix_gt is None:
-        prefix_gt = prefix
-    m0 = pred[f"{prefix}matches0"]
-    gt0 = data[f"gt_{prefix_gt}matches0"].to(m0.device)
+    recall, precision = rate(matchable), rate(claimed)
+    best = pred[f"{prefix}matching_scores0"].argmax(1, keepdim=True)
+    first = (hit * matchable).gather(1, best).squeeze(1) / (eps + matchable.sum(1))
     return {
-        f"{prefix}match_recall": recall(m0, gt0),
-        f"{prefix}match_precision": precision(m0, gt0),
-        f"{prefix}accuracy": accuracy(m0, gt0),
-        f"{prefix}average_precision": ranking_ap(m0, gt0, pred[f"{prefix}matching_scores0"]),
+        f"{prefix}match_recall": recall,
+        f"{prefix}match_precision": precision,
+        f"{prefix}accuracy": rate(labelled),
+        f"{prefix}average_precision": precision * (recall - first),
     }
 
 

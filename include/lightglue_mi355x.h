@@ -8,6 +8,11 @@
  *     filter_matches(scores,th) :321-337  -> lg_filter_matches
  *   gluefactory_nonfree/superglue.py:181-201 log_optimal_transport(scores, alpha, iters)
  *                                         -> lg_log_optimal_transport
+ *   training (gluefactory/train.py:450 `loss.backward()` through torch autograd):
+ *     LightGlue.forward in training mode  -> lg_train_forward (activation-saving forward)
+ *     its backward                         -> lg_train_backward
+ *     MatchAssignment + log double softmax
+ *       (+ losses.NLLLoss) backward        -> lg_head_backward
  * The binding a maintainer adds on the reference side is in INTEGRATION.md (ctypes).
  *
  * Conventions
@@ -33,7 +38,7 @@
 extern "C" {
 #endif
 
-#define LG_ABI_VERSION 5
+#define LG_ABI_VERSION 6
 
 enum {
   LG_OK = 0,
@@ -200,6 +205,73 @@ int lg_attention_workspace_bytes(int32_t B, int32_t H, int32_t Nq, int32_t Nk, s
 int lg_attention(const float* q, const float* k, const float* v, int32_t B, int32_t H, int32_t Nq,
                  int32_t Nk, float scale, int32_t precision, float* ctx, void* workspace,
                  size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Training: the backward pass of LightGlue (the reference differentiates its forward with torch
+ * autograd: gluefactory/train.py:436-450 over lightglue.py:444-579 and :614-663).  No reference
+ * counterpart as an interface; these entry points are what a torch.autograd.Function binds.
+ *
+ * Parameters are passed as raw fp32 device pointers in the state-dict schema order
+ * (lg_weight_name(h, i), i < lg_weight_count(h)) in the reference's own layouts (Wqkv
+ * [768,256] with rows h*192 + d*3 + t, lightglue.py:185, ...), and gradients come back in the same
+ * order and layouts: `grads[i]` (device, numel lg_weight_numel(h, i)) is overwritten when non-null;
+ * entries a call does not own are left untouched.  All arithmetic is fp32 (f32-input matrix cores).
+ *
+ * lg_train_forward: the training-mode forward (no pruning / early stop, :502-503) that keeps every
+ * activation its backward needs in `saved` (lg_train_saved_bytes; caller-owned, pass the same
+ * buffer to lg_train_backward) and writes every layer's descriptors to
+ * layer_descriptors0/1 [B,L,M,256] / [B,L,N,256] (the training-mode ref_descriptors, :521-524,572).
+ * lg_train_backward: given d(loss)/d(layer_descriptors0/1) (nullable: zero), writes the gradients of
+ * input_proj.*, posenc.*, transformers.* (grads) and of the input descriptors grad_desc0/1
+ * [B,M,input_dim] / [B,N,input_dim] (nullable).  Scratch: lg_train_scratch_bytes.  Both are
+ * stream-ordered and asynchronous; the dQ sums of the attention backward use float atomics, so
+ * repeated calls may differ in the last bits.
+ */
+int lg_train_saved_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+int lg_train_scratch_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+int lg_train_forward(lg_handle_t* h, const float* const* params, const lg_inputs_t* in, float* layer_descriptors0,
+                     float* layer_descriptors1, void* saved, size_t saved_bytes, void* stream);
+int lg_train_backward(lg_handle_t* h, const float* const* params, const lg_inputs_t* in, const void* saved,
+                      size_t saved_bytes, const float* grad_layer_descriptors0, const float* grad_layer_descriptors1,
+                      float* const* grads, float* grad_desc0, float* grad_desc1, void* scratch, size_t scratch_bytes,
+                      void* stream);
+
+/* Backward of MatchAssignment `layer` (python-style index) on desc0 [B,M,256] / desc1 [B,N,256]
+ * (lightglue.py:306-315 and sigmoid_log_double_softmax :284-296), recomputing what it needs.
+ * The gradient of the log assignment is `la_grad` [B,M+1,N+1] scaled per pair: s_in[b] on the
+ * inner block, s_dust[b] on the dustbin row / column (s_in / s_dust nullable = 1; the corner is
+ * ignored).  Plain autograd passes d(loss)/d(log_assignment) with both null; the fused NLL backward
+ * (losses.py:6-58: nll = bal * nll_pos + (1 - bal) * nll_neg, linear in la) passes the NLLLoss
+ * weights [B,M+1,N+1] with s_in = -g bal / num_pos, s_dust = -g (1 - bal) / (num_neg0 + num_neg1),
+ * so no dense gradient tensor is formed.  grad_similarity [B,M,N] (nullable) adds
+ * d(loss)/d(similarity) for callers that use MatchAssignment's second output.  grad_token0/1
+ * [B,M] / [B,N] (nullable; layers 0..L-2): d(loss)/d(token_confidence logits); TokenConfidence.loss
+ * detaches its inputs (:109-110), so they reach only token_confidence.<layer>.token.0.*.
+ * Writes the grads of log_assignment.<layer>.* (and token_confidence.<layer>.* when grad_token* is
+ * given) and grad_desc0/1 (nullable).  Scratch: lg_head_scratch_bytes.  Asynchronous. */
+int lg_head_scratch_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, const float* desc0, const float* desc1,
+                     int32_t B, int32_t M, int32_t N, const float* la_grad, const float* s_in, const float* s_dust,
+                     const float* grad_similarity, const float* grad_token0, const float* grad_token1,
+                     float* const* grads, float* grad_desc0, float* grad_desc1, void* scratch, size_t scratch_bytes,
+                     void* stream);
+
+/* Kernel-level entries of the training kernels (tests; no reference counterpart).
+ * lg_train_gemm: C[b] = alpha (op(A[b]) op(B[b]) + bias) + beta C[b] on the f32 matrix cores,
+ *   op(A)(m,k) = ta ? A[k*lda+m] : A[m*lda+k], op(B)(k,n) = tb ? B[n*ldb+k] : B[k*ldb+n];
+ *   workspace: lg_train_gemm_workspace_bytes (split-k partials; 0 is allowed, then no split).
+ * lg_train_attention / _backward: the fp32 training attention on fp32 head-major-in-columns
+ *   tensors [B*Nq or B*Nk, 256] (head h at columns 64h..): O, lse [B*H*Nq] (log2 units); the
+ *   backward writes dQ (zeroed first), dK, dV; delta_ws [B*H*Nq] floats.  Synchronise. */
+int lg_train_gemm_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t batch, size_t* bytes);
+int lg_train_gemm(const float* A, const float* Bm, float* C, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA,
+                  int64_t sB, int64_t sC, int32_t M, int32_t N, int32_t K, int32_t batch, float alpha, float beta,
+                  const float* bias, int32_t ta, int32_t tb, void* workspace, size_t workspace_bytes, void* stream);
+int lg_train_attention(const float* q, const float* k, const float* v, int32_t B, int32_t H, int32_t Nq, int32_t Nk,
+                       float scale, float* o, float* lse, void* stream);
+int lg_train_attention_backward(const float* q, const float* k, const float* v, const float* o, const float* lse,
+                                const float* grad_o, int32_t B, int32_t H, int32_t Nq, int32_t Nk, float scale,
+                                float* grad_q, float* grad_k, float* grad_v, float* delta_ws, void* stream);
 
 #ifdef __cplusplus
 }

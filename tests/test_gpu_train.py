@@ -1,0 +1,217 @@
+"""LightGlue backward pass on the HIP library (training path, include/lightglue_mi355x.h
+"Training") -- needs an MI355X.
+
+Gradients are checked two ways:
+* against the reference's own autograd gradients (tests/golden/grad_*.npz, make_grad_golden.py:
+  float64 values at seeded sample positions), and
+* against the float64 autograd gradients of the oracle restatement (oracle/lightglue_train_ref.py,
+  itself pinned to those goldens by tests/test_oracle_grad.py) on EVERY entry of every tensor.
+Bar per tensor: max |g_gpu - g64| <= 8 * spread32 + 1e-6 * max|g64| + 1e-12, where spread32 is
+how far the reference's own float32 autograd gradient lies from float64 (stored in the golden).
+The HIP path is fp32 arithmetic like the reference's float32 run, with different summation orders
+(and float-atomic dQ sums), so a few spreads of headroom are the right scale.
+Kernel-level checks: the f32 matrix-core GEMM in every transpose form (split-k included) and the
+training attention forward / backward against float64 torch.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import lgamd  # noqa: F401
+from grad_golden_util import golden_entries, grad_case, grad_names, load_grad, oracle_grads
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _p(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _lib():
+    from lightglue_amd import _lib
+
+    return _lib, _lib.load()
+
+
+# ------------------------------------------------------------------ kernel level
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K,batch", [(200, 136, 72, 1), (37, 300, 129, 3), (256, 512, 5000, 1), (33, 17, 4100, 2)])
+def test_train_gemm_matches_fp64(ta, tb, M, N, K, batch):
+    L, lib = _lib()
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn((batch, K, M) if ta else (batch, M, K), generator=g)
+    Bm = torch.randn((batch, N, K) if tb else (batch, K, N), generator=g)
+    C0 = torch.randn((batch, M, N), generator=g)
+    bias = torch.randn(N, generator=g)
+    alpha, beta = 0.75, 1.0
+    ref = alpha * ((A.transpose(1, 2) if ta else A).double() @ (Bm.transpose(1, 2) if tb else Bm).double()
+                   + bias.double()) + beta * C0.double()
+    Ad, Bd, Cd, bd = A.to(DEV), Bm.to(DEV), C0.to(DEV), bias.to(DEV)
+    nb = ctypes.c_size_t()
+    L.check(lib.lg_train_gemm_workspace_bytes(M, N, K, batch, ctypes.byref(nb)), "ws")
+    ws = torch.empty(max(nb.value, 4), dtype=torch.uint8, device=DEV)
+    lda = A.shape[2]
+    ldb = Bm.shape[2]
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L.check(lib.lg_train_gemm(_p(Ad), _p(Bd), _p(Cd), lda, ldb, N, A[0].numel(), Bm[0].numel(), M * N, M, N, K, batch,
+                              alpha, beta, _p(bd), ta, tb, _p(ws), nb.value, st), "lg_train_gemm")
+    err = (Cd.cpu().double() - ref).abs().max().item()
+    # fp32 accumulation over K terms of |a b| ~ 1: a few ulps of sqrt(K)-scale sums
+    assert err <= 2e-6 * max(K, 64) ** 0.5 * 8, err
+
+
+def _attn_ref(q, k, v, scale):
+    s = torch.einsum("bhid,bhjd->bhij", q, k) * scale
+    return torch.softmax(s, -1) @ v
+
+
+@pytest.mark.parametrize("B,Nq,Nk", [(2, 96, 96), (1, 200, 77), (3, 33, 300), (1, 1, 5)])
+def test_train_attention_forward_backward_fp64(B, Nq, Nk):
+    L, lib = _lib()
+    H, scale = 4, 0.125
+    g = torch.Generator().manual_seed(B * 1000 + Nq + Nk)
+    q = torch.randn(B, Nq, 256, generator=g) * 2
+    k = torch.randn(B, Nk, 256, generator=g) * 2
+    v = torch.randn(B, Nk, 256, generator=g)
+    go = torch.randn(B, Nq, 256, generator=g)
+
+    def heads(t):
+        return t.double().unflatten(-1, (H, 64)).transpose(1, 2)
+
+    qd, kd, vd = (heads(t).requires_grad_() for t in (q, k, v))
+    o = _attn_ref(qd, kd, vd, scale)
+    o.backward(heads(go))
+    o_ref = o.detach().transpose(1, 2).flatten(-2)
+    dq_ref, dk_ref, dv_ref = (t.grad.transpose(1, 2).flatten(-2) for t in (qd, kd, vd))
+
+    qg, kg, vg, gog = (t.to(DEV).contiguous() for t in (q, k, v, go))
+    og = torch.empty(B, Nq, 256, device=DEV)
+    lse = torch.empty(B * H * Nq, device=DEV)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L.check(lib.lg_train_attention(_p(qg), _p(kg), _p(vg), B, H, Nq, Nk, scale, _p(og), _p(lse), st), "fwd")
+    np.testing.assert_allclose(og.cpu().double().numpy(), o_ref.numpy(), atol=2e-5, rtol=1e-5)
+    s = torch.einsum("bhid,bhjd->bhij", heads(q), heads(k)) * scale
+    lse_ref = torch.logsumexp(s, -1).flatten() / np.log(2.0)
+    np.testing.assert_allclose(lse.cpu().double().numpy(), lse_ref.numpy(), atol=2e-5, rtol=1e-6)
+    dq, dk, dv = (torch.empty_like(t) for t in (qg, kg, vg))
+    delta = torch.empty(B * H * Nq, device=DEV)
+    L.check(lib.lg_train_attention_backward(_p(qg), _p(kg), _p(vg), _p(og), _p(lse), _p(gog), B, H, Nq, Nk, scale,
+                                            _p(dq), _p(dk), _p(dv), _p(delta), st), "bwd")
+    for got, ref in ((dq, dq_ref), (dk, dk_ref), (dv, dv_ref)):
+        r = ref.numpy()
+        np.testing.assert_allclose(got.cpu().double().numpy(), r, atol=2e-5 * max(1.0, np.abs(r).max()), rtol=1e-5)
+
+
+# ------------------------------------------------------------------ full backward
+def _gpu_grads(conf, sd, pair, gt):
+    from lightglue_amd import LightGlue
+
+    model = LightGlue(conf).to(DEV)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model.train()
+    data = {k: torch.from_numpy(v).to(DEV) for k, v in pair.items()
+            if not k.startswith(("image_size", "descriptors"))}
+    d0 = torch.from_numpy(pair["descriptors0"]).to(DEV).requires_grad_()
+    d1 = torch.from_numpy(pair["descriptors1"]).to(DEV).requires_grad_()
+    data["descriptors0"], data["descriptors1"] = d0, d1
+    data["view0"] = {"image_size": torch.from_numpy(pair["image_size0"]).to(DEV)}
+    data["view1"] = {"image_size": torch.from_numpy(pair["image_size1"]).to(DEV)}
+    data.update({k: torch.from_numpy(v).to(DEV) for k, v in gt.items()})
+    pred = model(data)
+    losses, _ = model.loss(pred, data)
+    loss = torch.mean(losses["total"])  # train.py:436
+    loss.backward()  # train.py:450
+    grads = {n: (p.grad.detach().double().cpu().numpy() if p.grad is not None else None)
+             for n, p in model.named_parameters()}
+    return float(loss.detach()), grads, d0.grad.double().cpu().numpy(), d1.grad.double().cpu().numpy(), pred
+
+
+@pytest.mark.parametrize("name", grad_names())
+def test_backward_matches_reference_and_oracle(name):
+    g, meta = load_grad(name)
+    conf, sd, pair, gt = grad_case(meta)
+    loss, grads, gd0, gd1, pred = _gpu_grads(conf, sd, pair, gt)
+    assert abs(loss - float(g["loss64"])) <= 1e-4 * abs(float(g["loss64"]))
+    _, og, ogd0, ogd1 = oracle_grads(conf, sd, pair, gt)
+    worst, bad = [], []
+    for n in meta["names"]:
+        assert grads[n] is not None, f"no gradient for {n}"
+        tol = 8 * float(g[f"spread32:{n}"]) + 1e-6 * float(g[f"max64:{n}"]) + 1e-12
+        idx, ref = golden_entries(g, n)
+        got = grads[n].reshape(-1)
+        e_gold = np.abs((got if idx is None else got[idx]) - ref).max()
+        e_full = np.abs(got - og[n].reshape(-1)).max()
+        worst.append((max(e_gold, e_full) / tol, n))
+        if e_gold > tol or e_full > tol:
+            bad.append((n, float(e_gold), float(e_full), tol, float(g[f"max64:{n}"])))
+    for got, ref, key in ((gd0, ogd0, "gdesc0"), (gd1, ogd1, "gdesc1")):
+        tol = 8 * float(g[f"spread_{key}"]) + 1e-6 * np.abs(g[key]).max() + 1e-12
+        e_gold, e_full = np.abs(got - g[key]).max(), np.abs(got - ref).max()
+        worst.append((max(e_gold, e_full) / tol, key))
+        if e_gold > tol or e_full > tol:
+            bad.append((key, float(e_gold), float(e_full), tol, float(np.abs(g[key]).max())))
+    worst.sort(reverse=True)
+    print(name, "loss", loss, "worst err/tol:", [(n, round(r, 3)) for r, n in worst[:6]])
+    assert not bad, bad[:12]
+
+
+def test_training_forward_matches_eval_forward_descriptors():
+    """The autograd training forward (fp32 f32-MFMA kernels) and the no-grad training-mode forward
+    (the fp16x3 eval kernels with the training gate) produce the same per-layer descriptors."""
+    from lightglue_amd import LightGlue
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1, "n_layers": 3}
+    sd = synthetic_state_dict(conf, seed=2)
+    pair = synthetic_pair(B=2, M=100, N=90, seed=5)
+    model = LightGlue(conf).to(DEV)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model.train()
+    data = {k: torch.from_numpy(v).to(DEV) for k, v in pair.items() if not k.startswith("image_size")}
+    data["view0"] = {"image_size": torch.from_numpy(pair["image_size0"]).to(DEV)}
+    data["view1"] = {"image_size": torch.from_numpy(pair["image_size1"]).to(DEV)}
+    with torch.no_grad():
+        ref = model(data)
+    pred = model(data)
+    assert pred["ref_descriptors0"].requires_grad
+    for k in ("ref_descriptors0", "ref_descriptors1", "log_assignment"):
+        np.testing.assert_allclose(pred[k].detach().cpu().numpy(), ref[k].cpu().numpy(), atol=1e-4, rtol=1e-4)
+    assert torch.equal(pred["matches0"], ref["matches0"])
+
+
+def test_head_backward_dense_and_similarity_gradients():
+    """_Head (plain autograd through log_assignment and similarity) against float64 torch."""
+    from lightglue_amd import LightGlue
+    from lightglue_amd.lightglue import _Head
+    from lightglue_amd.weights import synthetic_state_dict
+    from oracle.lightglue_ref import match_assignment
+
+    conf = {"n_layers": 2}
+    sd = synthetic_state_dict(conf, seed=4)
+    model = LightGlue(conf).to(DEV)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    gen = torch.Generator().manual_seed(3)
+    B, M, N = 2, 70, 45
+    d0 = torch.randn(B, M, 256, generator=gen)
+    d1 = torch.randn(B, N, 256, generator=gen)
+    gla = torch.randn(B, M + 1, N + 1, generator=gen)
+    gsim = torch.randn(B, M, N, generator=gen) * 0.1
+    W = {k: torch.from_numpy(v).double().requires_grad_() for k, v in sd.items()}
+    x0, x1 = d0.double().requires_grad_(), d1.double().requires_grad_()
+    la, sim = match_assignment(x0, x1, W, "log_assignment.0")
+    ((la * gla.double()).sum() + (sim * gsim.double()).sum()).backward()
+    params = model._schema_params(DEV)
+    g0, g1 = d0.to(DEV).requires_grad_(), d1.to(DEV).requires_grad_()
+    la_g, sim_g, _, _ = _Head.apply(model, 0, False, g0, g1, *params)
+    ((la_g * gla.to(DEV)).sum() + (sim_g * gsim.to(DEV)).sum()).backward()
+    for got, ref in ((g0.grad, x0.grad), (g1.grad, x1.grad)):
+        r = ref.numpy()
+        np.testing.assert_allclose(got.cpu().double().numpy(), r, atol=1e-5 * np.abs(r).max(), rtol=0)
+    named = dict(model.named_parameters())
+    for n in ("log_assignment.0.final_proj.weight", "log_assignment.0.final_proj.bias",
+              "log_assignment.0.matchability.weight", "log_assignment.0.matchability.bias"):
+        r = W[n].grad.numpy()
+        np.testing.assert_allclose(named[n].grad.cpu().double().numpy(), r, atol=1e-5 * np.abs(r).max(), rtol=0)

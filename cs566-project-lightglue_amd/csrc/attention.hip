@@ -58,6 +58,8 @@ __device__ __forceinline__ int xcd_chunk(int id, int n) {
 #ifndef LG_ATTN_REF
 #define LG_ATTN_REF 11
 #endif
+static_assert(LG_ATTN_RAISE <= 15, "e = 2^acc <= 2^LG_ATTN_RAISE must stay a finite fp16 for the P split");
+static_assert(LG_ATTN_REF < LG_ATTN_RAISE, "the re-reference target must lie below the raise threshold");
 #ifndef LG_ATTN_REVERSE
 #define LG_ATTN_REVERSE 1  // configs[2] three same-box pairs: 1326 vs 1321 pairs/s, attention -0.6 %
 #endif

@@ -1249,6 +1249,14 @@ int lg_profile_read(lg_handle_t* h, int kernel, double* total_ms, int64_t* launc
   double ms = 0.0, fl = 0.0, by = 0.0;
   int64_t n = 0;
   std::vector<int> snap;
+  // the snapshot copies (prof_counts) are queued after their record's end event, on whatever
+  // stream the forward ran: wait for the device before reading them (profiling reads only)
+  for (auto& r : h->recs)
+    if (r.snap >= 0) {
+      LG_HIP(hipSetDevice(h->device));
+      LG_HIP(hipDeviceSynchronize());
+      break;
+    }
   for (auto& r : h->recs) {
     if (r.kind != kernel) continue;
     LG_HIP(hipEventSynchronize(r.b));

@@ -586,15 +586,29 @@ static void launch_scaled(const float* scores, const float* v, float* u, float* 
 // row kernel has only ~2 rows per wave, so its fixed costs (v staging, the 8-wave merge tree, the
 // partial write, the merge launch) outweigh the faster Infinity-Cache reads; streaming stays the
 // default.
+// The schedule knobs are read from the environment ONCE per process (the workspace
+// query and the run must agree, whatever the environment does in between).
+struct SkEnv {
+  int group = 0;        // LG_SK_GROUP (pairs; <= 0: unset)
+  double group_mb = 0;  // LG_SK_GROUP_MB (MiB; <= 0: unset)
+  int streams = 2;      // LG_SK_STREAMS
+};
+static const SkEnv& sk_env() {
+  static const SkEnv env = [] {
+    SkEnv x;
+    if (const char* e = getenv("LG_SK_GROUP")) x.group = atoi(e) > 0 ? atoi(e) : -1;  // set, <= 0: every pair
+    if (const char* e = getenv("LG_SK_GROUP_MB")) x.group_mb = atof(e);
+    if (const char* e = getenv("LG_SK_STREAMS")) x.streams = atoi(e);
+    return x;
+  }();
+  return env;
+}
 static int sk_group(int B, int M, int N) {
   const size_t per = (size_t)M * N * 4;
-  if (const char* e = getenv("LG_SK_GROUP")) {
-    const int g = atoi(e);
-    return g <= 0 ? B : std::min(g, B);
-  }
-  const char* e = getenv("LG_SK_GROUP_MB");
-  if (!e) return B;  // streaming schedule
-  const size_t cap = (size_t)atof(e) << 20;
+  const SkEnv& env = sk_env();
+  if (env.group != 0) return env.group < 0 ? B : std::min(env.group, B);
+  if (env.group_mb <= 0) return B;  // streaming schedule
+  const size_t cap = (size_t)env.group_mb << 20;
   if ((size_t)B * per <= cap) return B;
   return (int)std::max<size_t>(1, std::min<size_t>(B, cap / per));
 }
@@ -603,11 +617,9 @@ static int sk_group(int B, int M, int N) {
 // to the caller's stream with events: one group's small merge launch and launch gaps overlap the
 // other group's row kernel, and both groups' scores share the Infinity Cache (2 x 67 MB at N =
 // 4096).  Streams and events are created once per device and reused.
-static int sk_streams_wanted(int groups) {
-  int s = 2;
-  if (const char* e = getenv("LG_SK_STREAMS")) s = atoi(e);
-  return std::max(1, std::min({s, groups, 4}));
-}
+static int sk_streams_wanted(int groups) { return std::max(1, std::min({sk_env().streams, groups, 4})); }
+// one fork..join at a time per process: the library-owned streams and the fork event are shared
+static std::mutex g_sk_enqueue_mu;
 struct SkStreams {
   hipStream_t s[4] = {};
   hipEvent_t fork = nullptr, join[4] = {};
@@ -679,7 +691,9 @@ hipError_t log_optimal_transport(const float* scores, float alpha, int B, int M,
       const bool nt = LG_SK_NT && G == B;
       const int ns = ns0;
       SkStreams* ss = nullptr;
+      std::unique_lock<std::mutex> enqueue_lock(g_sk_enqueue_mu, std::defer_lock);
       if (ns > 1) {
+        enqueue_lock.lock();
         if ((e = sk_streams_for_device(ss)) != hipSuccess) return e;
         if ((e = hipEventRecord(ss->fork, st)) != hipSuccess) return e;
         for (int q = 0; q < ns; ++q)
@@ -708,6 +722,7 @@ hipError_t log_optimal_transport(const float* scores, float alpha, int B, int M,
           if ((e = hipEventRecord(ss->join[q], ss->s[q])) != hipSuccess) return e;
           if ((e = hipStreamWaitEvent(st, ss->join[q], 0)) != hipSuccess) return e;
         }
+        enqueue_lock.unlock();
       }
       if ((e = hipGetLastError()) != hipSuccess) return e;
       // the flag decides whether the exact kernel reruns: one 4-byte read-back

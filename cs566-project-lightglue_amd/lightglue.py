@@ -650,15 +650,21 @@ class LightGlue(nn.Module):
             k0, k1 = out.kept0, out.kept1
             pred["stop_layer"] = stop.to(torch.int64)
             pred["kept0"], pred["kept1"] = kept[0].to(torch.int64), kept[1].to(torch.int64)
+            # the similarity (return_similarity) is the kept block too: rows / columns past the kept
+            # counts are workspace, and its kept rows are in the same compacted order as la
             if b == 1:
                 pred["log_assignment"] = la[:, : k0 + 1, : k1 + 1]
                 pred["ref_descriptors0"] = rd0[:, None, :k0]
                 pred["ref_descriptors1"] = rd1[:, None, :k1]
+                if sim is not None:
+                    pred["similarity"] = sim[:, :k0, :k1]
             else:
                 ks = kept.tolist()
                 pred["log_assignment"] = [la[i, : ks[0][i] + 1, : ks[1][i] + 1] for i in range(b)]
                 pred["ref_descriptors0"] = [rd0[i, None, : ks[0][i]] for i in range(b)]
                 pred["ref_descriptors1"] = [rd1[i, None, : ks[1][i]] for i in range(b)]
+                if sim is not None:
+                    pred["similarity"] = [sim[i, None, : ks[0][i], : ks[1][i]] for i in range(b)]
         return pred
 
     # ------------------------------------------------------------ profiling (bench.py)

@@ -11,8 +11,11 @@ holds the whole batch.
   CHUNKS of pair indices (guided self-scheduling) from an atomic counter in the process group's
   c10d store (``store.add``) and match each chunk in one batched forward -- the reference asserts
   B == 1 when pruning (lightglue.py:528,533); the HIP forward prunes and stops every pair of a batch
-  on its own -- then one ``all_reduce(MAX)`` merges the outputs (each pair is written by exactly one
-  rank; the rest of the buffer holds -2 / -inf).
+  on its own -- then the ranks all-gather only the rows they matched, each tagged with its pair
+  index (a tiny count exchange first, so the gather is fixed-size), and scatter them into place.
+
+Results travel packed: one int32 row per pair, ``[pair | matches0 (M) | matches1 (N) | scores0 (M) |
+scores1 (N)]`` with the fp32 scores bit-cast (8 (M + N) + 4 bytes per pair; matches are < 2^31).
 
 ``matcher`` is any callable with the ``LightGlue.forward`` contract; in production it is
 ``lightglue_amd.LightGlue`` on this rank's GPU (the gather then runs on RCCL).  The CPU tests
@@ -43,22 +46,23 @@ def _slice(data, a, b):
     return out
 
 
-def _pack(pred, M, N, rows, device):
-    """[rows, 2M+2N] float64 rows: matches as exact small integers, scores widened."""
-    buf = torch.empty((rows, 2 * M + 2 * N), dtype=torch.float64, device=device)
-    buf[:, :M] = pred["matches0"].to(torch.float64)
-    buf[:, M : M + N] = pred["matches1"].to(torch.float64)
-    buf[:, M + N : 2 * M + N] = pred["matching_scores0"].to(torch.float64)
-    buf[:, 2 * M + N :] = pred["matching_scores1"].to(torch.float64)
+def _pack(pred, M, N, rows, first, device):
+    """[rows, 1 + 2M + 2N] int32: pair index, matches as int32, fp32 scores bit-cast."""
+    buf = torch.empty((rows, 1 + 2 * M + 2 * N), dtype=torch.int32, device=device)
+    buf[:, 0] = torch.arange(first, first + rows, dtype=torch.int32, device=device)
+    buf[:, 1 : 1 + M] = pred["matches0"].to(torch.int32)
+    buf[:, 1 + M : 1 + M + N] = pred["matches1"].to(torch.int32)
+    buf[:, 1 + M + N : 1 + 2 * M + N] = pred["matching_scores0"].to(torch.float32).contiguous().view(torch.int32)
+    buf[:, 1 + 2 * M + N :] = pred["matching_scores1"].to(torch.float32).contiguous().view(torch.int32)
     return buf
 
 
 def _unpack(buf, M, N):
     return {
-        "matches0": buf[:, :M].to(torch.int64),
-        "matches1": buf[:, M : M + N].to(torch.int64),
-        "matching_scores0": buf[:, M + N : 2 * M + N].to(torch.float32),
-        "matching_scores1": buf[:, 2 * M + N :].to(torch.float32),
+        "matches0": buf[:, 1 : 1 + M].to(torch.int64),
+        "matches1": buf[:, 1 + M : 1 + M + N].to(torch.int64),
+        "matching_scores0": buf[:, 1 + M + N : 1 + 2 * M + N].contiguous().view(torch.float32),
+        "matching_scores1": buf[:, 1 + 2 * M + N :].contiguous().view(torch.float32),
     }
 
 
@@ -71,12 +75,12 @@ def match_static(matcher, data, group=None):
     a, b = shard_range(B, world, rank)
     per = -(-B // world)  # padded rows per rank so the all-gather is fixed-size
     device = data["keypoints0"].device
-    local = torch.full((per, 2 * M + 2 * N), -2.0, dtype=torch.float64, device=device)
+    local = torch.zeros((per, 1 + 2 * M + 2 * N), dtype=torch.int32, device=device)
     if b > a:
         with torch.no_grad():
             pred = matcher(_slice(data, a, b))
-        local[: b - a] = _pack(pred, M, N, b - a, device)
-    out = torch.empty((world * per, 2 * M + 2 * N), dtype=torch.float64, device=device)
+        local[: b - a] = _pack(pred, M, N, b - a, a, device)
+    out = torch.empty((world * per, 1 + 2 * M + 2 * N), dtype=torch.int32, device=device)
     dist.all_gather_into_tensor(out, local, group=group)
     rows = torch.cat([out[r * per : r * per + (shard_range(B, world, r)[1] - shard_range(B, world, r)[0])] for r in range(world)])
     return _unpack(rows, M, N)
@@ -98,9 +102,10 @@ def match_dynamic(matcher, data, group=None, store=None, key="lightglue_amd/next
     """Work-queue sharding in chunks of pairs: each rank pulls a contiguous chunk of pair indices
     from an atomic counter in the process group's c10d store (``store.add``), matches it in ONE
     batched forward (pruning / early stop are per pair inside the batch), and repeats until the
-    batch is exhausted; one ``all_reduce(MAX)`` then merges the outputs (each pair is written by
-    exactly one rank; the rest of the buffer holds -2 / -inf).  Chunk sizes follow
-    :func:`guided_chunk`.  Without an initialised process group the same loop runs on a local
+    batch is exhausted; the ranks then all-gather the rows they matched (tagged with their pair
+    indices, padded to the largest count) and scatter them into place: about the result size
+    through the collective (:func:`exchange_bytes`) instead of a whole-batch reduction.  Chunk sizes
+    follow :func:`guided_chunk`.  Without an initialised process group the same loop runs on a local
     counter (world size 1).  Returns (results, [(start, stop) chunks this rank matched])."""
     global _dynamic_calls
     B, M = data["keypoints0"].shape[:2]
@@ -122,9 +127,8 @@ def match_dynamic(matcher, data, group=None, store=None, key="lightglue_amd/next
             return local[0] - n
         return store.add(ckey, n) - n
 
-    buf = torch.full((B, 2 * M + 2 * N), -2.0, dtype=torch.float64, device=device)
-    buf[:, M + N :] = float("-inf")
-    done = []
+    width = 1 + 2 * M + 2 * N
+    parts, done = [], []
     while True:
         seen = pull(0)
         if seen >= B:
@@ -136,8 +140,33 @@ def match_dynamic(matcher, data, group=None, store=None, key="lightglue_amd/next
         b = min(B, a + c)
         with torch.no_grad():
             pred = matcher(_slice(data, a, b))
-        buf[a:b] = _pack(pred, M, N, b - a, device)
+        parts.append(_pack(pred, M, N, b - a, a, device))
         done.append((a, b))
-    if distributed:
-        dist.all_reduce(buf, op=dist.ReduceOp.MAX, group=group)
-    return _unpack(buf, M, N), done
+    mine = torch.cat(parts) if parts else torch.empty((0, width), dtype=torch.int32, device=device)
+    if not distributed:
+        return _unpack(mine[mine[:, 0].argsort()], M, N), done
+    # fixed-size gather of exactly the rows each rank matched: counts first (one int per rank), then
+    # the tagged rows padded to the largest count; every pair arrives exactly once
+    n = torch.tensor([mine.shape[0]], dtype=torch.int64, device=device)
+    counts = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(counts, n, group=group)
+    cl = counts.tolist()
+    cap = max(cl)
+    padded = torch.zeros((cap, width), dtype=torch.int32, device=device)
+    padded[: mine.shape[0]] = mine
+    every = torch.empty((world * cap, width), dtype=torch.int32, device=device)
+    dist.all_gather_into_tensor(every, padded, group=group)
+    rows = torch.cat([every[r * cap : r * cap + cl[r]] for r in range(world)])
+    out = torch.empty((B, width), dtype=torch.int32, device=device)
+    out[rows[:, 0].long()] = rows
+    return _unpack(out, M, N), done
+
+
+def exchange_bytes(B, M, N, world, counts=None):
+    """Bytes one match_static / match_dynamic call moves through the collective (all ranks'
+    contributions of the final gather; the count exchange of match_dynamic adds 8 per rank).
+    ``counts`` = rows matched per rank (dynamic); None = static shards."""
+    width = 4 * (1 + 2 * M + 2 * N)
+    if counts is None:
+        return world * (-(-B // world)) * width
+    return world * max(counts) * width + 8 * world

@@ -101,3 +101,42 @@ def test_assignment_head_and_similarity_agree_with_forward():
     md0 = (pred["ref_descriptors0"][:, 0].double() @ W.T + bb) / 4.0
     md1 = (pred["ref_descriptors1"][:, 0].double() @ W.T + bb) / 4.0
     torch.testing.assert_close(pred["similarity"].double(), md0 @ md1.transpose(1, 2), atol=2e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_similarity_with_pruning_is_the_kept_block(B):
+    """With width pruning and return_similarity, pred["similarity"] is sliced like log_assignment
+    (b == 1: [1, M', N']; b > 1: per-pair list of [1, M_b, N_b]) and holds md0 md1^T of the kept
+    descriptors (ref_descriptors*, same compacted order) -- ADVICE r3."""
+    from golden_util import PRUNE_BIAS
+    from lightglue_amd import LightGlue
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+
+    conf = {"filter_threshold": 0.1, "width_confidence": 0.95, "return_similarity": True}
+    sd = synthetic_state_dict(conf, seed=6)
+    for i, v in enumerate(PRUNE_BIAS):
+        sd[f"log_assignment.{i}.matchability.bias"][:] = v
+    model = LightGlue(conf).eval().to(DEV)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    p = synthetic_pair(B=B, M=512, N=480, seed=21)
+    data = {k: torch.from_numpy(v).to(DEV) for k, v in p.items() if not k.startswith("image_size")}
+    data["view0"] = {"image_size": torch.from_numpy(p["image_size0"]).to(DEV)}
+    data["view1"] = {"image_size": torch.from_numpy(p["image_size1"]).to(DEV)}
+    with torch.no_grad():
+        pred = model(data)
+    W = model.log_assignment[-1].final_proj.weight.double()
+    bb = model.log_assignment[-1].final_proj.bias.double()
+    sims = pred["similarity"] if B > 1 else [pred["similarity"]]
+    las = pred["log_assignment"] if B > 1 else [pred["log_assignment"]]
+    rd0s = pred["ref_descriptors0"] if B > 1 else [pred["ref_descriptors0"]]
+    rd1s = pred["ref_descriptors1"] if B > 1 else [pred["ref_descriptors1"]]
+    assert len(sims) == B
+    pruned = False
+    for sim, la, r0, r1 in zip(sims, las, rd0s, rd1s):
+        k0, k1 = r0.shape[-2], r1.shape[-2]
+        pruned |= k0 < 512 or k1 < 480
+        assert sim.shape == (1, k0, k1) and la.shape == (1, k0 + 1, k1 + 1)
+        md0 = (r0[:, 0].double() @ W.T + bb) / 4.0
+        md1 = (r1[:, 0].double() @ W.T + bb) / 4.0
+        torch.testing.assert_close(sim.double(), md0 @ md1.transpose(1, 2), atol=2e-5, rtol=1e-5)
+    assert pruned

@@ -473,12 +473,19 @@ def test_training_mode_gates_pruning_and_early_stop():
     assert torch.equal(tr["matches0"], full["matches0"])
 
 
-def test_training_mode_with_autograd_raises():
+def test_training_mode_with_autograd_is_differentiable():
+    """Training mode with gradients enabled runs the autograd training path (tests/test_gpu_train.py
+    pins its gradients): every layer's descriptors and the log assignment carry a graph, and a
+    backward reaches every parameter."""
     from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
 
-    model = _model({}, synthetic_state_dict({}, seed=0)).train()
-    with pytest.raises(NotImplementedError):
-        model(_gpu_data(synthetic_pair(B=1, M=16, seed=3)))
+    model = _model({"n_layers": 2}, synthetic_state_dict({"n_layers": 2}, seed=0)).train()
+    pred = model(_gpu_data(synthetic_pair(B=1, M=16, seed=3)))
+    assert pred["ref_descriptors0"].requires_grad and pred["log_assignment"].requires_grad
+    assert pred["ref_descriptors0"].shape[1] == 2
+    (pred["ref_descriptors0"].sum() + pred["log_assignment"][:, :-1, :-1].sum()).backward()
+    missing = [n for n, p in model.named_parameters() if p.grad is None and not n.startswith(("token_confidence", "log_assignment.0"))]
+    assert not missing, missing
 
 
 @pytest.mark.parametrize("name", ["tiny_ragged_b2", "input_proj_n128"])

@@ -188,3 +188,30 @@ def test_bench_workload_rehearsals(workload, path):
     assert res["n_gpus"] == 2 and res["pairs_timed"] == 2 * 5 * 2
     assert path in res["config"]["parallelism"]
     assert res["config"]["workload"].startswith(workload)
+
+
+def test_exchange_bytes_within_twice_the_result_size():
+    """at configs[3] (64 pairs per GPU x 8 ranks, N = 2048) the bytes one
+    match_dynamic call moves through the collective stay within 2x the packed result size, under
+    guided chunks and even with an unlucky split of the queue (one rank taking an extra chunk)."""
+    import lgamd  # noqa: F401
+    from lightglue_amd.parallel import exchange_bytes, guided_chunk
+
+    B, N, world = 512, 2048, 8
+    result = B * (4 + 8 * (N + N))  # one packed int32 row per pair
+    # simulate the shared queue with the ranks pulling round-robin
+    counts, seen, r = [0] * world, 0, 0
+    while seen < B:
+        c = min(guided_chunk(B - seen, world, 32), B - seen)
+        counts[r % world] += c
+        seen += c
+        r += 1
+    assert sum(counts) == B
+    assert exchange_bytes(B, N, N, world, counts) <= 2 * result
+    skew = list(counts)
+    skew[0] += 32
+    skew[1] -= 32
+    assert exchange_bytes(B, N, N, world, skew) <= 2 * result
+    # the round-3 exchange: an all_reduce of the whole B x (2M + 2N) float64 buffer
+    assert exchange_bytes(B, N, N, world, counts) < B * (4 * N) * 8
+    assert exchange_bytes(B, N, N, world) <= 1.01 * result  # static shards

@@ -273,18 +273,14 @@ def run(args):
     def sinkhorn_matcher(d):
         """configs[4]: the matcher's final similarity through the Sinkhorn head (superglue.py:173-201,
         288-298) instead of the dual softmax."""
-        from lightglue_amd import filter_matches, log_optimal_transport
-
-        pred = model(d)
         if selftest:
-            return pred
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        Z = log_optimal_transport(pred["similarity"], SINKHORN_ALPHA, SINKHORN_ITERS)
-        e1.record()
-        sk_events.append((e0, e1, d["keypoints0"].shape[0]))
-        m0, m1, s0, s1 = filter_matches(Z, SINKHORN_THRESHOLD)
-        return {"matches0": m0, "matches1": m1, "matching_scores0": s0, "matching_scores1": s1}
+            return model(d)
+        from lightglue_amd.assignment import sinkhorn_match
+
+        n = d["keypoints0"].shape[0]
+        out, _ = sinkhorn_match(model, d, SINKHORN_ALPHA, SINKHORN_ITERS, SINKHORN_THRESHOLD,
+                                on_sinkhorn=lambda e0, e1: sk_events.append((e0, e1, n)))
+        return out
 
     matcher = sinkhorn_matcher if wl == "configs4" else model
 

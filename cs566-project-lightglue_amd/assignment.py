@@ -3,6 +3,9 @@
 * :func:`filter_matches`       == ``gluefactory/models/matchers/lightglue.py:321-337``
                                   (identical to ``gluefactory_nonfree/superglue.py:288-298``)
 * :func:`log_optimal_transport` == ``gluefactory_nonfree/superglue.py:181-201``
+* :func:`sinkhorn_match`        == configs[4]'s composition: a LightGlue forward's final similarity
+                                  (``lightglue.py:306-315``) through the SuperGlue Sinkhorn head
+                                  (``superglue.py:181-201,214``) and its mutual filter (``:288-298``)
 
 Inputs must be fp32 CUDA (HIP) tensors; there is no CPU path.
 """
@@ -69,3 +72,29 @@ def log_optimal_transport(scores: torch.Tensor, alpha, iters: int) -> torch.Tens
         "lg_log_optimal_transport",
     )
     return Z
+
+
+# SuperGlue's head (superglue.py:214-215; bin_score initialised to 1.0): 50 iterations, threshold 0.2
+SINKHORN_ALPHA, SINKHORN_ITERS, SINKHORN_THRESHOLD = 1.0, 50, 0.2
+
+
+def sinkhorn_match(model, data, alpha=SINKHORN_ALPHA, iters=SINKHORN_ITERS, threshold=SINKHORN_THRESHOLD,
+                   on_sinkhorn=None):
+    """configs[4] (BASELINE.json): ``model`` (a LightGlue with ``return_similarity``) matches
+    ``data``; its final head's similarity goes through ``log_optimal_transport`` and
+    ``filter_matches``.  ``on_sinkhorn(t0, t1)`` (optional) is called with two recorded CUDA events
+    around the Sinkhorn call (bench.py times the kernel with them).  Returns the matches dict and Z."""
+    pred = model(data)
+    sim = pred["similarity"]
+    if isinstance(sim, list):
+        raise ValueError("sinkhorn_match needs a dense similarity (pruning off)")
+    e0 = e1 = None
+    if on_sinkhorn is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    Z = log_optimal_transport(sim, alpha, iters)
+    if on_sinkhorn is not None:
+        e1.record()
+        on_sinkhorn(e0, e1)
+    m0, m1, s0, s1 = filter_matches(Z, threshold)
+    return {"matches0": m0, "matches1": m1, "matching_scores0": s0, "matching_scores1": s1}, Z

@@ -23,6 +23,10 @@
 #include "common.h"
 #include "kernels.h"
 
+#ifndef LG_SK_LOG2
+#define LG_SK_LOG2 1  // sinkhorn_scaled_kernel's row pass in log2 units with packed adds / FMAs (VERDICT r3 item 4;
+                      // 5.186 -> 5.105 ms at configs[4], two alternating same-box rounds, profiles/r04/sk_log2_ab.log)
+#endif
 #ifndef LG_SK_NT
 #define LG_SK_NT 1  // streaming (non-temporal) score loads in sinkhorn_scaled_kernel: 5.94 -> 5.21 ms at B = 8, N = 4096
 #endif
@@ -340,9 +344,13 @@ __global__ __launch_bounds__(W * 64) void sinkhorn_scaled_kernel(const float* __
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x / P, p = blockIdx.x - b * P;
   const float* vb = v + (size_t)b * (N + 1);
-  for (int j = tid; j < 4 * (kSkMaxN / 4 + 1); j += W * 64) reinterpret_cast<float*>(vs)[j] = j < N ? vb[j] : 0.f;
+  // LG_SK_LOG2: the row pass works in log2 units (v staged as v log2 e, scores scaled by the same
+  // FMA that adds v), so the exponentials are bare v_exp_f32 with no per-score multiply, and the
+  // adds / FMAs run two columns per packed instruction
+  constexpr float vsc = LG_SK_LOG2 ? 1.4426950408889634f : 1.f;
+  for (int j = tid; j < 4 * (kSkMaxN / 4 + 1); j += W * 64) reinterpret_cast<float*>(vs)[j] = j < N ? vb[j] * vsc : 0.f;
   const float vbin = vb[N];
-  const float ybin = alpha + vbin;
+  const float ybin = LG_SK_LOG2 ? (alpha + vbin) * vsc : alpha + vbin;
   __syncthreads();
 
   float acc[K4][4];
@@ -358,6 +366,51 @@ __global__ __launch_bounds__(W * 64) void sinkhorn_scaled_kernel(const float* __
   auto process = [&](float (&y)[K4][4], int i, bool bin_row) {
     asm volatile("" ::: "memory");  // re-read v from LDS per row rather than pinning 4*K4 registers
     float m = ybin;
+#if LG_SK_LOG2
+    const f32x2_ L2 = {vsc, vsc};
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const float4 vv = vs[min(64 * k + lane, kSkMaxN / 4)];
+      const f32x2_ t0 = __builtin_elementwise_fma(f32x2_{y[k][0], y[k][1]}, L2, f32x2_{vv.x, vv.y});
+      const f32x2_ t1 = __builtin_elementwise_fma(f32x2_{y[k][2], y[k][3]}, L2, f32x2_{vv.z, vv.w});
+      y[k][0] = t0.x;
+      y[k][1] = t0.y;
+      y[k][2] = t1.x;
+      y[k][3] = t1.y;
+      m = fmaxf(m, fmaxf(t0.x, t0.y));
+      m = fmaxf(m, fmaxf(t1.x, t1.y));
+    }
+    m = wave_max_dpp(m);
+    const float eb = __builtin_amdgcn_exp2f(ybin - m);
+    f32x2_ s2 = {lane == 0 ? eb : 0.f, 0.f};
+    const f32x2_ nm = {-m, -m};
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const f32x2_ d0 = f32x2_{y[k][0], y[k][1]} + nm, d1 = f32x2_{y[k][2], y[k][3]} + nm;
+      y[k][0] = __builtin_amdgcn_exp2f(d0.x);
+      y[k][1] = __builtin_amdgcn_exp2f(d0.y);
+      y[k][2] = __builtin_amdgcn_exp2f(d1.x);
+      y[k][3] = __builtin_amdgcn_exp2f(d1.y);
+      s2 += f32x2_{y[k][0], y[k][1]} + f32x2_{y[k][2], y[k][3]};
+    }
+    const float s = wave_sum_dpp(s2.x + s2.y);
+    const float lm = bin_row ? lm_bin : lm_in;
+    const float l2s = __log2f(s);
+    const float ui = lm - (m + l2s) * 0.6931471805599453f;  // superglue.py:178, natural units
+    if (lane == 0) u[(size_t)b * (M + 1) + i] = ui;
+    const float a = __builtin_amdgcn_exp2f(lm * vsc - l2s);
+    const f32x2_ a2 = {a, a};
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const f32x2_ r0 = __builtin_elementwise_fma(f32x2_{y[k][0], y[k][1]}, a2, f32x2_{acc[k][0], acc[k][1]});
+      const f32x2_ r1 = __builtin_elementwise_fma(f32x2_{y[k][2], y[k][3]}, a2, f32x2_{acc[k][2], acc[k][3]});
+      acc[k][0] = r0.x;
+      acc[k][1] = r0.y;
+      acc[k][2] = r1.x;
+      acc[k][3] = r1.y;
+    }
+    accb = fmaf(eb, a, accb);
+#else
 #pragma unroll
     for (int k = 0; k < K4; ++k) {
       const float4 vv = vs[min(64 * k + lane, kSkMaxN / 4)];
@@ -389,6 +442,7 @@ __global__ __launch_bounds__(W * 64) void sinkhorn_scaled_kernel(const float* __
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[k][e] = fmaf(y[k][e], a, acc[k][e]);
     accb = fmaf(eb, a, accb);
+#endif
   };
   const int rl = min(r1, M);  // real rows; the dustbin row M (all alpha) is handled after
   auto load = [&](float (&y)[K4][4], int i) {

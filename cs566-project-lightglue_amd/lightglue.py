@@ -664,7 +664,7 @@ class LightGlue(nn.Module):
                 pred["ref_descriptors0"] = [rd0[i, None, : ks[0][i]] for i in range(b)]
                 pred["ref_descriptors1"] = [rd1[i, None, : ks[1][i]] for i in range(b)]
                 if sim is not None:
-                    pred["similarity"] = [sim[i, None, : ks[0][i], : ks[1][i]] for i in range(b)]
+                    pred["similarity"] = [sim[i, : ks[0][i], : ks[1][i]] for i in range(b)]
         return pred
 
     # ------------------------------------------------------------ profiling (bench.py)

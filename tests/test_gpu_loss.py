@@ -106,8 +106,9 @@ def test_assignment_head_and_similarity_agree_with_forward():
 @pytest.mark.parametrize("B", [1, 3])
 def test_similarity_with_pruning_is_the_kept_block(B):
     """With width pruning and return_similarity, pred["similarity"] is sliced like log_assignment
-    (b == 1: [1, M', N']; b > 1: per-pair list of [1, M_b, N_b]) and holds md0 md1^T of the kept
-    descriptors (ref_descriptors*, same compacted order) -- ADVICE r3."""
+    (b == 1: [1, M', N']; b > 1: per-pair list of [M_b, N_b], as the [M_b+1, N_b+1] log-assignment
+    list) and holds md0 md1^T of the kept descriptors (ref_descriptors*, same compacted order) --
+    ADVICE r3."""
     from golden_util import PRUNE_BIAS
     from lightglue_amd import LightGlue
     from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
@@ -135,8 +136,9 @@ def test_similarity_with_pruning_is_the_kept_block(B):
     for sim, la, r0, r1 in zip(sims, las, rd0s, rd1s):
         k0, k1 = r0.shape[-2], r1.shape[-2]
         pruned |= k0 < 512 or k1 < 480
-        assert sim.shape == (1, k0, k1) and la.shape == (1, k0 + 1, k1 + 1)
-        md0 = (r0[:, 0].double() @ W.T + bb) / 4.0
-        md1 = (r1[:, 0].double() @ W.T + bb) / 4.0
-        torch.testing.assert_close(sim.double(), md0 @ md1.transpose(1, 2), atol=2e-5, rtol=1e-5)
+        assert tuple(sim.shape[-2:]) == (k0, k1) and tuple(la.shape[-2:]) == (k0 + 1, k1 + 1)
+        assert sim.dim() == la.dim()
+        md0 = (r0.reshape(k0, 256).double() @ W.T + bb) / 4.0
+        md1 = (r1.reshape(k1, 256).double() @ W.T + bb) / 4.0
+        torch.testing.assert_close(sim.reshape(k0, k1).double(), md0 @ md1.T, atol=2e-5, rtol=1e-5)
     assert pruned

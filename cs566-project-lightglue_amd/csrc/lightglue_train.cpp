@@ -495,7 +495,7 @@ HeadScratch carve_head_scratch(char* base, int B, int M, int N) {
   s.GT = c.f(R);
   s.ws_floats = std::max({tgemm_ws_floats(D, D, (int)R, 1), tgemm_ws_floats(M, D, N, B), tgemm_ws_floats(N, D, M, B)});
   s.WS = c.f(s.ws_floats + 64);
-  s.PART = c.f(colsum_part_floats((int)R, D) + 64);
+  s.PART = c.f(std::max({colsum_part_floats((int)R, D), sim_lse_part_floats(B, M, N), la_grad_sums_part_floats(B, M, N)}) + 64);
   s.bytes = c.off;
   return s;
 }
@@ -541,9 +541,9 @@ int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, 
     TGemm g{s.MD, s.MD + o1, s.SIM, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B, 1.f, 0.f, nullptr};
     TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st));
   }
-  TR_HIP(sim_lse(s.SIM, B, M, N, s.LSER, s.LSEC, c.st));
+  TR_HIP(sim_lse(s.SIM, B, M, N, s.LSER, s.LSEC, c.part, c.st));
   // sigmoid_log_double_softmax backward (:284-296)
-  TR_HIP(la_grad_sums(la_grad, s_in, s_dust, B, M, N, s.RS, s.RS + R0, s.GD, s.GD + R0, c.st));
+  TR_HIP(la_grad_sums(la_grad, s_in, s_dust, B, M, N, s.RS, s.RS + R0, s.GD, s.GD + R0, c.part, c.st));
   TR_HIP(la_grad_sim(s.SIM, la_grad, s_in, s.LSER, s.LSEC, s.RS, s.RS + R0, grad_similarity, B, M, N, c.st));
   TR_HIP(la_grad_z(s.Z, s.RS, s.GD, R, s.GZ, c.st));
   // d/d(final_proj output) = d/d(md) / 4: gmd0 = gsim md1, gmd1 = gsim^T md0

@@ -115,12 +115,14 @@ hipError_t add_layer_rows(float* GX, const float* g0, const float* g1, int B, in
 
 // ---- assignment head backward (MatchAssignment + sigmoid_log_double_softmax, lightglue.py:284-315)
 // sim [B][M][N]: lser [B*M], lsec [B*N] natural-log row / column logsumexp
-hipError_t sim_lse(const float* sim, int B, int M, int N, float* lser, float* lsec, hipStream_t st);
+size_t sim_lse_part_floats(int B, int M, int N);
+hipError_t sim_lse(const float* sim, int B, int M, int N, float* lser, float* lsec, float* part, hipStream_t st);
 // Gradient of the log assignment T [B][M+1][N+1] scaled per pair (s_in for the inner block,
 // s_dust for the dustbins; null = 1): rs [B*M] / cs [B*N] = scaled inner row / column sums,
 // gd0 [B*M] / gd1 [B*N] = scaled dustbin entries.
+size_t la_grad_sums_part_floats(int B, int M, int N);
 hipError_t la_grad_sums(const float* T, const float* s_in, const float* s_dust, int B, int M, int N, float* rs,
-                        float* cs, float* gd0, float* gd1, hipStream_t st);
+                        float* cs, float* gd0, float* gd1, float* part, hipStream_t st);
 // In place: sim -> d(loss)/d(sim) = 2 g - softmax_row * rs - softmax_col * cs (+ gsim_ext);
 // gz0 [B*M] / gz1 [B*N] = d/d(matchability logits).
 hipError_t la_grad_sim(float* sim, const float* T, const float* s_in, const float* lser, const float* lsec,

@@ -722,25 +722,88 @@ __global__ __launch_bounds__(256) void lngelu_bwd_kernel(const float* gout, cons
 }
 
 // ============================================================================ column sums
-constexpr int CS_BLOCKS = 256;
+// out[c] = sum_r s[r] G[r][c]: workgroups of 4 row lanes x 64 columns (a wave reads 256 contiguous
+// bytes of one row per load), ~2048 workgroups over (column blocks, row chunks), fixed-order
+// partials, then the same kernel again over the partials until one row is left.
+constexpr int CS_TARGET_WG = 2048;
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* G, long long ld, int rows, int cols,
-                                                          const float* s, int rpb, float* part) {
-  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (int c = threadIdx.x; c < cols; c += 256) {
-    float acc = 0.f;
-    for (int r = r0; r < r1; ++r) {
-      const float v = G[(long long)r * ld + c];
-      acc = s ? fmaf(s[r], v, acc) : acc + v;
+                                                          const float* s, int rpb, float* part, long long sG = 0,
+                                                          long long sP = 0) {
+  __shared__ float red[4][64];
+  G += blockIdx.z * sG;
+  part += blockIdx.z * sP;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  float a0 = 0.f, a1 = 0.f;
+  if (c < cols) {
+    int r = r0 + g;
+    for (; r + 4 < r1; r += 8) {
+      const float v0 = G[(long long)r * ld + c], v1 = G[(long long)(r + 4) * ld + c];
+      a0 = s ? fmaf(s[r], v0, a0) : a0 + v0;
+      a1 = s ? fmaf(s[r + 4], v1, a1) : a1 + v1;
     }
-    part[(long long)blockIdx.x * cols + c] = acc;
+    if (r < r1) {
+      const float v0 = G[(long long)r * ld + c];
+      a0 = s ? fmaf(s[r], v0, a0) : a0 + v0;
+    }
+  }
+  red[g][threadIdx.x & 63] = a0 + a1;
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    const int t = threadIdx.x;
+    part[(long long)blockIdx.y * cols + c] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
   }
 }
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nblk, int cols, float* out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float acc = 0.f;
-  for (int i = 0; i < nblk; ++i) acc += part[(long long)i * cols + c];
-  out[c] = acc;
+
+// column logsumexp of sim [B][M][N] in row chunks: (max, sum) partials [B][chunks][N], merged in
+// chunk order
+constexpr int LSE_ROWS = 64;
+__global__ __launch_bounds__(256) void sim_lse_col_part_kernel(const float* sim, int M, int N, float2* part) {
+  __shared__ float2 red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6, b = blockIdx.z;
+  const int r0 = blockIdx.y * LSE_ROWS, r1 = min(M, r0 + LSE_ROWS);
+  float m = -INFINITY, acc = 0.f;
+  if (c < N) {
+    const float* s = sim + (long long)b * M * N + c;
+    for (int r = r0 + g; r < r1; r += 4) {
+      const float v = s[(long long)r * N];
+      if (v > m) {
+        acc = acc * expf(m - v) + 1.f;
+        m = v;
+      } else {
+        acc += expf(v - m);
+      }
+    }
+  }
+  red[g][threadIdx.x & 63] = make_float2(m, acc);
+  __syncthreads();
+  if (g == 0 && c < N) {
+    float mm = -INFINITY, ss = 0.f;
+    for (int k = 0; k < 4; ++k) {
+      const float2 o = red[k][threadIdx.x];
+      const float mx = fmaxf(mm, o.x);
+      if (mx > -INFINITY) {
+        ss = ss * expf(mm - mx) + o.y * expf(o.x - mx);
+        mm = mx;
+      }
+    }
+    part[((long long)b * gridDim.y + blockIdx.y) * N + c] = make_float2(mm, ss);
+  }
+}
+__global__ __launch_bounds__(256) void sim_lse_col_final_kernel(const float2* part, int nch, int B, int N, float* lsec) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (long long)B * N) return;
+  const long long b = id / N, c = id - b * N;
+  float mm = -INFINITY, ss = 0.f;
+  for (int k = 0; k < nch; ++k) {
+    const float2 o = part[(b * nch + k) * N + c];
+    const float mx = fmaxf(mm, o.x);
+    if (mx > -INFINITY) {
+      ss = ss * expf(mm - mx) + o.y * expf(o.x - mx);
+      mm = mx;
+    }
+  }
+  lsec[id] = mm + logf(ss);
 }
 
 // ============================================================================ small row ops
@@ -793,18 +856,6 @@ __global__ __launch_bounds__(256) void sim_lse_row_kernel(const float* sim, int 
   acc = wave_sum(acc);
   if (l == 0) lser[row] = m + logf(acc);
 }
-// column logsumexp: a thread per (pair, column) walks the rows (coalesced across the block)
-__global__ __launch_bounds__(256) void sim_lse_col_kernel(const float* sim, int B, int M, int N, float* lsec) {
-  const int j = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
-  if (j >= N) return;
-  const float* s = sim + (long long)b * M * N + j;
-  float m = -INFINITY;
-  for (int i = 0; i < M; ++i) m = fmaxf(m, s[(long long)i * N]);
-  float acc = 0.f;
-  for (int i = 0; i < M; ++i) acc += expf(s[(long long)i * N] - m);
-  lsec[(long long)b * N + j] = m + logf(acc);
-}
-
 __global__ __launch_bounds__(256) void la_row_sums_kernel(const float* T, const float* s_in, const float* s_dust, int B,
                                                           int M, int N, float* rs, float* gd0) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
@@ -819,15 +870,16 @@ __global__ __launch_bounds__(256) void la_row_sums_kernel(const float* T, const 
     gd0[row] = t[N] * (s_dust ? s_dust[b] : 1.f);
   }
 }
-__global__ __launch_bounds__(256) void la_col_sums_kernel(const float* T, const float* s_in, const float* s_dust, int B,
-                                                          int M, int N, float* cs, float* gd1) {
+__global__ __launch_bounds__(256) void la_col_final_kernel(const float* part, int nb, const float* T, const float* s_in,
+                                                           const float* s_dust, int B, int M, int N, float* cs,
+                                                           float* gd1) {
   const int j = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
   if (j >= N) return;
-  const float* t = T + (long long)b * (M + 1) * (N + 1) + j;
+  const float* p = part + (long long)b * nb * N + j;
   float acc = 0.f;
-  for (int i = 0; i < M; ++i) acc += t[(long long)i * (N + 1)];
+  for (int k = 0; k < nb; ++k) acc += p[(long long)k * N];
   cs[(long long)b * N + j] = acc * (s_in ? s_in[b] : 1.f);
-  gd1[(long long)b * N + j] = t[(long long)M * (N + 1)] * (s_dust ? s_dust[b] : 1.f);
+  gd1[(long long)b * N + j] = T[(long long)b * (M + 1) * (N + 1) + (long long)M * (N + 1) + j] * (s_dust ? s_dust[b] : 1.f);
 }
 
 __global__ __launch_bounds__(256) void la_grad_sim_kernel(float* sim, const float* T, const float* s_in,
@@ -976,31 +1028,61 @@ hipError_t lngelu_fwd(const float* h, const float* gamma, const float* beta, int
   return hipGetLastError();
 }
 
-size_t lngelu_bwd_part_floats(int R) { return (size_t)cdiv(std::max(R, 1), LN_ROWS) * 2 * 512; }
+size_t lngelu_bwd_part_floats(int R) {
+  const int nblk = (int)cdiv(std::max(R, 1), LN_ROWS);
+  return (size_t)nblk * 1024 + colsum_part_floats(nblk, 512);
+}
 
 hipError_t lngelu_bwd(const float* gout, const float* h, const float* stats, const float* gamma, const float* beta,
                       int R, float* gh, float* part, float* dgamma, float* dbeta, hipStream_t st) {
   const int nblk = (int)cdiv(std::max(R, 1), LN_ROWS);
   hipLaunchKernelGGL(lngelu_bwd_kernel, dim3(nblk), dim3(256), 0, st, gout, h, stats, gamma, beta, R, gh, part);
   // dgamma = sum of the even partial rows, dbeta of the odd ones: [blk][2][512] read as [blk*2][512]
-  if (dgamma)
-    hipLaunchKernelGGL(colsum_part_kernel, dim3(1), dim3(256), 0, st, part, 1024ll, nblk, 512, (const float*)nullptr, nblk,
-                       dgamma);
-  if (dbeta)
-    hipLaunchKernelGGL(colsum_part_kernel, dim3(1), dim3(256), 0, st, part + 512, 1024ll, nblk, 512, (const float*)nullptr,
-                       nblk, dbeta);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  // dgamma / dbeta: column sums of the partial rows [blk][2][512] (read as two 512-wide windows of
+  // [blk][1024]); the sums' own partials go after the LN partials
+  float* cs_part = part + (size_t)nblk * 1024;
+  if (e == hipSuccess && dgamma) e = colsum(part, 1024, nblk, 512, nullptr, cs_part, dgamma, st);
+  if (e == hipSuccess && dbeta) e = colsum(part + 512, 1024, nblk, 512, nullptr, cs_part, dbeta, st);
+  return e;
 }
 
-size_t colsum_part_floats(int rows, int cols) { return (size_t)CS_BLOCKS * std::max(cols, 1); }
+namespace {
+int cs_chunks(int rows, int cols) {
+  const int cb = (cols + 63) / 64;
+  return std::max(1, std::min((rows + 15) / 16, CS_TARGET_WG / cb));
+}
+}  // namespace
+
+size_t colsum_part_floats(int rows, int cols) {
+  size_t total = 0;
+  for (int nb = cs_chunks(std::max(rows, 1), cols); nb > 1; nb = cs_chunks(nb, cols)) total += (size_t)nb * std::max(cols, 1);
+  return total + std::max(cols, 1);
+}
 
 hipError_t colsum(const float* G, long long ld, int rows, int cols, const float* s, float* part, float* out,
                   hipStream_t st) {
   if (cols == 0) return hipSuccess;
-  const int rpb = std::max(1, (int)cdiv(std::max(rows, 1), CS_BLOCKS));
-  const int nblk = (int)cdiv(std::max(rows, 1), rpb);
-  hipLaunchKernelGGL(colsum_part_kernel, dim3(nblk), dim3(256), 0, st, G, ld, rows, cols, s, rpb, part);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, st, part, nblk, cols, out);
+  if (rows == 0) return hipMemsetAsync(out, 0, sizeof(float) * cols, st);
+  const int cb = (cols + 63) / 64;
+  const float* src = G;
+  long long sld = ld;
+  const float* sc = s;
+  int n = rows;
+  float* p = part;
+  while (true) {
+    const int nb = cs_chunks(n, cols);
+    const int rpb = (n + nb - 1) / nb;
+    const int m = (n + rpb - 1) / rpb;
+    float* dst = m == 1 ? out : p;
+    hipLaunchKernelGGL(colsum_part_kernel, dim3(cb, m), dim3(256), 0, st, src, sld, n, cols, sc, rpb, dst);
+    if (m == 1) break;
+    src = p;
+    sld = cols;
+    sc = nullptr;
+    n = m;
+    p += (size_t)m * cols;
+  }
   return hipGetLastError();
 }
 
@@ -1032,21 +1114,42 @@ hipError_t add_layer_rows(float* GX, const float* g0, const float* g1, int B, in
   return hipGetLastError();
 }
 
-hipError_t sim_lse(const float* sim, int B, int M, int N, float* lser, float* lsec, hipStream_t st) {
+size_t sim_lse_part_floats(int B, int M, int N) { return 2 * (size_t)B * cdiv(std::max(M, 1), LSE_ROWS) * N; }
+
+hipError_t sim_lse(const float* sim, int B, int M, int N, float* lser, float* lsec, float* part, hipStream_t st) {
   if (B * M == 0 || N == 0) return hipSuccess;
   hipLaunchKernelGGL(sim_lse_row_kernel, dim3(cdiv((long long)B * M, 4)), dim3(256), 0, st, sim, B * M, N, lser);
-  hipLaunchKernelGGL(sim_lse_col_kernel, dim3(cdiv(N, 256), B), dim3(256), 0, st, sim, B, M, N, lsec);
+  const int nch = (int)cdiv(M, LSE_ROWS);
+  float2* p2 = reinterpret_cast<float2*>(part);
+  hipLaunchKernelGGL(sim_lse_col_part_kernel, dim3(cdiv(N, 64), nch, B), dim3(256), 0, st, sim, M, N, p2);
+  hipLaunchKernelGGL(sim_lse_col_final_kernel, dim3(cdiv((long long)B * N, 256)), dim3(256), 0, st, p2, nch, B, N, lsec);
   return hipGetLastError();
 }
 
+size_t la_grad_sums_part_floats(int B, int M, int N) {
+  const int cb = (int)cdiv(std::max(N, 1), 64);
+  const int nb = std::max(1, std::min((int)cdiv(std::max(M, 1), 16), std::max(1, CS_TARGET_WG / (cb * std::max(B, 1)))));
+  return (size_t)B * nb * std::max(N, 1);
+}
+
 hipError_t la_grad_sums(const float* T, const float* s_in, const float* s_dust, int B, int M, int N, float* rs,
-                        float* cs, float* gd0, float* gd1, hipStream_t st) {
+                        float* cs, float* gd0, float* gd1, float* part, hipStream_t st) {
   if (B == 0) return hipSuccess;
   if (M > 0)
     hipLaunchKernelGGL(la_row_sums_kernel, dim3(cdiv((long long)B * M, 4)), dim3(256), 0, st, T, s_in, s_dust, B, M, N, rs,
                        gd0);
-  if (N > 0)
-    hipLaunchKernelGGL(la_col_sums_kernel, dim3(cdiv(N, 256), B), dim3(256), 0, st, T, s_in, s_dust, B, M, N, cs, gd1);
+  if (N > 0) {
+    // inner column sums per pair: batched two-pass column sums (partials [B][nb][N]), then one
+    // scaling pass that also picks up the dustbin-row entries
+    const int cb = (int)cdiv(N, 64);
+    const int nb = std::max(1, std::min((int)cdiv(std::max(M, 1), 16), std::max(1, CS_TARGET_WG / (cb * B))));
+    const int rpb = (int)cdiv(std::max(M, 1), nb);
+    const int m = (int)cdiv(std::max(M, 1), rpb);
+    hipLaunchKernelGGL(colsum_part_kernel, dim3(cb, m, B), dim3(256), 0, st, T, (long long)(N + 1), M, N,
+                       (const float*)nullptr, rpb, part, (long long)(M + 1) * (N + 1), (long long)m * N);
+    hipLaunchKernelGGL(la_col_final_kernel, dim3(cdiv(N, 256), B), dim3(256), 0, st, part, m, T, s_in, s_dust, B, M, N, cs,
+                       gd1);
+  }
   return hipGetLastError();
 }
 

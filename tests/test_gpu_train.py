@@ -215,3 +215,65 @@ def test_head_backward_dense_and_similarity_gradients():
               "log_assignment.0.matchability.weight", "log_assignment.0.matchability.bias"):
         r = W[n].grad.numpy()
         np.testing.assert_allclose(named[n].grad.cpu().double().numpy(), r, atol=1e-5 * np.abs(r).max(), rtol=0)
+
+
+@pytest.mark.parametrize("conf,B,M,N", [({"n_layers": 2}, 2, 70, 45), ({"n_layers": 1, "input_dim": 64}, 1, 33, 130),
+                                        ({"n_layers": 2, "add_scale_ori": True}, 3, 40, 40)])
+def test_trunk_backward_ragged_vs_oracle(conf, B, M, N):
+    """The training trunk (lg_train_forward / lg_train_backward) on ragged sets (M != N, sizes that
+    are no multiple of any tile), input_proj and scale/ori positions, under an arbitrary loss on
+    every layer's descriptors: every parameter gradient and both descriptor gradients against
+    float64 autograd of the oracle (oracle/lightglue_train_ref.train_forward).  Bar: 2e-5 of each
+    tensor's largest entry (fp32 arithmetic through <= 2 layers)."""
+    from lightglue_amd import LightGlue
+    from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
+    from oracle.lightglue_train_ref import train_forward
+
+    sd = synthetic_state_dict(conf, seed=11)
+    pair = synthetic_pair(B=B, M=M, N=N, seed=12, dim=int(conf.get("input_dim", 256)))
+    if conf.get("add_scale_ori"):
+        rng = np.random.Generator(np.random.PCG64(5))
+        for k, n in (("0", M), ("1", N)):
+            pair["scales" + k] = (rng.random((B, n)) * 2).astype(np.float32)
+            pair["oris" + k] = (rng.random((B, n)) * 6.28 - 3.14).astype(np.float32)
+    L = int(conf["n_layers"])
+    gen = torch.Generator().manual_seed(7)
+    w0 = torch.randn(B, L, M, 256, generator=gen)
+    w1 = torch.randn(B, L, N, 256, generator=gen)
+    # float64 oracle
+    W = {k: torch.from_numpy(v).double().requires_grad_() for k, v in sd.items()}
+    data64 = {k: torch.from_numpy(v).double() for k, v in pair.items() if not k.startswith("descriptors")}
+    x0 = torch.from_numpy(pair["descriptors0"]).double().requires_grad_()
+    x1 = torch.from_numpy(pair["descriptors1"]).double().requires_grad_()
+    data64["descriptors0"], data64["descriptors1"] = x0, x1
+    layers, _ = train_forward(W, data64, conf)
+    loss64 = sum((a * w0[:, i].double()).sum() + (b * w1[:, i].double()).sum() for i, (a, b) in enumerate(layers))
+    loss64.backward()
+    # HIP
+    model = LightGlue(conf).to(DEV)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model.train()
+    data = {k: torch.from_numpy(v).to(DEV) for k, v in pair.items() if not k.startswith(("image_size", "descriptors"))}
+    g0 = torch.from_numpy(pair["descriptors0"]).to(DEV).requires_grad_()
+    g1 = torch.from_numpy(pair["descriptors1"]).to(DEV).requires_grad_()
+    data["descriptors0"], data["descriptors1"] = g0, g1
+    data["view0"] = {"image_size": torch.from_numpy(pair["image_size0"]).to(DEV)}
+    data["view1"] = {"image_size": torch.from_numpy(pair["image_size1"]).to(DEV)}
+    pred = model(data)
+    ((pred["ref_descriptors0"] * w0.to(DEV)).sum() + (pred["ref_descriptors1"] * w1.to(DEV)).sum()).backward()
+    named = dict(model.named_parameters())
+    bad = []
+    for n, w in W.items():
+        if not n.startswith(("input_proj", "posenc.Wr", "transformers")):
+            continue
+        r = w.grad.numpy()
+        got = named[n].grad.double().cpu().numpy()
+        err, scale = np.abs(got - r).max(), np.abs(r).max()
+        if err > 2e-5 * scale + 1e-9:
+            bad.append((n, float(err), float(scale)))
+    for got, ref, key in ((g0, x0, "d0"), (g1, x1, "d1")):
+        r = ref.grad.numpy()
+        err = np.abs(got.grad.double().cpu().numpy() - r).max()
+        if err > 2e-5 * np.abs(r).max() + 1e-9:
+            bad.append((key, float(err), float(np.abs(r).max())))
+    assert not bad, bad[:8]

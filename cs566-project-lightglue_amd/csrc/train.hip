@@ -31,7 +31,11 @@ __device__ __forceinline__ f32x16 zero16() {
 // staged in LDS k-major ([k][128 + 32]): a lane reads column (tile base + lane&31) of k-row
 // 2s + (lane>>5); the 160-float row pitch puts the two lane halves on disjoint bank halves.
 // Operands stored the other way round (m-major in memory) are transposed on the LDS write.
-constexpr int TG_BM = 128, TG_BN = 128, TG_BK = 32, TG_P = 160;
+#ifndef LG_TG_BK
+#define LG_TG_BK 16  // k-tile of the training GEMM (16: 40 KiB of LDS, several workgroups per CU)
+#endif
+constexpr int TG_BM = 128, TG_BN = 128, TG_BK = LG_TG_BK, TG_P = 160;
+constexpr int TG_Q = TG_BK / 8;  // float4 loads per thread per operand and k-tile
 
 struct TGemmK {
   TGemm g;
@@ -43,11 +47,11 @@ struct TGemmK {
 // X(i, k) for i in [i0, i0 + 128), k in [k0, k0 + 32): KMAJ -> X[k*ld + i], else X[i*ld + k]
 template <bool KMAJ>
 __device__ __forceinline__ void tg_load(const float* X, long long ld, int i0, int D, int k0, int kend, int vec, int t,
-                                        f32x4 (&r)[4]) {
-  if (KMAJ) {
+                                        f32x4 (&r)[TG_Q]) {
+  if (KMAJ) {  // TG_BK k-rows of 128 i: thread t -> k-row (t >> 5) + 8q, i 4(t & 31) .. +3
     const int kr = t >> 5, i = i0 + (t & 31) * 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < TG_Q; ++q) {
       const int k = k0 + kr + 8 * q;
       if (vec && k < kend && i + 3 < D) {
         r[q] = *reinterpret_cast<const f32x4*>(X + (long long)k * ld + i);
@@ -56,11 +60,12 @@ __device__ __forceinline__ void tg_load(const float* X, long long ld, int i0, in
         for (int e = 0; e < 4; ++e) r[q][e] = (k < kend && i + e < D) ? X[(long long)k * ld + i + e] : 0.f;
       }
     }
-  } else {
-    const int ir = t >> 3, k = k0 + (t & 7) * 4;
+  } else {  // 128 i-rows of TG_BK k: thread t -> row (t / (TG_BK/4)) + (1024/TG_BK) q, k 4(t % (TG_BK/4)) .. +3
+    constexpr int KQ = TG_BK / 4, RS = 256 / KQ;
+    const int ir = t / KQ, k = k0 + (t % KQ) * 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = i0 + ir + 32 * q;
+    for (int q = 0; q < TG_Q; ++q) {
+      const int i = i0 + ir + RS * q;
       if (vec && i < D && k + 3 < kend) {
         r[q] = *reinterpret_cast<const f32x4*>(X + (long long)i * ld + k);
       } else {
@@ -72,17 +77,18 @@ __device__ __forceinline__ void tg_load(const float* X, long long ld, int i0, in
 }
 
 template <bool KMAJ>
-__device__ __forceinline__ void tg_store(float* S, int t, const f32x4 (&r)[4]) {
+__device__ __forceinline__ void tg_store(float* S, int t, const f32x4 (&r)[TG_Q]) {
   if (KMAJ) {
     const int kr = t >> 5, i4 = (t & 31) * 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(S + (kr + 8 * q) * TG_P + i4) = r[q];
+    for (int q = 0; q < TG_Q; ++q) *reinterpret_cast<f32x4*>(S + (kr + 8 * q) * TG_P + i4) = r[q];
   } else {
-    const int ir = t >> 3, k4 = (t & 7) * 4;
+    constexpr int KQ = TG_BK / 4, RS = 256 / KQ;
+    const int ir = t / KQ, k4 = (t % KQ) * 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < TG_Q; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) S[(k4 + e) * TG_P + ir + 32 * q] = r[q][e];
+      for (int e = 0; e < 4; ++e) S[(k4 + e) * TG_P + ir + RS * q] = r[q][e];
   }
 }
 
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemmK p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
-  f32x4 ra[4], rb[4];
+  f32x4 ra[TG_Q], rb[TG_Q];
   if (nk > 0) {
     tg_load<TA>(A, g.lda, m0, g.M, kbeg, kend, p.vecA, t, ra);
     tg_load<!TB>(B, g.ldb, n0, g.N, kbeg, kend, p.vecB, t, rb);
@@ -332,21 +338,26 @@ __global__ __launch_bounds__(256) void tattn_fwd_kernel(TAttn a) {
   if (h == 0) a.lse[(long long)item * a.Nq + qrow] = m + log2f(lsum);
 }
 
-// Backward: a workgroup = 4 waves x 32 keys of one (pair, head); the key sits on the lane, so S
-// and dP come out with their columns = keys and are directly the B operands of dV^T += dO^T P and
-// dK^T += Q^T dS (permuted query order row32 on both operands).  Row constants seed the
-// accumulators (S' = Q (cK)^T - lse, dP' = dO V^T - delta), so p = exp2(S') and dS = p * dP'
-// need no further VALU.  dQ: dS crosses LDS once, each wave multiplies a 32 x 32 quarter of the
-// (32 queries x 64 dims) tile over 64 of the workgroup's 128 keys, and adds it with float
-// atomics (two 128-B row segments per instruction: the full atomic rate).
-constexpr int TB_QP = 66, TB_KP = 66, TB_DP = 136;
+// Backward: a workgroup = 8 waves x 32 keys (256 keys) of one (pair, head); the key sits on the
+// lane, so S and dP come out with their columns = keys and are directly the B operands of
+// dV^T += dO^T P and dK^T += Q^T dS (permuted query order row32 on both operands).  Row constants
+// seed the accumulators (S' = Q (cK)^T - lse, dP' = dO V^T - delta), so p = exp2(S') and
+// dS = p * dP' need no further VALU.  dQ: dS crosses LDS once; each wave owns one 16 x 16 tile
+// (16 queries x 16 dims) of the 32 x 64 dQ tile and sums it over all 256 keys with
+// v_mfma_f32_16x16x4_f32, so every dQ element gets ONE float atomic per workgroup (four 64-B row
+// segments per instruction).  Against 4 waves x 128 keys with 32 x 32 dQ quarters: a quarter of
+// the atomic bytes, and two waves per SIMD.
+constexpr int TB_W = 8, TB_KEYS = 32 * TB_W;
+constexpr int TB_QP = 66, TB_KP = 80, TB_DP = TB_KEYS + 4;
 
-__global__ __launch_bounds__(256) void tattn_bwd_kernel(TAttn a) {
-  __shared__ __attribute__((aligned(16))) float Qs[2][32 * TB_QP];
-  __shared__ __attribute__((aligned(16))) float dOs[2][32 * TB_QP];
-  __shared__ __attribute__((aligned(16))) float Kall[128 * TB_KP];
+__global__ __launch_bounds__(64 * TB_W) void tattn_bwd_kernel(TAttn a) {
+  // one Q / dO tile buffer: the next tile waits in registers and lands after the barrier that
+  // ends this tile's reads of it
+  __shared__ __attribute__((aligned(16))) float Qs[32 * TB_QP];
+  __shared__ __attribute__((aligned(16))) float dOs[32 * TB_QP];
+  __shared__ __attribute__((aligned(16))) float Kall[TB_KEYS * TB_KP];
   __shared__ __attribute__((aligned(16))) float dSs[32 * TB_DP];
-  __shared__ float lse_s[2][32], del_s[2][32];
+  __shared__ float lse_s[32], del_s[32];
   const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, l32 = l & 31;
   const int item = blockIdx.y, b = item / a.H, hd = item - b * a.H;
   const float* Q = a.Q + (long long)b * a.Nq * a.ldq + hd * 64;
@@ -355,7 +366,7 @@ __global__ __launch_bounds__(256) void tattn_bwd_kernel(TAttn a) {
   const float* V = a.V + (long long)b * a.Nk * a.ldv + hd * 64;
   const float* lse = a.lse + (long long)item * a.Nq;
   const float* del = a.delta + (long long)item * a.Nq;
-  const int kb0 = blockIdx.x * 128;
+  const int kb0 = blockIdx.x * TB_KEYS;
   const int key = kb0 + w * 32 + l32;
   const bool kv = key < a.Nk;
   const float c = a.scale * kLog2e;
@@ -369,78 +380,68 @@ __global__ __launch_bounds__(256) void tattn_bwd_kernel(TAttn a) {
 #pragma unroll
     for (int s = 0; s < 32; ++s) kf[s] = vf[s] = 0.f;
   }
-  // the workgroup's 128 keys (unscaled) for dQ: thread t -> rows (t>>4) + 16q, q < 8
+  // the workgroup's 256 keys (unscaled) for dQ: thread t -> rows (t>>4) + 32q, q < 8
   {
     const int sr = t >> 4, sc = (t & 15) * 4;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int k = kb0 + sr + 16 * q;
+    for (int q = 0; q < TB_KEYS / 32; ++q) {
+      const int k = kb0 + sr + 32 * q;
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < a.Nk) v = *reinterpret_cast<const f32x4*>(K + (long long)k * a.ldk + sc);
-      float* kp = Kall + (sr + 16 * q) * TB_KP + sc;
-      *reinterpret_cast<f32x2*>(kp) = f32x2{v[0], v[1]};
-      *reinterpret_cast<f32x2*>(kp + 2) = f32x2{v[2], v[3]};
+      *reinterpret_cast<f32x4*>(Kall + (sr + 32 * q) * TB_KP + sc) = v;
     }
   }
-  // query tiles: 32 rows x 64 floats of Q and dO; thread t -> rows (t>>4) + 16q, q < 2
+  // query tiles: 32 rows x 64 floats of Q and dO; thread t -> row t>>4, columns 4(t&15)..+3
   const int sr = t >> 4, sc = (t & 15) * 4;
-  f32x4 rq[2], rd[2];
+  f32x4 rq, rd;
   float rl = 0.f, rdl = 0.f;
   auto load_q = [&](int qt) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int qi = qt * 32 + sr + 16 * q;
-      if (qi < a.Nq) {
-        rq[q] = *reinterpret_cast<const f32x4*>(Q + (long long)qi * a.ldq + sc);
-        rd[q] = *reinterpret_cast<const f32x4*>(dO + (long long)qi * a.ldo + sc);
-      } else {
-        rq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-        rd[q] = rq[q];
-      }
+    const int qi = qt * 32 + sr;
+    if (qi < a.Nq) {
+      rq = *reinterpret_cast<const f32x4*>(Q + (long long)qi * a.ldq + sc);
+      rd = *reinterpret_cast<const f32x4*>(dO + (long long)qi * a.ldo + sc);
+    } else {
+      rq = f32x4{0.f, 0.f, 0.f, 0.f};
+      rd = rq;
     }
     if (t < 32) {
-      const int qi = qt * 32 + t;
-      rl = qi < a.Nq ? lse[qi] : INFINITY;  // padded queries: p = exp2(-inf) = 0
-      rdl = qi < a.Nq ? del[qi] : 0.f;
+      const int qj = qt * 32 + t;
+      rl = qj < a.Nq ? lse[qj] : INFINITY;  // padded queries: p = exp2(-inf) = 0
+      rdl = qj < a.Nq ? del[qj] : 0.f;
     }
   };
-  auto store_q = [&](int st) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      float* qp = Qs[st] + (sr + 16 * q) * TB_QP + sc;
-      float* dp = dOs[st] + (sr + 16 * q) * TB_QP + sc;
-      *reinterpret_cast<f32x2*>(qp) = f32x2{rq[q][0], rq[q][1]};
-      *reinterpret_cast<f32x2*>(qp + 2) = f32x2{rq[q][2], rq[q][3]};
-      *reinterpret_cast<f32x2*>(dp) = f32x2{rd[q][0], rd[q][1]};
-      *reinterpret_cast<f32x2*>(dp + 2) = f32x2{rd[q][2], rd[q][3]};
-    }
+  auto store_q = [&]() {
+    float* qp = Qs + sr * TB_QP + sc;
+    float* dp = dOs + sr * TB_QP + sc;
+    *reinterpret_cast<f32x2*>(qp) = f32x2{rq[0], rq[1]};
+    *reinterpret_cast<f32x2*>(qp + 2) = f32x2{rq[2], rq[3]};
+    *reinterpret_cast<f32x2*>(dp) = f32x2{rd[0], rd[1]};
+    *reinterpret_cast<f32x2*>(dp + 2) = f32x2{rd[2], rd[3]};
     if (t < 32) {
-      lse_s[st][t] = rl;
-      del_s[st][t] = rdl;
+      lse_s[t] = rl;
+      del_s[t] = rdl;
     }
   };
   f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
   const int nqt = (a.Nq + 31) / 32;
-  const int qdt = w & 1, qkh = w >> 1;  // this wave's dQ quarter: dims 32*qdt.., keys 64*qkh..
-  float* dQ = a.dQ + (long long)b * a.Nq * a.ldq + hd * 64 + 32 * qdt + l32;
+  const int qh = w & 1, dq = w >> 1;  // this wave's dQ tile: queries 16 qh .., dims 16 dq ..
+  const int l16 = l & 15, lk = l >> 4;
+  float* dQ = a.dQ + (long long)b * a.Nq * a.ldq + hd * 64 + 16 * dq + l16;
   load_q(0);
-  store_q(0);
+  store_q();
   __syncthreads();
   for (int qt = 0; qt < nqt; ++qt) {
-    const int cur = qt & 1;
     if (qt + 1 < nqt) load_q(qt + 1);
-    const float* qs = Qs[cur];
-    const float* dos = dOs[cur];
     f32x16 sacc, pacc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      sacc[r] = -lse_s[cur][row32(r, h)];
-      pacc[r] = -del_s[cur][row32(r, h)];
+      sacc[r] = -lse_s[row32(r, h)];
+      pacc[r] = -del_s[row32(r, h)];
     }
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
-      sacc = mfma32(qs[l32 * TB_QP + 2 * s + h], kf[s], sacc);
-      pacc = mfma32(dos[l32 * TB_QP + 2 * s + h], vf[s], pacc);
+      sacc = mfma32(Qs[l32 * TB_QP + 2 * s + h], kf[s], sacc);
+      pacc = mfma32(dOs[l32 * TB_QP + 2 * s + h], vf[s], pacc);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -453,24 +454,24 @@ __global__ __launch_bounds__(256) void tattn_bwd_kernel(TAttn a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qr = row32(r, h) * TB_QP + 32 * dt + l32;
-        dvt[dt] = mfma32(dos[qr], sacc[r], dvt[dt]);
-        dkt[dt] = mfma32(qs[qr], pacc[r], dkt[dt]);
+        dvt[dt] = mfma32(dOs[qr], sacc[r], dvt[dt]);
+        dkt[dt] = mfma32(Qs[qr], pacc[r], dkt[dt]);
       }
 #pragma unroll
     for (int r = 0; r < 16; ++r) dSs[row32(r, h) * TB_DP + w * 32 + l32] = pacc[r];
     __syncthreads();
-    f32x16 qacc = zero16();
+    f32x4 qacc = {0.f, 0.f, 0.f, 0.f};
+    const float* ds_row = dSs + (16 * qh + l16) * TB_DP + lk;
+    const float* k_col = Kall + lk * TB_KP + 16 * dq + l16;
+#pragma unroll 16
+    for (int s = 0; s < TB_KEYS / 4; ++s)
+      qacc = __builtin_amdgcn_mfma_f32_16x16x4f32(ds_row[4 * s], k_col[4 * s * TB_KP], qacc, 0, 0, 0);
 #pragma unroll
-    for (int s = 0; s < 32; ++s) {
-      const int kl = qkh * 64 + 2 * s + h;
-      qacc = mfma32(dSs[l32 * TB_DP + kl], Kall[kl * TB_KP + 32 * qdt + l32], qacc);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qi = qt * 32 + row32(r, h);
+    for (int r = 0; r < 4; ++r) {
+      const int qi = qt * 32 + 16 * qh + 4 * lk + r;
       if (qi < a.Nq) atomicAdd(dQ + (long long)qi * a.ldq, qacc[r] * a.scale);
     }
-    if (qt + 1 < nqt) store_q(cur ^ 1);
+    if (qt + 1 < nqt) store_q();  // every wave is past this tile's reads of Qs / dOs (barrier above)
     __syncthreads();
   }
   if (!kv) return;
@@ -977,7 +978,7 @@ hipError_t tattn_forward(const TAttn& a, hipStream_t st) {
 
 hipError_t tattn_backward(const TAttn& a, hipStream_t st) {
   if (a.B * a.H == 0 || a.Nk == 0) return hipSuccess;
-  hipLaunchKernelGGL(tattn_bwd_kernel, dim3(cdiv(a.Nk, 128), a.B * a.H), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(tattn_bwd_kernel, dim3(cdiv(a.Nk, TB_KEYS), a.B * a.H), dim3(64 * TB_W), 0, st, a);
   return hipGetLastError();
 }
 

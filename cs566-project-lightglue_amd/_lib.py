@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = [
     "lg_train_backward",
     "lg_head_scratch_bytes",
     "lg_head_backward",
+    "lg_head_forward",
     "lg_train_gemm_workspace_bytes",
     "lg_train_gemm",
     "lg_train_attention",
@@ -276,6 +277,7 @@ def load():
             ctypes.c_int,
             [_P, _P, i32, _P, _P, i32, i32, i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, sz, _P],
         ),
+        "lg_head_forward": (ctypes.c_int, [_P, _P, i32, _P, _P, i32, i32, i32, _P, _P, _P, _P, _P, sz, _P]),
         "lg_train_gemm_workspace_bytes": (ctypes.c_int, [i32, i32, i32, i32, ctypes.POINTER(sz)]),
         "lg_train_gemm": (
             ctypes.c_int,

@@ -579,6 +579,44 @@ int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, 
   return LG_OK;
 }
 
+int lg_head_forward(lg_handle_t* h, const float* const* params, int32_t layer, const float* desc0, const float* desc1,
+                    int32_t B, int32_t M, int32_t N, float* log_assignment, float* similarity, float* token_logits0,
+                    float* token_logits1, void* scratch, size_t scratch_bytes, void* stream) {
+  if (!params || !desc0 || !desc1 || !log_assignment || !scratch) return fail(LG_E_INVALID, "null argument");
+  if (int e = check_shape(h, B, M, N)) return e;
+  const int L = handle_config(h)->n_layers;
+  if (layer < 0) layer += L;
+  if (layer < 0 || layer >= L) return fail(LG_E_INVALID, "layer index out of range");
+  if ((token_logits0 || token_logits1) && layer >= L - 1)
+    return fail(LG_E_INVALID, "token_confidence exists for layers 0..n_layers-2 only (lightglue.py:395-397)");
+  HeadScratch s = carve_head_scratch((char*)scratch, B, M, N);
+  if (scratch_bytes < s.bytes) return fail(LG_E_WORKSPACE, "scratch too small: need " + std::to_string(s.bytes));
+  TR_HIP(hipSetDevice(handle_device(h)));
+  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART};
+  const Params P{h, params, nullptr};
+  const std::string a = "log_assignment." + std::to_string(layer);
+  const int R0 = B * M, R = B * (M + N);
+  const size_t o1 = (size_t)R0 * D;
+  float* sim = similarity ? similarity : s.SIM;
+  // md = final_proj(desc) / d**0.25, z = matchability(desc), sim = md0 md1^T (:306-315)
+  TR_HIP(hipMemcpyAsync(s.X, desc0, o1 * 4, hipMemcpyDeviceToDevice, c.st));
+  TR_HIP(hipMemcpyAsync(s.X + o1, desc1, (size_t)(R - R0) * D * 4, hipMemcpyDeviceToDevice, c.st));
+  TR_HIP(linear(c, s.X, D, R, D, P.w(a + ".final_proj.weight"), P.w(a + ".final_proj.bias"), D, s.MD, D, 0.f, 0.25f));
+  TR_HIP(gemv256(s.X, R, P.w(a + ".matchability.weight"), P.w(a + ".matchability.bias"), s.Z, c.st));
+  {
+    TGemm g{s.MD, s.MD + o1, sim, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B, 1.f, 0.f, nullptr};
+    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st));
+  }
+  TR_HIP(sim_lse(sim, B, M, N, s.LSER, s.LSEC, c.part, c.st));
+  TR_HIP(la_forward(sim, s.LSER, s.LSEC, s.Z, s.Z + R0, B, M, N, log_assignment, c.st));
+  if (token_logits0 || token_logits1) {  // TokenConfidence's Linear (:109-110)
+    const std::string t = "token_confidence." + std::to_string(layer) + ".token.0";
+    if (token_logits0) TR_HIP(gemv256(desc0, R0, P.w(t + ".weight"), P.w(t + ".bias"), token_logits0, c.st));
+    if (token_logits1) TR_HIP(gemv256(desc1, R - R0, P.w(t + ".weight"), P.w(t + ".bias"), token_logits1, c.st));
+  }
+  return LG_OK;
+}
+
 // ------------------------------------------------------------------ kernel-level entries (tests)
 int lg_train_gemm_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t batch, size_t* bytes) {
   if (!bytes || M < 0 || N < 0 || K < 0 || batch < 0) return fail(LG_E_INVALID, "bad argument");

@@ -128,5 +128,8 @@ hipError_t la_grad_sums(const float* T, const float* s_in, const float* s_dust, 
 hipError_t la_grad_sim(float* sim, const float* T, const float* s_in, const float* lser, const float* lsec,
                        const float* rs, const float* cs, const float* gsim_ext, int B, int M, int N, hipStream_t st);
 hipError_t la_grad_z(const float* z, const float* rs, const float* gd, int rows, float* gz, hipStream_t st);
+// sigmoid_log_double_softmax forward: la [B][M+1][N+1] from sim, its row / column LSE and z0 / z1
+hipError_t la_forward(const float* sim, const float* lser, const float* lsec, const float* z0, const float* z1, int B, int M,
+                      int N, float* la, hipStream_t st);
 
 }  // namespace lg

@@ -901,6 +901,32 @@ __global__ __launch_bounds__(256) void la_grad_sim_kernel(float* sim, const floa
   sim[id] = v;
 }
 
+// sigmoid_log_double_softmax (lightglue.py:284-296) from sim [B][M][N], its row / column
+// logsumexp and the matchability logits z0 [B*M] / z1 [B*N]: la [B][M+1][N+1]
+__global__ __launch_bounds__(256) void la_forward_kernel(const float* sim, const float* lser, const float* lsec,
+                                                         const float* z0, const float* z1, int B, int M, int N,
+                                                         float* la) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long per = (long long)(M + 1) * (N + 1);
+  if (id >= per * B) return;
+  const int b = (int)(id / per);
+  const long long e = id - b * per;
+  const int i = (int)(e / (N + 1)), j = (int)(e - (long long)i * (N + 1));
+  float v;
+  if (i < M && j < N) {
+    const float s = sim[((long long)b * M + i) * N + j];
+    const float cert = log_sigmoid(z0[(long long)b * M + i]) + log_sigmoid(z1[(long long)b * N + j]);
+    v = ((s - lser[(long long)b * M + i]) + (s - lsec[(long long)b * N + j])) + cert;
+  } else if (i < M) {
+    v = log_sigmoid(-z0[(long long)b * M + i]);
+  } else if (j < N) {
+    v = log_sigmoid(-z1[(long long)b * N + j]);
+  } else {
+    v = 0.f;
+  }
+  la[id] = v;
+}
+
 // d/dz of logsigmoid(z) (inner entries, summed: rs) and logsigmoid(-z) (the dustbin entry gd)
 __global__ __launch_bounds__(256) void la_grad_z_kernel(const float* z, const float* rs, const float* gd, int rows,
                                                         float* gz) {
@@ -1160,6 +1186,14 @@ hipError_t la_grad_sim(float* sim, const float* T, const float* s_in, const floa
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(la_grad_sim_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, sim, T, s_in, lser, lsec, rs, cs, gsim_ext,
                      B, M, N);
+  return hipGetLastError();
+}
+
+hipError_t la_forward(const float* sim, const float* lser, const float* lsec, const float* z0, const float* z1, int B, int M,
+                      int N, float* la, hipStream_t st) {
+  const long long n = (long long)B * (M + 1) * (N + 1);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(la_forward_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, sim, lser, lsec, z0, z1, B, M, N, la);
   return hipGetLastError();
 }
 

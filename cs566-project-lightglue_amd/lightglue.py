@@ -140,7 +140,7 @@ class _TrainTrunk(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, model, inputs, d0, d1, *params):
-        lib = model._ensure_handle(d0.device)
+        lib = model._ensure_handle(d0.device, upload=False)
         ctx.model, ctx.inputs = model, inputs
         b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
         L, dd = int(model.conf.n_layers), int(model.conf.descriptor_dim)
@@ -161,7 +161,7 @@ class _TrainTrunk(torch.autograd.Function):
     def backward(ctx, g_rd0, g_rd1):
         model = ctx.model
         d0, d1, *params = ctx.saved_tensors
-        lib = model._ensure_handle(d0.device)
+        lib = model._ensure_handle(d0.device, upload=False)
         b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
         names = model._schema_names()
         grads = [torch.empty_like(p) if (_trunk_param(nm) and ctx.needs_input_grad[4 + i]) else None
@@ -185,7 +185,7 @@ class _TrainTrunk(torch.autograd.Function):
 
 def _head_backward(model, layer, d0, d1, params, needs, la_grad, s_in, s_dust, g_sim, g_t0, g_t1):
     """lg_head_backward for head ``layer``: (gd0, gd1, per-parameter grads or None)."""
-    lib = model._ensure_handle(d0.device)
+    lib = model._ensure_handle(d0.device, upload=False)
     b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
     L = int(model.conf.n_layers)
     li = layer % L
@@ -208,6 +208,25 @@ def _head_backward(model, layer, d0, d1, params, needs, la_grad, s_in, s_dust, g
     return gd0, gd1, grads
 
 
+def _head_forward(model, layer, d0, d1, params, tokens, similarity=False):
+    """lg_head_forward: MatchAssignment ``layer`` (+ the token logits) on raw parameters, fp32."""
+    lib = model._ensure_handle(d0.device, upload=False)
+    b, m, n = d0.shape[0], d0.shape[1], d1.shape[1]
+    dev = d0.device
+    la = torch.empty((b, m + 1, n + 1), dtype=torch.float32, device=dev)
+    sim = torch.empty((b, m, n), dtype=torch.float32, device=dev) if similarity else None
+    t0 = torch.empty((b, m), dtype=torch.float32, device=dev) if tokens else None
+    t1 = torch.empty((b, n), dtype=torch.float32, device=dev) if tokens else None
+    nb = ctypes.c_size_t()
+    _lib.check(lib.lg_head_scratch_bytes(model._handle, b, m, n, ctypes.byref(nb)), "lg_head_scratch_bytes")
+    scratch = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(lib.lg_head_forward(model._handle, model._param_array(params), int(layer), _ptr(d0), _ptr(d1), b, m, n,
+                                   _ptr(la), _ptr(sim), _ptr(t0), _ptr(t1), _ptr(scratch), nb.value,
+                                   ctypes.c_void_p(stream)), "lg_head_forward")
+    return la, sim, t0, t1
+
+
 class _Head(torch.autograd.Function):
     """``log_assignment[layer](desc0, desc1)`` (MatchAssignment + sigmoid_log_double_softmax,
     lightglue.py:284-315) -> (log_assignment, similarity, token logits 0, token logits 1); the
@@ -216,9 +235,9 @@ class _Head(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, layer, tokens, d0, d1, *params):
         d0c, d1c = d0.float().contiguous(), d1.float().contiguous()
-        out = model.assignment_head(layer, d0c, d1c, token_logits=tokens)
-        la, sim = out[0], out[1]
-        t0, t1 = (out[2], out[3]) if tokens else (la.new_zeros(0), la.new_zeros(0))
+        la, sim, t0, t1 = _head_forward(model, layer, d0c, d1c, params, tokens, similarity=True)
+        if not tokens:
+            t0, t1 = la.new_zeros(0), la.new_zeros(0)
         ctx.model, ctx.layer, ctx.tokens = model, layer, tokens
         ctx.save_for_backward(d0c, d1c, *params)
         return la, sim, t0, t1
@@ -244,15 +263,16 @@ class _HeadNLL(torch.autograd.Function):
     scales instead of a dense gradient."""
 
     @staticmethod
-    def forward(ctx, model, layer, data, balancing, tokens, d0, d1, *params):
-        from .superglue import _nll, nll_weights
+    def forward(ctx, model, layer, gt, balancing, tokens, d0, d1, *params):
+        from .superglue import _nll
 
+        # gt = (data, NLLLoss weights [B, M+1, N+1], nll_inputs(data)): built once per loss()
+        data, w, prepared = gt
         d0c, d1c = d0.float().contiguous(), d1.float().contiguous()
-        out = model.assignment_head(layer, d0c, d1c, token_logits=tokens)
-        la = out[0]
-        t0, t1 = (out[2], out[3]) if tokens else (la.new_zeros(0), la.new_zeros(0))
-        terms = _nll(la, data, 1, float(balancing))  # [5, B]: nll, nll_pos, nll_neg, num_pos, num_neg
-        w = nll_weights(la, data)
+        la, _, t0, t1 = _head_forward(model, layer, d0c, d1c, params, tokens)
+        if not tokens:
+            t0, t1 = la.new_zeros(0), la.new_zeros(0)
+        terms = _nll(la, data, 1, float(balancing), prepared)  # [5, B]: nll, nll_pos, nll_neg, num_pos, num_neg
         ctx.model, ctx.layer, ctx.tokens, ctx.bal = model, layer, tokens, float(balancing)
         ctx.save_for_backward(d0c, d1c, w, terms[3].clone(), terms[4].clone(), *params)
         ctx.mark_non_differentiable(la)
@@ -389,7 +409,10 @@ class LightGlue(nn.Module):
             _lib.PRECISIONS[str(c.precision)],
         )
 
-    def _ensure_handle(self, device):
+    def _ensure_handle(self, device, upload=True):
+        """The native handle for this config on ``device``; with ``upload`` the parameters are
+        (re)packed into it when they changed.  The training path passes raw parameter pointers
+        to every call and never needs the packed copy (upload=False)."""
         lib = _lib.load()
         cfg = self._lib_config()
         cfg_key = tuple(getattr(cfg, f) for f, _ in _lib.LGConfig._fields_)
@@ -402,6 +425,8 @@ class LightGlue(nn.Module):
             self._handle, self._handle_device, self._cfg_key = h, device, cfg_key
             self._weights_key = None
             self._gen += 1
+        if not upload:
+            return lib
         key = self._weights_signature()
         if key != self._weights_key:
             sd = self.state_dict(keep_vars=True)
@@ -529,7 +554,7 @@ class LightGlue(nn.Module):
         return self._schema_list
 
     def _schema_params(self, device):
-        self._ensure_handle(device)
+        self._ensure_handle(device, upload=False)
         named = dict(self.named_parameters())
         params = []
         for nm in self._schema_names():
@@ -729,13 +754,18 @@ class LightGlue(nn.Module):
         lconf = self.conf.loss
         if lconf.get("fn", "nll") != "nll":
             raise NotImplementedError(f"loss fn {lconf.fn!r} (the reference defines only 'nll')")
+        from .superglue import nll_inputs, nll_weights
+
         bal = float(lconf.nll_balancing)
         rd0, rd1 = pred["ref_descriptors0"], pred["ref_descriptors1"]
         N = rd0.shape[1]
         params = self._schema_params(rd0.device)
+        b, m, n = rd0.shape[0], rd0.shape[2], rd1.shape[2]
+        # the ground truth's loss weights (losses.py:62-73) once, as the reference (gt_weights, :633)
+        gt = (data, nll_weights(rd0.new_empty((b, m + 1, n + 1)), data), nll_inputs(data, rd0.device))
 
         def head(i, tokens):
-            return _HeadNLL.apply(self, i, data, bal, tokens, rd0[:, i], rd1[:, i], *params)
+            return _HeadNLL.apply(self, i, gt, bal, tokens, rd0[:, i], rd1[:, i], *params)
 
         nll, nll_pos, nll_neg, num_pos, num_neg, _, _, _ = head(-1, False)
         losses = {"total": nll, "last": nll.clone().detach(), "assignment_nll": nll, "nll_pos": nll_pos,
@@ -746,14 +776,17 @@ class LightGlue(nn.Module):
         la_final = pred["log_assignment"].detach()
         losses["row_norm"] = la_final.exp()[:, :-1].sum(2).mean(1)
         bce = torch.nn.functional.binary_cross_entropy_with_logits
+        if N > 1:  # the final head's argmaxes, shared by every layer's TokenConfidence.loss
+            fin0 = la_final[:, :-1, :].max(-1).indices
+            fin1 = la_final[:, :, :-1].max(-2).indices
         for i in range(N - 1):
             nll_i, _, _, _, _, la_i, lg0, lg1 = head(i, True)
             weight = lconf.gamma ** (N - i - 1) if lconf.gamma > 0.0 else i + 1
             sum_weights += weight
             losses["total"] = losses["total"] + nll_i * weight
             # TokenConfidence.loss (:108-122): does layer i already pick the final argmax?
-            hit0 = (la_final[:, :-1, :].max(-1).indices == la_i[:, :-1, :].max(-1).indices).float()
-            hit1 = (la_final[:, :, :-1].max(-2).indices == la_i[:, :, :-1].max(-2).indices).float()
+            hit0 = (fin0 == la_i[:, :-1, :].max(-1).indices).float()
+            hit1 = (fin1 == la_i[:, :, :-1].max(-2).indices).float()
             tok = (bce(lg0, hit0, reduction="none").mean(-1) + bce(lg1, hit1, reduction="none").mean(-1)) / 2.0
             losses["confidence"] = losses.get("confidence", 0.0) + tok / (N - 1)
         losses["total"] = losses["total"] / sum_weights

@@ -245,14 +245,20 @@ class SuperGlue(nn.Module):
         raise NotImplementedError
 
 
-def _nll(la, data, mode, balancing):
+def nll_inputs(data, device):
+    """The ground truth in the layouts sg_nll_loss reads (uint8 assignment, int64 matches); convert
+    once per loss() and pass ``prepared=`` to every head's _nll."""
+    return (data["gt_assignment"].to(device=device).bool().to(torch.uint8).contiguous(),
+            data["gt_matches0"].to(device=device, dtype=torch.int64).contiguous(),
+            data["gt_matches1"].to(device=device, dtype=torch.int64).contiguous())
+
+
+def _nll(la, data, mode, balancing, prepared=None):
     if not la.is_cuda:
         raise RuntimeError("lightglue_amd NLL loss runs on a HIP device; inputs are on the CPU")
     device = la.device
     B, M1, N1 = la.shape
-    gta = data["gt_assignment"].to(device=device).bool().to(torch.uint8).contiguous()
-    g0 = data["gt_matches0"].to(device=device, dtype=torch.int64).contiguous()
-    g1 = data["gt_matches1"].to(device=device, dtype=torch.int64).contiguous()
+    gta, g0, g1 = prepared if prepared is not None else nll_inputs(data, device)
     la = la.float().contiguous()
     out = torch.empty((5, B), device=device)
     lib = _lib.load()

@@ -250,6 +250,13 @@ int lg_train_backward(lg_handle_t* h, const float* const* params, const lg_input
  * Writes the grads of log_assignment.<layer>.* (and token_confidence.<layer>.* when grad_token* is
  * given) and grad_desc0/1 (nullable).  Scratch: lg_head_scratch_bytes.  Asynchronous. */
 int lg_head_scratch_bytes(const lg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+/* The same head's forward on raw parameters, fp32 (f32 matrix cores): log_assignment [B,M+1,N+1],
+ * similarity [B,M,N] (nullable), token_logits0/1 (nullable) -- lg_assignment_head's outputs without
+ * the handle's packed weights (the training path never uploads them).  Scratch:
+ * lg_head_scratch_bytes.  Asynchronous. */
+int lg_head_forward(lg_handle_t* h, const float* const* params, int32_t layer, const float* desc0, const float* desc1,
+                    int32_t B, int32_t M, int32_t N, float* log_assignment, float* similarity, float* token_logits0,
+                    float* token_logits1, void* scratch, size_t scratch_bytes, void* stream);
 int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, const float* desc0, const float* desc1,
                      int32_t B, int32_t M, int32_t N, const float* la_grad, const float* s_in, const float* s_dust,
                      const float* grad_similarity, const float* grad_token0, const float* grad_token1,

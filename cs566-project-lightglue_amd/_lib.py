@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LIGHTGLUE_MI355X_LIB", os.path.join(_HERE, "liblightglue_mi355x.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 LG_OK, LG_E_INVALID, LG_E_HIP, LG_E_WEIGHTS, LG_E_WORKSPACE, LG_E_INTERNAL = 0, -1, -2, -3, -4, -5
 
@@ -65,6 +65,12 @@ EXPORTED_SYMBOLS = [
     "sg_workspace_bytes",
     "sg_forward",
     "sg_nll_loss",
+    # SuperGlue training
+    "sg_train_saved_bytes",
+    "sg_train_scratch_bytes",
+    "sg_train_forward",
+    "sg_train_backward",
+    "sg_nll_backward",
 ]
 KERNEL_IDS = {"attention": 0, "gemm": 1, "assign": 2}
 # lg_config_t.precision (include/lightglue_mi355x.h): "auto" = fp16x3 (device-side range scaling)
@@ -313,6 +319,11 @@ def load():
         "sg_workspace_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
         "sg_forward": (ctypes.c_int, [_P, ctypes.POINTER(SGInputs), ctypes.POINTER(SGOutputs), _P, sz, _P]),
         "sg_nll_loss": (ctypes.c_int, [_P, i32, i32, i32, _P, _P, _P, i32, ctypes.c_float, _P, _P]),
+        "sg_train_saved_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
+        "sg_train_scratch_bytes": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(sz)]),
+        "sg_train_forward": (ctypes.c_int, [_P, _P, ctypes.POINTER(SGInputs), ctypes.POINTER(SGOutputs), _P, sz, _P]),
+        "sg_train_backward": (ctypes.c_int, [_P, _P, ctypes.POINTER(SGInputs), _P, sz, _P, _P, _P, _P, _P, _P, sz, _P]),
+        "sg_nll_backward": (ctypes.c_int, [_P, _P, _P, _P, i32, i32, i32, _P, _P, _P, i32, ctypes.c_float, _P, _P]),
         "lg_profile_read": (
             ctypes.c_int,
             [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),

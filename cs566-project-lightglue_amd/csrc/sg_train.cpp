@@ -1,0 +1,507 @@
+// C-ABI of the SuperGlue training path (include/superglue_mi355x.h, "Training"): the training-mode
+// forward that keeps its activations, its backward, and the NLL loss gradient -- what torch
+// autograd computes for the reference (gluefactory/train.py:436-450 over
+// gluefactory_nonfree/superglue.py:253-339).  Kernels: train.hip (GEMM, attention) and
+// sg_train.hip (batch-statistics BatchNorm, keypoint-encoder input, Sinkhorn and its backward).
+//
+// Row space: R = B (M + N) rows -- image-0 rows (pair-major, R0 = B M of them) then image-1 rows;
+// every activation is row-major fp32.  The projections' output channels are gathered head-major
+// (head h at columns 64h.., channel d*4 + h of the reference's view(b, dim, h, n), :121-127) so the
+// training attention kernels run unchanged; merge's input columns are gathered the same way and
+// gradients are scattered back to the reference layouts.
+//
+// BatchNorm: every AttentionalPropagation call normalises one image set with its own batch
+// statistics (:135-139 is called per image, :160-170).  Running statistics follow the
+// reference's training step: the keypoint encoder's once per image set in the forward; the GNN's
+// once per image set in the forward and once more in the backward, because the reference
+// recomputes each GNN layer under torch.utils.checkpoint (:151-155) and the recomputation
+// updates them again (measured on the reference: num_batches_tracked +4 per step).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/lightglue_mi355x.h"
+#include "../../include/superglue_mi355x.h"
+#include "kernels.h"
+#include "train.h"
+
+namespace lg {
+int api_fail(int code, const char* msg);
+const sg_config_t* sg_handle_config(const sg_handle* h);
+int sg_handle_device(const sg_handle* h);
+int sg_handle_weight_index(const sg_handle* h, const std::string& name);
+}  // namespace lg
+
+namespace {
+
+using namespace lg;
+
+int fail(int code, const std::string& msg) { return api_fail(code, msg.c_str()); }
+
+#define ST_HIP(expr)                                                                                \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    if (_e != hipSuccess) return fail(LG_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+constexpr int D = 256, H = 4;
+constexpr float kMomentum = 0.1f;  // nn.BatchNorm1d default
+
+struct Dims {
+  int B, M, N, R, R0, L, T, cin;
+  std::vector<int> ch;  // keypoint encoder channels: cin, widths..., 256
+  std::vector<int> type;
+};
+
+Dims dims_of(const sg_handle_t* h, int B, int M, int N) {
+  const sg_config_t& c = *sg_handle_config(h);
+  Dims d;
+  d.B = B;
+  d.M = M;
+  d.N = N;
+  d.R0 = B * M;
+  d.R = B * (M + N);
+  d.L = c.n_layers;
+  d.T = c.sinkhorn_iterations;
+  d.cin = c.use_scores ? 3 : 2;
+  d.ch = {d.cin};
+  for (int i = 0; i < c.n_kenc; ++i) d.ch.push_back(c.keypoint_encoder[i]);
+  d.ch.push_back(D);
+  d.type.assign(c.layer_types, c.layer_types + c.n_layers);
+  return d;
+}
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  float* f(size_t n) {
+    char* p = base ? base + off : nullptr;
+    off += (n * sizeof(float) + 255) & ~size_t(255);
+    return reinterpret_cast<float*>(p);
+  }
+};
+
+struct Enc {
+  float *A, *G, *ST;  // pre-BN conv output, post-ReLU activation, [2][3][C] statistics
+};
+struct Lay {
+  float *WQKV, *BQKV, *WM, *QKV, *LSE, *O, *CAT, *H1, *ST, *G, *Y;
+};
+struct Saved {
+  float *KIN, *X0, *MD, *COST, *CC, *U, *V, *FWS, *PART;
+  std::vector<Enc> enc;
+  std::vector<Lay> lay;
+  size_t bytes;
+};
+
+Saved carve_saved(char* base, const Dims& d) {
+  Carver c{base};
+  Saved s;
+  const size_t R = d.R;
+  const int nk = (int)d.ch.size() - 1;
+  s.KIN = c.f(R * d.cin);
+  for (int i = 1; i < nk; ++i) {
+    Enc e;
+    e.A = c.f(R * d.ch[i]);
+    e.G = c.f(R * d.ch[i]);
+    e.ST = c.f(6 * (size_t)d.ch[i]);
+    s.enc.push_back(e);
+  }
+  s.X0 = c.f(R * D);
+  const size_t nl = (size_t)d.B * H * (d.M + d.N);
+  for (int l = 0; l < d.L; ++l) {
+    Lay y;
+    y.WQKV = c.f(3 * D * D);
+    y.BQKV = c.f(3 * D);
+    y.WM = c.f(D * D);
+    y.QKV = c.f(R * 3 * D);
+    y.LSE = c.f(nl);
+    y.O = c.f(R * D);
+    y.CAT = c.f(R * 2 * D);
+    y.H1 = c.f(R * 2 * D);
+    y.ST = c.f(6 * 2 * D);
+    y.G = c.f(R * 2 * D);
+    y.Y = c.f(R * D);
+    s.lay.push_back(y);
+  }
+  s.MD = c.f(R * D);
+  const size_t M1 = d.M + 1, N1 = d.N + 1;
+  s.COST = c.f((size_t)d.B * d.M * d.N);
+  s.CC = c.f((size_t)d.B * M1 * N1);
+  s.U = c.f((size_t)std::max(d.T, 1) * d.B * M1);
+  s.V = c.f((size_t)(d.T + 1) * d.B * N1);
+  s.FWS = c.f(filter_workspace_floats(d.B, d.M, d.N) + 64);
+  const int rmax = std::max(d.R0, d.R - d.R0);
+  size_t p = bn_part_floats(rmax, 2 * D);
+  for (size_t i = 1; i + 1 < d.ch.size(); ++i) p = std::max(p, bn_part_floats(rmax, d.ch[i]));
+  s.PART = c.f(p + 64);
+  s.bytes = c.off;
+  return s;
+}
+
+struct Scratch {
+  float *GX, *GX2, *GG, *GH, *GC, *GO, *GQKV, *DELTA, *GCOST, *GMD, *GW, *GB, *SK, *WS, *PART;
+  size_t ws_floats, bytes;
+};
+
+Scratch carve_scratch(char* base, const Dims& d) {
+  Carver c{base};
+  Scratch s;
+  const size_t R = d.R;
+  s.GX = c.f(R * D);
+  s.GX2 = c.f(R * D);
+  s.GG = c.f(R * 2 * D);
+  s.GH = c.f(R * 2 * D);
+  s.GC = c.f(R * 2 * D);
+  s.GO = c.f(R * D);
+  s.GQKV = c.f(R * 3 * D);
+  s.DELTA = c.f((size_t)d.B * H * (d.M + d.N));
+  s.GCOST = c.f((size_t)d.B * d.M * d.N);
+  s.GMD = c.f(R * D);
+  s.GW = c.f(3 * D * D);
+  s.GB = c.f(3 * D);
+  s.SK = c.f(sk_train_scratch_floats(d.B, d.M, d.N));
+  size_t w = 0;
+  auto upd = [&](int M, int N, int K, int batch) { w = std::max(w, tgemm_ws_floats(M, N, K, batch)); };
+  for (size_t i = 1; i < d.ch.size(); ++i) upd(d.ch[i], d.ch[i - 1], d.R, 1);
+  upd(3 * D, D, d.R, 1);
+  upd(D, D, d.R, 1);
+  upd(2 * D, 2 * D, d.R, 1);
+  upd(D, 2 * D, d.R, 1);
+  upd(d.M, D, d.N, d.B);
+  upd(d.N, D, d.M, d.B);
+  s.ws_floats = w;
+  s.WS = c.f(w + 64);
+  size_t p = std::max(colsum_part_floats(d.R, 3 * D), bn_part_floats(std::max(d.R0, d.R - d.R0), 2 * D));
+  for (size_t i = 1; i + 1 < d.ch.size(); ++i) p = std::max(p, bn_part_floats(std::max(d.R0, d.R - d.R0), d.ch[i]));
+  s.PART = c.f(p + 64);
+  s.bytes = c.off;
+  return s;
+}
+
+struct Params {
+  const sg_handle_t* h;
+  float* const* p;
+  float* const* g;
+  float* w(const std::string& n) const { return p[sg_handle_weight_index(h, n)]; }
+  float* gr(const std::string& n) const { return g ? g[sg_handle_weight_index(h, n)] : nullptr; }
+};
+
+struct Ctx {
+  hipStream_t st;
+  float* ws;
+  size_t ws_floats;
+  float* part;
+};
+
+// y[rows,N] = alpha (x[rows,K] W[N,K]^T + b) + beta y
+hipError_t linear(const Ctx& c, const float* x, long long ldx, int rows, int K, const float* W, const float* b, int N,
+                  float* y, long long ldy, float beta = 0.f) {
+  TGemm g{x, W, y, ldx, K, ldy, 0, 0, 0, rows, N, K, 1, 1.f, beta, b};
+  return tgemm(g, false, true, c.ws, c.ws_floats, c.st);
+}
+// dx[rows,K] (+)= dy[rows,N] W[N,K]
+hipError_t linear_dgrad(const Ctx& c, const float* dy, long long lddy, int rows, int N, const float* W, int K, float* dx,
+                        long long lddx, float beta = 0.f) {
+  TGemm g{dy, W, dx, lddy, K, lddx, 0, 0, 0, rows, K, N, 1, 1.f, beta, nullptr};
+  return tgemm(g, false, false, c.ws, c.ws_floats, c.st);
+}
+// dW[N,K] = dy^T x; db = colsum(dy)
+hipError_t linear_wgrad(const Ctx& c, const float* dy, long long lddy, const float* x, long long ldx, int rows, int N, int K,
+                        float* dW, float* db) {
+  if (dW) {
+    TGemm g{dy, x, dW, lddy, ldx, K, 0, 0, 0, N, K, rows, 1, 1.f, 0.f, nullptr};
+    hipError_t e = tgemm(g, true, false, c.ws, c.ws_floats, c.st);
+    if (e != hipSuccess) return e;
+  }
+  if (db) return colsum(dy, lddy, rows, N, nullptr, c.part, db, c.st);
+  return hipSuccess;
+}
+
+TAttn attn_args(const float* QKV, size_t qrow, size_t krow, float* O, float* lse, int B, int Nq, int Nk) {
+  TAttn a{};
+  a.Q = QKV + qrow * 3 * D;
+  a.K = QKV + krow * 3 * D + D;
+  a.V = QKV + krow * 3 * D + 2 * D;
+  a.O = O + qrow * D;
+  a.lse = lse;
+  a.ldq = a.ldk = a.ldv = 3 * D;
+  a.ldo = D;
+  a.B = B;
+  a.H = H;
+  a.Nq = Nq;
+  a.Nk = Nk;
+  a.scale = 0.125f;  // 1 / sqrt(dim), dim = 64 (:107-111)
+  return a;
+}
+
+std::string conv_name(const std::string& p, int idx) { return p + "." + std::to_string(idx); }
+
+int check_shape(const sg_handle_t* h, int B, int M, int N) {
+  if (!h) return fail(LG_E_INVALID, "null handle");
+  if (B <= 0) return fail(LG_E_INVALID, "batch must be >= 1");
+  if (M <= 0 || N <= 0) return fail(LG_E_INVALID, "empty keypoint set");
+  if ((long long)B * M < 2 || (long long)B * N < 2)
+    return fail(LG_E_INVALID, "Expected more than 1 value per channel when training (BatchNorm1d batch statistics)");
+  if ((long long)B * (M + N) > (1ll << 30) / 1024) return fail(LG_E_INVALID, "row count too large");
+  return LG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sg_train_saved_bytes(const sg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (int e = check_shape(h, B, M, N)) return e;
+  if (!bytes) return fail(LG_E_INVALID, "null argument");
+  *bytes = carve_saved(nullptr, dims_of(h, B, M, N)).bytes;
+  return LG_OK;
+}
+
+int sg_train_scratch_bytes(const sg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes) {
+  if (int e = check_shape(h, B, M, N)) return e;
+  if (!bytes) return fail(LG_E_INVALID, "null argument");
+  *bytes = carve_scratch(nullptr, dims_of(h, B, M, N)).bytes;
+  return LG_OK;
+}
+
+int sg_train_forward(sg_handle_t* h, float* const* params, const sg_inputs_t* in, sg_outputs_t* out, void* saved,
+                     size_t saved_bytes, void* stream) {
+  if (!params || !in || !out || !saved || !out->log_assignment) return fail(LG_E_INVALID, "null argument");
+  if (int e = check_shape(h, in->B, in->M, in->N)) return e;
+  if (!in->keypoints0 || !in->keypoints1 || !in->descriptors0 || !in->descriptors1)
+    return fail(LG_E_INVALID, "null input tensor");
+  const Dims d = dims_of(h, in->B, in->M, in->N);
+  if (d.cin == 3 && (!in->scores0 || !in->scores1)) return fail(LG_E_INVALID, "use_scores needs scores0/1");
+  Saved s = carve_saved((char*)saved, d);
+  if (saved_bytes < s.bytes) return fail(LG_E_WORKSPACE, "saved buffer too small: need " + std::to_string(s.bytes));
+  ST_HIP(hipSetDevice(sg_handle_device(h)));
+  // the forward's GEMMs run without split-k (no workspace)
+  const Ctx c{(hipStream_t)stream, nullptr, 0, s.PART};
+  const Params P{h, params, nullptr};
+  const int B = d.B, M = d.M, N = d.N, R = d.R, R0 = d.R0;
+  const size_t o1 = (size_t)R0;
+  const int rows_of[2] = {R0, R - R0};
+  const size_t off_of[2] = {0, o1};
+  // keypoint encoder (:89-104,274-275): [x, y(, score)] -> MLP with batch-statistics BatchNorm
+  ST_HIP(kenc_input(in->keypoints0, in->scores0, in->image_size0, (float)in->image_w0, (float)in->image_h0, B, M, d.cin,
+                    s.KIN, c.st));
+  ST_HIP(kenc_input(in->keypoints1, in->scores1, in->image_size1, (float)in->image_w1, (float)in->image_h1, B, N, d.cin,
+                    s.KIN + o1 * d.cin, c.st));
+  ST_HIP(hipMemcpyAsync(s.X0, in->descriptors0, o1 * D * 4, hipMemcpyDeviceToDevice, c.st));
+  ST_HIP(hipMemcpyAsync(s.X0 + o1 * D, in->descriptors1, (size_t)(R - R0) * D * 4, hipMemcpyDeviceToDevice, c.st));
+  const int nk = (int)d.ch.size() - 1;
+  const float* prev = s.KIN;
+  for (int i = 1; i <= nk; ++i) {
+    const std::string cv = conv_name("kenc.encoder", 3 * (i - 1));
+    const int Ci = d.ch[i], Cp = d.ch[i - 1];
+    if (i == nk) {  // desc + kenc(...) (:274-275)
+      ST_HIP(linear(c, prev, Cp, R, Cp, P.w(cv + ".weight"), P.w(cv + ".bias"), D, s.X0, D, 1.f));
+      break;
+    }
+    const Enc& e = s.enc[i - 1];
+    ST_HIP(linear(c, prev, Cp, R, Cp, P.w(cv + ".weight"), P.w(cv + ".bias"), Ci, e.A, Ci));
+    const std::string bn = conv_name("kenc.encoder", 3 * (i - 1) + 1);
+    for (int set = 0; set < 2; ++set) {
+      ST_HIP(bn_train_fwd(e.A + off_of[set] * Ci, Ci, rows_of[set], Ci, P.w(bn + ".weight"), P.w(bn + ".bias"),
+                          e.G + off_of[set] * Ci, Ci, e.ST + set * 3 * Ci, c.part, c.st));
+      ST_HIP(bn_running_update(P.w(bn + ".running_mean"), P.w(bn + ".running_var"), e.ST + set * 3 * Ci, Ci, kMomentum, c.st));
+    }
+    prev = e.G;
+  }
+  // AttentionalGNN (:142-170)
+  const size_t lse1 = (size_t)B * H * M;
+  for (int l = 0; l < d.L; ++l) {
+    const std::string p = "gnn.layers." + std::to_string(l);
+    const Lay& y = s.lay[l];
+    const float* X = l == 0 ? s.X0 : s.lay[l - 1].Y;
+    for (int t = 0; t < 3; ++t) {
+      const std::string pj = p + ".attn.proj." + std::to_string(t);
+      ST_HIP(head_gather(P.w(pj + ".weight"), D, D, false, false, y.WQKV + (size_t)t * D * D, c.st));
+      ST_HIP(head_gather(P.w(pj + ".bias"), D, 1, false, false, y.BQKV + t * D, c.st));
+    }
+    ST_HIP(head_gather(P.w(p + ".attn.merge.weight"), D, D, true, false, y.WM, c.st));
+    // q = proj0(x), k / v = proj1 / proj2(source) (:121-124): one GEMM over every row; the
+    // attention pairs image-0 queries with image-0 (self) or image-1 (cross) keys and back
+    ST_HIP(linear(c, X, D, R, D, y.WQKV, y.BQKV, 3 * D, y.QKV, 3 * D));
+    const bool cross = d.type[l] == 1;
+    ST_HIP(tattn_forward(attn_args(y.QKV, 0, cross ? o1 : 0, y.O, y.LSE, B, M, cross ? N : M), c.st));
+    ST_HIP(tattn_forward(attn_args(y.QKV, o1, cross ? 0 : o1, y.O, y.LSE + lse1, B, N, cross ? M : N), c.st));
+    // mlp(cat([x, merge(message)])) (:125-127,135-139) with batch-statistics BatchNorm per image set
+    ST_HIP(hipMemcpy2DAsync(y.CAT, 2 * D * 4, X, D * 4, D * 4, R, hipMemcpyDeviceToDevice, c.st));
+    ST_HIP(linear(c, y.O, D, R, D, y.WM, P.w(p + ".attn.merge.bias"), D, y.CAT + D, 2 * D));
+    ST_HIP(linear(c, y.CAT, 2 * D, R, 2 * D, P.w(p + ".mlp.0.weight"), P.w(p + ".mlp.0.bias"), 2 * D, y.H1, 2 * D));
+    for (int set = 0; set < 2; ++set) {
+      ST_HIP(bn_train_fwd(y.H1 + off_of[set] * 2 * D, 2 * D, rows_of[set], 2 * D, P.w(p + ".mlp.1.weight"),
+                          P.w(p + ".mlp.1.bias"), y.G + off_of[set] * 2 * D, 2 * D, y.ST + set * 6 * D, c.part, c.st));
+      ST_HIP(bn_running_update(P.w(p + ".mlp.1.running_mean"), P.w(p + ".mlp.1.running_var"), y.ST + set * 6 * D, 2 * D,
+                               kMomentum, c.st));
+    }
+    // desc + delta (:166)
+    ST_HIP(hipMemcpyAsync(y.Y, X, (size_t)R * D * 4, hipMemcpyDeviceToDevice, c.st));
+    ST_HIP(linear(c, y.G, 2 * D, R, 2 * D, P.w(p + ".mlp.3.weight"), P.w(p + ".mlp.3.bias"), D, y.Y, D, 1.f));
+  }
+  const float* XL = d.L ? s.lay[d.L - 1].Y : s.X0;
+  if (out->descriptors0) ST_HIP(hipMemcpyAsync(out->descriptors0, XL, o1 * D * 4, hipMemcpyDeviceToDevice, c.st));
+  if (out->descriptors1)
+    ST_HIP(hipMemcpyAsync(out->descriptors1, XL + o1 * D, (size_t)(R - R0) * D * 4, hipMemcpyDeviceToDevice, c.st));
+  // md = final_proj(desc); cost = md0^T md1 / sqrt(256) (:279-282)
+  ST_HIP(linear(c, XL, D, R, D, P.w("final_proj.weight"), P.w("final_proj.bias"), D, s.MD, D));
+  {
+    TGemm g{s.MD, s.MD + o1 * D, s.COST, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B,
+            1.f / 16.f, 0.f, nullptr};
+    ST_HIP(tgemm(g, false, true, nullptr, 0, c.st));
+  }
+  if (out->sinkhorn_cost)
+    ST_HIP(hipMemcpyAsync(out->sinkhorn_cost, s.COST, (size_t)B * M * N * 4, hipMemcpyDeviceToDevice, c.st));
+  ST_HIP(sk_train_forward(s.COST, P.w("bin_score"), B, M, N, d.T, s.CC, s.U, s.V, out->log_assignment, c.st));
+  if (out->matches0 && out->matches1 && out->matching_scores0 && out->matching_scores1)
+    ST_HIP(filter_from_scores(out->log_assignment, B, M, N, sg_handle_config(h)->filter_threshold, s.FWS, out->matches0,
+                              out->matches1, out->matching_scores0, out->matching_scores1, c.st));
+  return LG_OK;
+}
+
+int sg_train_backward(sg_handle_t* h, float* const* params, const sg_inputs_t* in, const void* saved, size_t saved_bytes,
+                      const float* grad_log_assignment, const float* grad_cost, float* const* grads, float* grad_desc0,
+                      float* grad_desc1, void* scratch, size_t scratch_bytes, void* stream) {
+  if (!params || !in || !saved || !scratch) return fail(LG_E_INVALID, "null argument");
+  if (int e = check_shape(h, in->B, in->M, in->N)) return e;
+  const Dims d = dims_of(h, in->B, in->M, in->N);
+  Saved s = carve_saved((char*)saved, d);
+  if (saved_bytes < s.bytes) return fail(LG_E_WORKSPACE, "saved buffer too small");
+  Scratch w = carve_scratch((char*)scratch, d);
+  if (scratch_bytes < w.bytes) return fail(LG_E_WORKSPACE, "scratch too small: need " + std::to_string(w.bytes));
+  ST_HIP(hipSetDevice(sg_handle_device(h)));
+  const Ctx c{(hipStream_t)stream, w.WS, w.ws_floats, w.PART};
+  const Params P{h, params, grads};
+  const int B = d.B, M = d.M, N = d.N, R = d.R, R0 = d.R0;
+  const size_t o1 = (size_t)R0;
+  const int rows_of[2] = {R0, R - R0};
+  const size_t off_of[2] = {0, o1};
+  // Sinkhorn (:174-201) -> d/d cost, d/d bin_score
+  if (grad_log_assignment) {
+    ST_HIP(sk_train_backward(s.CC, s.U, s.V, grad_log_assignment, grad_cost, B, M, N, d.T, w.GCOST, P.gr("bin_score"), w.SK,
+                             c.st));
+  } else {
+    if (grad_cost) ST_HIP(hipMemcpyAsync(w.GCOST, grad_cost, (size_t)B * M * N * 4, hipMemcpyDeviceToDevice, c.st));
+    else ST_HIP(hipMemsetAsync(w.GCOST, 0, (size_t)B * M * N * 4, c.st));
+    if (float* g = P.gr("bin_score")) ST_HIP(hipMemsetAsync(g, 0, 4, c.st));
+  }
+  // cost = md0^T md1 / 16: gmd0 = gcost md1 / 16, gmd1 = gcost^T md0 / 16
+  {
+    TGemm g{w.GCOST, s.MD + o1 * D, w.GMD, N, D, D, (long long)M * N, (long long)N * D, (long long)M * D, M, D, N, B,
+            1.f / 16.f, 0.f, nullptr};
+    ST_HIP(tgemm(g, false, false, c.ws, c.ws_floats, c.st));
+  }
+  {
+    TGemm g{w.GCOST, s.MD, w.GMD + o1 * D, N, D, D, (long long)M * N, (long long)M * D, (long long)N * D, N, D, M, B,
+            1.f / 16.f, 0.f, nullptr};
+    ST_HIP(tgemm(g, true, false, c.ws, c.ws_floats, c.st));
+  }
+  const float* XL = d.L ? s.lay[d.L - 1].Y : s.X0;
+  ST_HIP(linear_wgrad(c, w.GMD, D, XL, D, R, D, D, P.gr("final_proj.weight"), P.gr("final_proj.bias")));
+  ST_HIP(linear_dgrad(c, w.GMD, D, R, D, P.w("final_proj.weight"), D, w.GX, D));
+  const size_t lse1 = (size_t)B * H * M;
+  float* GX = w.GX;
+  float* GX2 = w.GX2;
+  for (int l = d.L - 1; l >= 0; --l) {
+    const std::string p = "gnn.layers." + std::to_string(l);
+    const Lay& y = s.lay[l];
+    const float* X = l == 0 ? s.X0 : s.lay[l - 1].Y;
+    // delta = mlp.3(G): GX -> GG (d/d G)
+    ST_HIP(linear_wgrad(c, GX, D, y.G, 2 * D, R, D, 2 * D, P.gr(p + ".mlp.3.weight"), P.gr(p + ".mlp.3.bias")));
+    ST_HIP(linear_dgrad(c, GX, D, R, D, P.w(p + ".mlp.3.weight"), 2 * D, w.GG, 2 * D));
+    for (int set = 0; set < 2; ++set) {
+      const size_t o = off_of[set] * 2 * D;
+      ST_HIP(bn_train_bwd(y.H1 + o, 2 * D, w.GG + o, 2 * D, rows_of[set], 2 * D, y.ST + set * 6 * D, P.w(p + ".mlp.1.weight"),
+                          P.w(p + ".mlp.1.bias"), w.GH + o, 2 * D, P.gr(p + ".mlp.1.weight"), P.gr(p + ".mlp.1.bias"), set,
+                          c.part, c.st));
+    }
+    // the reference's checkpoint recomputation updates the running statistics again (:151-155)
+    for (int set = 0; set < 2; ++set)
+      ST_HIP(bn_running_update(P.w(p + ".mlp.1.running_mean"), P.w(p + ".mlp.1.running_var"), y.ST + set * 6 * D, 2 * D,
+                               kMomentum, c.st));
+    ST_HIP(linear_wgrad(c, w.GH, 2 * D, y.CAT, 2 * D, R, 2 * D, 2 * D, P.gr(p + ".mlp.0.weight"), P.gr(p + ".mlp.0.bias")));
+    ST_HIP(linear_dgrad(c, w.GH, 2 * D, R, 2 * D, P.w(p + ".mlp.0.weight"), 2 * D, w.GC, 2 * D));
+    ST_HIP(add_rows256(GX, D, w.GC, 2 * D, GX2, D, R, c.st));  // residual + the mlp's x input
+    // merge (head-major columns): d/d merge.weight gathered back to the reference's columns
+    const float* gmsg = w.GC + D;
+    ST_HIP(linear_wgrad(c, gmsg, 2 * D, y.O, D, R, D, D, P.gr(p + ".attn.merge.weight") ? w.GW : nullptr,
+                        P.gr(p + ".attn.merge.bias")));
+    if (float* g = P.gr(p + ".attn.merge.weight")) ST_HIP(head_gather(w.GW, D, D, true, true, g, c.st));
+    ST_HIP(linear_dgrad(c, gmsg, 2 * D, R, D, y.WM, D, w.GO, D));
+    // attention backward
+    ST_HIP(attn_delta(y.O, w.GO, D, B, H, M, w.DELTA, c.st));
+    ST_HIP(attn_delta(y.O + o1 * D, w.GO + o1 * D, D, B, H, N, w.DELTA + lse1, c.st));
+    ST_HIP(hipMemsetAsync(w.GQKV, 0, (size_t)R * 3 * D * 4, c.st));
+    const bool cross = d.type[l] == 1;
+    for (int img = 0; img < 2; ++img) {
+      const size_t qrow = img ? o1 : 0, krow = cross ? (img ? 0 : o1) : qrow;
+      const int nq = img ? N : M, nkk = cross ? (img ? M : N) : nq;
+      TAttn a = attn_args(y.QKV, qrow, krow, y.O, y.LSE + (img ? lse1 : 0), B, nq, nkk);
+      a.dO = w.GO + qrow * D;
+      a.delta = w.DELTA + (img ? lse1 : 0);
+      a.dQ = w.GQKV + qrow * 3 * D;
+      a.dK = w.GQKV + krow * 3 * D + D;
+      a.dV = w.GQKV + krow * 3 * D + 2 * D;
+      a.accum_kv = 0;
+      ST_HIP(tattn_backward(a, c.st));
+    }
+    // projections: d/d (head-major) weight and bias, scattered back per projection
+    ST_HIP(linear_wgrad(c, w.GQKV, 3 * D, X, D, R, 3 * D, D, w.GW, w.GB));
+    for (int t = 0; t < 3; ++t) {
+      const std::string pj = p + ".attn.proj." + std::to_string(t);
+      if (float* g = P.gr(pj + ".weight")) ST_HIP(head_gather(w.GW + (size_t)t * D * D, D, D, false, true, g, c.st));
+      if (float* g = P.gr(pj + ".bias")) ST_HIP(head_gather(w.GB + t * D, D, 1, false, true, g, c.st));
+    }
+    ST_HIP(linear_dgrad(c, w.GQKV, 3 * D, R, 3 * D, y.WQKV, D, GX2, D, 1.f));
+    std::swap(GX, GX2);
+  }
+  // GX = d/d (desc + kenc(...)): the descriptors' gradient and the keypoint encoder's
+  if (grad_desc0) ST_HIP(hipMemcpyAsync(grad_desc0, GX, o1 * D * 4, hipMemcpyDeviceToDevice, c.st));
+  if (grad_desc1) ST_HIP(hipMemcpyAsync(grad_desc1, GX + o1 * D, (size_t)(R - R0) * D * 4, hipMemcpyDeviceToDevice, c.st));
+  const int nk = (int)d.ch.size() - 1;
+  const float* dY = GX;  // d/d (conv i output)
+  long long lddy = D;
+  float* bufs[2] = {w.GG, w.GH};
+  int nb = 0;
+  for (int i = nk; i >= 1; --i) {
+    const std::string cv = conv_name("kenc.encoder", 3 * (i - 1));
+    const int Ci = d.ch[i], Cp = d.ch[i - 1];
+    const float* xin = i == 1 ? s.KIN : s.enc[i - 2].G;
+    ST_HIP(linear_wgrad(c, dY, lddy, xin, Cp, R, Ci, Cp, P.gr(cv + ".weight"), P.gr(cv + ".bias")));
+    if (i == 1) break;  // the keypoints take no gradient
+    float* gG = bufs[nb];
+    float* gA = bufs[nb ^ 1];
+    nb ^= 1;
+    ST_HIP(linear_dgrad(c, dY, lddy, R, Ci, P.w(cv + ".weight"), Cp, gG, Cp));
+    const Enc& e = s.enc[i - 2];
+    const std::string bn = conv_name("kenc.encoder", 3 * (i - 2) + 1);
+    for (int set = 0; set < 2; ++set) {
+      const size_t o = off_of[set] * Cp;
+      ST_HIP(bn_train_bwd(e.A + o, Cp, gG + o, Cp, rows_of[set], Cp, e.ST + set * 3 * Cp, P.w(bn + ".weight"),
+                          P.w(bn + ".bias"), gA + o, Cp, P.gr(bn + ".weight"), P.gr(bn + ".bias"), set, c.part, c.st));
+    }
+    dY = gA;
+    lddy = Cp;
+  }
+  return LG_OK;
+}
+
+int sg_nll_backward(const float* stats, const float* grad_nll, const float* grad_nll_pos, const float* grad_nll_neg,
+                    int32_t B, int32_t M, int32_t N, const uint8_t* gt_assignment, const int64_t* gt_matches0,
+                    const int64_t* gt_matches1, int32_t mode, float nll_balancing, float* grad_log_assignment,
+                    void* stream) {
+  if (!stats || !gt_assignment || !gt_matches0 || !gt_matches1 || !grad_log_assignment || B < 0 || M < 0 || N < 0 ||
+      (mode != 0 && mode != 1))
+    return fail(LG_E_INVALID, "bad argument");
+  if (mode == 1 && M != N) return fail(LG_E_INVALID, "NLLLoss needs M == N (losses.py:72)");
+  ST_HIP(sg_nll_grad(gt_assignment, gt_matches0, gt_matches1, stats, grad_nll, grad_nll_pos, grad_nll_neg, B, M, N, mode,
+                     nll_balancing, grad_log_assignment, (hipStream_t)stream));
+  return LG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,516 @@
+// SuperGlue training kernels for gfx950: the batch-statistics BatchNorm + ReLU of the MLPs
+// (reference gluefactory_nonfree/superglue.py:63-72 with nn.BatchNorm1d in training mode), the
+// keypoint-encoder input (:75-86,100-104) and the log-domain Sinkhorn with its backward
+// (:174-201 differentiated by torch autograd in gluefactory/train.py:450).  The GNN's matrix
+// products and attention run on the training GEMM / attention kernels of train.hip.
+//
+// Every reduction is a fixed-order two-pass sum (per-block partials, then one ordered pass), so
+// repeated calls give identical bits.  BatchNorm tensors are row-major [rows][C] over the rows of
+// one image set (the reference's [b, C, n] batch statistics over (b, n)).
+#include <algorithm>
+#include <cmath>
+
+#include "common.h"
+#include "train.h"
+
+namespace lg {
+
+namespace {
+
+constexpr float kBnEps = 1e-5f;  // torch.nn.BatchNorm1d default
+constexpr int BN_RB = 128;        // rows per partial block
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// the forward's normalised value and its activation; the backward recomputes both identically
+__device__ __forceinline__ float bn_xhat(float x, float mu, float rs) { return (x - mu) * rs; }
+__device__ __forceinline__ float bn_y(float xh, float g, float b) { return g * xh + b; }
+
+// Partial column sums over rows [blk*BN_RB, ...): thread t owns columns 4 (t % tpr) .. +3 of row
+// lane t / tpr (tpr = C / 4).  mode 0: sum x; 1: sum (x - mean)^2; 2 (backward, dy' = dY masked by
+// ReLU(y) > 0): sum dy' -> part0, sum dy' xhat -> part1.
+__global__ __launch_bounds__(256) void bn_part_kernel(const float* X, long long ldx, int rows, int C, int mode,
+                                                      const float* mean, const float* rstd, const float* gamma,
+                                                      const float* beta, const float* dY, long long ldy, float* part0,
+                                                      float* part1) {
+  __shared__ float s0[256 * 4], s1[256 * 4];
+  const int tpr = C >> 2, rl = 256 / tpr;
+  const int t = threadIdx.x, c4 = t % tpr, lr = t / tpr;
+  const int r0 = blockIdx.x * BN_RB, r1 = min(rows, r0 + BN_RB);
+  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+  if (lr < rl) {
+    const int c = 4 * c4;
+    f32x4 mu = {0.f, 0.f, 0.f, 0.f}, rs = mu, g = mu, b = mu;
+    if (mode >= 1) mu = ld4(mean + c);
+    if (mode == 2) {
+      rs = ld4(rstd + c);
+      g = ld4(gamma + c);
+      b = ld4(beta + c);
+    }
+    for (int r = r0 + lr; r < r1; r += rl) {
+      const f32x4 x = ld4(X + (long long)r * ldx + c);
+      if (mode == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a0[e] += x[e];
+      } else if (mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = x[e] - mu[e];
+          a0[e] = fmaf(d, d, a0[e]);
+        }
+      } else {
+        const f32x4 dy = ld4(dY + (long long)r * ldy + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = bn_xhat(x[e], mu[e], rs[e]);
+          const float d = bn_y(xh, g[e], b[e]) > 0.f ? dy[e] : 0.f;
+          a0[e] += d;
+          a1[e] = fmaf(d, xh, a1[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    s0[4 * t + e] = a0[e];
+    s1[4 * t + e] = a1[e];
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float v0 = 0.f, v1 = 0.f;
+    for (int l = 0; l < rl; ++l) {  // fixed order over the row lanes
+      const int k = 4 * (l * tpr + (c >> 2)) + (c & 3);
+      v0 += s0[k];
+      v1 += s1[k];
+    }
+    part0[(long long)blockIdx.x * C + c] = v0;
+    if (mode == 2) part1[(long long)blockIdx.x * C + c] = v1;
+  }
+}
+
+// Ordered sum of the partials.  mode 0: mean; 1: rstd = 1 / sqrt(var + eps) and the unbiased
+// variance (running statistics); 2: s0 = sum dy', s1 = sum dy' xhat, dbeta / dgamma (+)= them.
+__global__ __launch_bounds__(256) void bn_final_kernel(const float* part0, const float* part1, int nb, int C, int rows,
+                                                       int mode, float* mean, float* rstd, float* varu, float* s0,
+                                                       float* s1, float* dgamma, float* dbeta, int accum) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int i = 0; i < nb; ++i) {
+    a += part0[(long long)i * C + c];
+    if (mode == 2) b += part1[(long long)i * C + c];
+  }
+  if (mode == 0) {
+    mean[c] = a / (float)rows;
+  } else if (mode == 1) {
+    rstd[c] = 1.f / sqrtf(a / (float)rows + kBnEps);
+    varu[c] = a / (float)(rows - 1);
+  } else {
+    s0[c] = a;
+    s1[c] = b;
+    if (dbeta) dbeta[c] = accum ? dbeta[c] + a : a;
+    if (dgamma) dgamma[c] = accum ? dgamma[c] + b : b;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_fwd_kernel(const float* X, long long ldx, int rows, int C,
+                                                           const float* mean, const float* rstd, const float* gamma,
+                                                           const float* beta, float* Y, long long ldy) {
+  const int tpr = C >> 2;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)rows * tpr) return;
+  const int r = (int)(i / tpr), c = 4 * (int)(i - (long long)r * tpr);
+  const f32x4 x = ld4(X + (long long)r * ldx + c), mu = ld4(mean + c), rs = ld4(rstd + c), g = ld4(gamma + c),
+              b = ld4(beta + c);
+  f32x4 y;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) y[e] = fmaxf(bn_y(bn_xhat(x[e], mu[e], rs[e]), g[e], b[e]), 0.f);
+  *reinterpret_cast<f32x4*>(Y + (long long)r * ldy + c) = y;
+}
+
+// dx = gamma rstd (dy' - s0 / n - xhat s1 / n)
+__global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const float* X, long long ldx, const float* dY, long long ldy,
+                                                           int rows, int C, const float* mean, const float* rstd,
+                                                           const float* gamma, const float* beta, const float* s0,
+                                                           const float* s1, float* dX, long long lddx) {
+  const int tpr = C >> 2;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)rows * tpr) return;
+  const int r = (int)(i / tpr), c = 4 * (int)(i - (long long)r * tpr);
+  const float inv_n = 1.f / (float)rows;
+  const f32x4 x = ld4(X + (long long)r * ldx + c), dy = ld4(dY + (long long)r * ldy + c), mu = ld4(mean + c),
+              rs = ld4(rstd + c), g = ld4(gamma + c), b = ld4(beta + c), a0 = ld4(s0 + c), a1 = ld4(s1 + c);
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float xh = bn_xhat(x[e], mu[e], rs[e]);
+    const float d = bn_y(xh, g[e], b[e]) > 0.f ? dy[e] : 0.f;
+    o[e] = g[e] * rs[e] * (d - a0[e] * inv_n - xh * (a1[e] * inv_n));
+  }
+  *reinterpret_cast<f32x4*>(dX + (long long)r * lddx + c) = o;
+}
+
+// running = (1 - momentum) running + momentum batch (torch.nn.functional.batch_norm, unbiased var)
+__global__ void bn_running_kernel(float* rm, float* rv, const float* mean, const float* varu, int C, float momentum) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  rm[c] = (1.f - momentum) * rm[c] + momentum * mean[c];
+  rv[c] = (1.f - momentum) * rv[c] + momentum * varu[c];
+}
+
+// normalize_keypoints (:75-86) + the encoder input [x, y(, score)] (:100-104), one row per keypoint
+__global__ void kenc_input_kernel(const float* kpts, const float* scores, const float* size, float w, float h, int B,
+                                  int n, int cin, float* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * n) return;
+  const int b = i / n;
+  const float sw = size ? size[2 * b] : w, sh = size ? size[2 * b + 1] : h;
+  const float scale = fmaxf(sw, sh) * 0.7f;
+  out[(long long)i * cin] = (kpts[2 * i] - sw / 2.f) / scale;
+  out[(long long)i * cin + 1] = (kpts[2 * i + 1] - sh / 2.f) / scale;
+  if (cin == 3) out[(long long)i * cin + 2] = scores[i];
+}
+
+// dst row r = src row perm(r), perm(h*64 + d) = d*4 + h (MultiHeadedAttention's view(b, dim, h, n),
+// :121-127, gathered head-major); cols: the same on columns (merge's input channels)
+__global__ void head_gather_kernel(const float* src, int rows, int cols, int by_cols, int inverse, float* dst) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int r = i / cols, c = i - r * cols;
+  auto perm = [](int k) { return (k & 63) * 4 + (k >> 6); };      // head-major -> reference
+  auto iperm = [](int k) { return (k & 3) * 64 + (k >> 2); };     // reference -> head-major
+  int sr = r, sc = c;
+  if (by_cols) sc = inverse ? iperm(c) : perm(c);
+  else sr = inverse ? iperm(r) : perm(r);
+  dst[i] = src[(long long)sr * cols + sc];
+}
+
+// ---------------------------------------------------------------- Sinkhorn (training)
+// couplings [B][M+1][N+1]: the cost with the dustbin score alpha (:185-192)
+__global__ void sk_couplings_kernel(const float* cost, const float* alpha, int B, int M, int N, float* Cc) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long per = (long long)(M + 1) * (N + 1);
+  if (i >= per * B) return;
+  const int b = (int)(i / per);
+  const long long e = i - b * per;
+  const int r = (int)(e / (N + 1)), c = (int)(e - (long long)r * (N + 1));
+  Cc[i] = (r < M && c < N) ? cost[((long long)b * M + r) * N + c] : alpha[0];
+}
+
+// online logsumexp of one lane's stream, then a wave reduction
+__device__ __forceinline__ void lse_push(float x, float& m, float& s) {
+  if (x > m) {
+    s = s * expf(m - x) + 1.f;  // s == 0 while m == -inf
+    m = x;
+  } else {
+    s += expf(x - m);
+  }
+}
+__device__ __forceinline__ float lse_wave(float m, float s) {
+  const float mx = wave_max(m);
+  const float t = mx == -INFINITY ? 0.f : s * expf(m - mx);
+  return mx + logf(wave_sum(t));
+}
+
+// u[b][i] = lmu_i - logsumexp_j (C[b][i][j] + v[b][j])          (:176, one wave per row)
+// mode 1 (backward): gu[b][i] = base[b][i] - sum_j g[b][j] exp(C + u_i + v_j - lnu_j)
+// mode 2: rowsum[b][i] = sum_j C[b][i][j] (the gradient's row sums)
+__global__ __launch_bounds__(256) void sk_row_kernel(const float* Cc, int B, int M1, int N1, const float* u,
+                                                     const float* v, const float* g, const float* base, float norm,
+                                                     float lmu_last, float lnu_last, int mode, float* out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (row >= B * M1) return;
+  const int b = row / M1, i = row - b * M1;
+  const float* c = Cc + (long long)row * N1;
+  const float* vb = v ? v + (long long)b * N1 : nullptr;
+  if (mode == 0) {
+    float m = -INFINITY, s = 0.f;
+    for (int j = l; j < N1; j += 64) lse_push(c[j] + vb[j], m, s);
+    const float lse = lse_wave(m, s);
+    if (l == 0) out[row] = (i < M1 - 1 ? norm : lmu_last) - lse;
+    return;
+  }
+  float acc = 0.f;
+  if (mode == 1) {
+    const float ui = u[row];
+    const float* gb = g + (long long)b * N1;
+    for (int j = l; j < N1; j += 64) acc = fmaf(gb[j], expf(c[j] + ui + vb[j] - (j < N1 - 1 ? norm : lnu_last)), acc);
+  } else {
+    for (int j = l; j < N1; j += 64) acc += c[j];
+  }
+  acc = wave_sum(acc);
+  if (l == 0) out[row] = mode == 1 ? (base ? base[row] : 0.f) - acc : acc;
+}
+
+// v[b][j] = lnu_j - logsumexp_i (C[b][i][j] + u[b][i])          (:177; 64 columns x 4 row groups)
+// mode 1 (backward of step t): with u = u_t, v = v_t, vp = v_{t-1}, gu = d/d u_t, gv = d/d v_t:
+//   pr = exp(C + vp_j + u_i - lmu_i) (u_t's softmax), pc = exp(C + u_i + v_j - lnu_j) (v_t's)
+//   out[j] = d/d v_{t-1} = -sum_i gu_i pr;  gC -= gv_j pc + gu_i pr  (in place)
+// mode 2: colsum[b][j] = sum_i C[b][i][j]
+__global__ __launch_bounds__(256) void sk_col_kernel(const float* Cc, int B, int M1, int N1, const float* u,
+                                                     const float* v, const float* vp, const float* gu, const float* gv,
+                                                     float* gC, float norm, float lmu_last, float lnu_last, int mode,
+                                                     float* out) {
+  __shared__ float sm[4][64], ss[4][64];
+  const int b = blockIdx.y, j = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  const bool ok = j < N1;
+  const long long base = (long long)b * M1 * N1;
+  float m = -INFINITY, s = 0.f;
+  if (ok) {
+    if (mode == 0) {
+      const float* ub = u + (long long)b * M1;
+      for (int i = grp; i < M1; i += 4) lse_push(Cc[base + (long long)i * N1 + j] + ub[i], m, s);
+    } else if (mode == 1) {
+      const float* ub = u + (long long)b * M1;
+      const float* gub = gu + (long long)b * M1;
+      const float vj = v[(long long)b * N1 + j], gvj = gv[(long long)b * N1 + j];
+      const float vpj = vp ? vp[(long long)b * N1 + j] : 0.f;
+      const float lnu = j < N1 - 1 ? norm : lnu_last;
+      float acc = 0.f;
+      for (int i = grp; i < M1; i += 4) {
+        const long long k = base + (long long)i * N1 + j;
+        const float cij = Cc[k], ui = ub[i], gui = gub[i];
+        const float pr = expf(cij + vpj + ui - (i < M1 - 1 ? norm : lmu_last));
+        const float pc = expf(cij + ui + vj - lnu);
+        acc = fmaf(gui, pr, acc);
+        gC[k] -= fmaf(gvj, pc, gui * pr);
+      }
+      s = -acc;
+    } else {
+      for (int i = grp; i < M1; i += 4) s += Cc[base + (long long)i * N1 + j];
+    }
+  }
+  sm[grp][threadIdx.x & 63] = m;
+  ss[grp][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (grp != 0 || !ok) return;
+  const int c = threadIdx.x & 63;
+  if (mode == 0) {
+    float mx = -INFINITY;
+    for (int q = 0; q < 4; ++q) mx = fmaxf(mx, sm[q][c]);
+    float t = 0.f;
+    for (int q = 0; q < 4; ++q) t += mx == -INFINITY ? 0.f : ss[q][c] * expf(sm[q][c] - mx);
+    out[(long long)b * N1 + j] = (j < N1 - 1 ? norm : lnu_last) - (mx + logf(t));
+  } else {
+    out[(long long)b * N1 + j] = ((ss[0][c] + ss[1][c]) + ss[2][c]) + ss[3][c];
+  }
+}
+
+// Z = C + u_i + v_j - norm (:178,200)
+__global__ void sk_out_kernel(const float* Cc, const float* u, const float* v, int B, int M1, int N1, float norm, float* Z) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long per = (long long)M1 * N1;
+  if (i >= per * B) return;
+  const int b = (int)(i / per);
+  const long long e = i - b * per;
+  const int r = (int)(e / N1), c = (int)(e - (long long)r * N1);
+  Z[i] = Cc[i] + u[(long long)b * M1 + r] + v[(long long)b * N1 + c] - norm;
+}
+
+// d/d cost = gC's inner block (+ gext); part[b] = sum of gC over pair b's dustbin entries
+__global__ __launch_bounds__(256) void sk_finish_kernel(const float* gC, const float* gext, int M, int N, float* gcost,
+                                                        float* part) {
+  __shared__ float red[256];
+  const int b = blockIdx.y;
+  const long long M1 = M + 1, N1 = N + 1;
+  const float* g = gC + (long long)b * M1 * N1;
+  if (blockIdx.x > 0) {  // inner block copy
+    const long long per = (long long)M * N;
+    for (long long e = (long long)(blockIdx.x - 1) * 256 + threadIdx.x; e < per; e += (long long)(gridDim.x - 1) * 256) {
+      const long long r = e / N, c = e - r * N;
+      float x = g[r * N1 + c];
+      if (gext) x += gext[(long long)b * per + e];
+      gcost[(long long)b * per + e] = x;
+    }
+    return;
+  }
+  float s = 0.f;
+  for (long long r = threadIdx.x; r < M; r += 256) s += g[r * N1 + N];
+  for (long long c = threadIdx.x; c <= N; c += 256) s += g[M * N1 + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[b] = red[0];
+}
+
+__global__ void sk_alpha_kernel(const float* part, int B, float* galpha) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += part[b];
+  galpha[0] = s;
+}
+
+// d/d log_assignment of SuperGlue.loss (mode 0, superglue.py:309-339) or NLLLoss (mode 1,
+// losses.py:26-73) from d/d (nll, nll_pos, nll_neg) [3][B] (rows nullable) and the forward's
+// out [5][B] (num_matchable, num_unmatchable).  Linear in la: gLA = -(c_in * positive) on the
+// inner block, -(c_dust * negative) on the dustbins (NLLLoss: the column dustbin written at
+// [:, -1, :m], losses.py:72), 0 elsewhere.
+__global__ void sg_nll_grad_kernel(const uint8_t* gta, const int64_t* gt0, const int64_t* gt1, const float* stats,
+                                   const float* g_nll, const float* g_pos, const float* g_neg, int B, int M, int N,
+                                   int mode, float bal, float* gla) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long M1 = M + 1, N1 = N + 1, per = M1 * N1;
+  if (i >= per * B) return;
+  const int b = (int)(i / per);
+  const long long e = i - b * per;
+  const int r = (int)(e / N1), c = (int)(e - (long long)r * N1);
+  const float gn = g_nll ? g_nll[b] : 0.f;
+  const float num_pos = stats[3 * B + b];
+  const float num_neg = mode == 0 ? stats[4 * B + b] : 2.f * stats[4 * B + b];
+  const float c_in = (bal * gn + (g_pos ? g_pos[b] : 0.f)) / num_pos;
+  const float c_dust = ((1.f - bal) * gn + (g_neg ? g_neg[b] : 0.f)) / num_neg;
+  float w = 0.f;
+  if (r < M && c < N) {
+    w = gta[((long long)b * M + r) * N + c] ? c_in : 0.f;
+  } else if (r < M && c == N) {
+    w = gt0[(long long)b * M + r] == -1 ? c_dust : 0.f;
+  } else if (r == M && c < N) {
+    // NLLLoss writes the column dustbins at [:, -1, :m] from gt_matches1 (M == N there)
+    w = gt1[(long long)b * N + c] == -1 ? c_dust : 0.f;
+  }
+  gla[i] = -w;
+}
+
+inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+size_t bn_part_floats(int rows, int C) { return 2 * (size_t)cdiv(rows, BN_RB) * C + 2 * (size_t)C; }
+
+hipError_t bn_train_fwd(const float* X, long long ldx, int rows, int C, const float* gamma, const float* beta,
+                        float* Y, long long ldy, float* stats, float* part, hipStream_t st) {
+  if (C % 4 || C > 1024 || rows < 2) return hipErrorInvalidValue;
+  const int nb = cdiv(rows, BN_RB);
+  float *mean = stats, *rstd = stats + C, *varu = stats + 2 * C;
+  hipLaunchKernelGGL(bn_part_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rows, C, 0, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, 0ll, part, nullptr);
+  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nullptr, nb, C, rows, 0, mean, nullptr,
+                     nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+  hipLaunchKernelGGL(bn_part_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rows, C, 1, mean, nullptr, nullptr, nullptr,
+                     nullptr, 0ll, part, nullptr);
+  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nullptr, nb, C, rows, 1, nullptr, rstd,
+                     varu, nullptr, nullptr, nullptr, nullptr, 0);
+  hipLaunchKernelGGL(bn_apply_fwd_kernel, dim3(cdiv((long long)rows * (C / 4), 256)), dim3(256), 0, st, X, ldx, rows, C,
+                     mean, rstd, gamma, beta, Y, ldy);
+  return hipGetLastError();
+}
+
+hipError_t bn_train_bwd(const float* X, long long ldx, const float* dY, long long ldy, int rows, int C,
+                        const float* stats, const float* gamma, const float* beta, float* dX, long long lddx,
+                        float* dgamma, float* dbeta, int accum, float* part, hipStream_t st) {
+  if (C % 4 || C > 1024 || rows < 2) return hipErrorInvalidValue;
+  const int nb = cdiv(rows, BN_RB);
+  const float *mean = stats, *rstd = stats + C;
+  float* p0 = part;
+  float* p1 = part + (size_t)nb * C;
+  float* s01 = part + 2 * (size_t)nb * C;  // [2][C]: sum dy', sum dy' xhat
+  hipLaunchKernelGGL(bn_part_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rows, C, 2, mean, rstd, gamma, beta, dY, ldy, p0,
+                     p1);
+  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, p0, p1, nb, C, rows, 2, nullptr, nullptr,
+                     nullptr, s01, s01 + C, dgamma, dbeta, accum);
+  hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(cdiv((long long)rows * (C / 4), 256)), dim3(256), 0, st, X, ldx, dY, ldy,
+                     rows, C, mean, rstd, gamma, beta, s01, s01 + C, dX, lddx);
+  return hipGetLastError();
+}
+
+hipError_t bn_running_update(float* rm, float* rv, const float* stats, int C, float momentum, hipStream_t st) {
+  hipLaunchKernelGGL(bn_running_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, rm, rv, stats, stats + 2 * C, C, momentum);
+  return hipGetLastError();
+}
+
+hipError_t kenc_input(const float* kpts, const float* scores, const float* size, float w, float h, int B, int n, int cin,
+                      float* out, hipStream_t st) {
+  hipLaunchKernelGGL(kenc_input_kernel, dim3(cdiv((long long)B * n, 256)), dim3(256), 0, st, kpts, scores, size, w, h, B, n,
+                     cin, out);
+  return hipGetLastError();
+}
+
+hipError_t head_gather(const float* src, int rows, int cols, bool by_cols, bool inverse, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(head_gather_kernel, dim3(cdiv((long long)rows * cols, 256)), dim3(256), 0, st, src, rows, cols,
+                     (int)by_cols, (int)inverse, dst);
+  return hipGetLastError();
+}
+
+hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M, int N, int iters, float* Cc, float* U,
+                            float* V, float* Z, hipStream_t st) {
+  const int M1 = M + 1, N1 = N + 1;
+  const float norm = -logf((float)(M + N)), lmu_last = logf((float)N) + norm, lnu_last = logf((float)M) + norm;
+  const long long tot = (long long)B * M1 * N1;
+  hipLaunchKernelGGL(sk_couplings_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, st, cost, alpha, B, M, N, Cc);
+  hipError_t e = hipMemsetAsync(V, 0, (size_t)B * N1 * sizeof(float), st);  // v_0 = 0 (:175)
+  if (e != hipSuccess) return e;
+  for (int t = 1; t <= iters; ++t) {
+    float* u = U + (size_t)(t - 1) * B * M1;
+    const float* vprev = V + (size_t)(t - 1) * B * N1;
+    float* v = V + (size_t)t * B * N1;
+    hipLaunchKernelGGL(sk_row_kernel, dim3(cdiv((long long)B * M1, 4)), dim3(256), 0, st, Cc, B, M1, N1, nullptr, vprev,
+                       nullptr, nullptr, norm, lmu_last, lnu_last, 0, u);
+    hipLaunchKernelGGL(sk_col_kernel, dim3(cdiv(N1, 64), B), dim3(256), 0, st, Cc, B, M1, N1, u, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, norm, lmu_last, lnu_last, 0, v);
+  }
+  const float* uT = iters > 0 ? U + (size_t)(iters - 1) * B * M1 : nullptr;
+  if (!uT) {  // no iterations: u = v = 0
+    e = hipMemsetAsync(U, 0, (size_t)B * M1 * sizeof(float), st);
+    if (e != hipSuccess) return e;
+    uT = U;
+  }
+  hipLaunchKernelGGL(sk_out_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, st, Cc, uT, V + (size_t)iters * B * N1, B, M1, N1,
+                     norm, Z);
+  return hipGetLastError();
+}
+
+size_t sk_train_scratch_floats(int B, int M, int N) {
+  return (size_t)B * (M + 1) * (N + 1) + 4 * (size_t)B * (M + N + 2) + B + 64;
+}
+
+hipError_t sk_train_backward(const float* Cc, const float* U, const float* V, const float* gZ, const float* gext, int B,
+                             int M, int N, int iters, float* gcost, float* galpha, float* ws, hipStream_t st) {
+  const int M1 = M + 1, N1 = N + 1;
+  const float norm = -logf((float)(M + N)), lmu_last = logf((float)N) + norm, lnu_last = logf((float)M) + norm;
+  const long long tot = (long long)B * M1 * N1;
+  float* gC = ws;
+  float* base = gC + tot;                   // [B][M1]: d/d u_T from Z
+  float* gu = base + (size_t)B * M1;        // [B][M1]
+  float* gv = gu + (size_t)B * M1;          // [B][N1]: d/d v_t
+  float* gv2 = gv + (size_t)B * N1;         // [B][N1]: d/d v_{t-1}
+  float* part = gv2 + (size_t)B * N1;       // [B]
+  hipError_t e = hipMemcpyAsync(gC, gZ, tot * sizeof(float), hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return e;
+  // Z = C + u_T + v_T - norm: d/d u_T = row sums of gZ, d/d v_T = column sums
+  hipLaunchKernelGGL(sk_row_kernel, dim3(cdiv((long long)B * M1, 4)), dim3(256), 0, st, gZ, B, M1, N1, nullptr, nullptr,
+                     nullptr, nullptr, norm, lmu_last, lnu_last, 2, base);
+  hipLaunchKernelGGL(sk_col_kernel, dim3(cdiv(N1, 64), B), dim3(256), 0, st, gZ, B, M1, N1, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, nullptr, norm, lmu_last, lnu_last, 2, gv);
+  for (int t = iters; t >= 1; --t) {
+    const float* u = U + (size_t)(t - 1) * B * M1;
+    const float* v = V + (size_t)t * B * N1;
+    const float* vp = t > 1 ? V + (size_t)(t - 1) * B * N1 : nullptr;  // v_0 = 0
+    // v_t = lnu - LSE_i(C + u_t): d/d u_t = base (t = T) - sum_j gv_j pc
+    hipLaunchKernelGGL(sk_row_kernel, dim3(cdiv((long long)B * M1, 4)), dim3(256), 0, st, Cc, B, M1, N1, u, v, gv,
+                       t == iters ? base : nullptr, norm, lmu_last, lnu_last, 1, gu);
+    // u_t = lmu - LSE_j(C + v_{t-1}): d/d v_{t-1}, and both steps' d/d C
+    hipLaunchKernelGGL(sk_col_kernel, dim3(cdiv(N1, 64), B), dim3(256), 0, st, Cc, B, M1, N1, u, v, vp, gu, gv, gC, norm,
+                       lmu_last, lnu_last, 1, gv2);
+    std::swap(gv, gv2);
+  }
+  const long long per = (long long)M * N;
+  const unsigned gx = 1 + (unsigned)std::min<long long>(cdiv(per, 256), 4096);
+  hipLaunchKernelGGL(sk_finish_kernel, dim3(gx, B), dim3(256), 0, st, gC, gext, M, N, gcost, part);
+  if (galpha) hipLaunchKernelGGL(sk_alpha_kernel, dim3(1), dim3(64), 0, st, part, B, galpha);
+  return hipGetLastError();
+}
+
+hipError_t sg_nll_grad(const uint8_t* gta, const int64_t* gt0, const int64_t* gt1, const float* stats, const float* g_nll,
+                       const float* g_pos, const float* g_neg, int B, int M, int N, int mode, float bal, float* gla,
+                       hipStream_t st) {
+  const long long tot = (long long)B * (M + 1) * (N + 1);
+  hipLaunchKernelGGL(sg_nll_grad_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, st, gta, gt0, gt1, stats, g_nll, g_pos, g_neg,
+                     B, M, N, mode, bal, gla);
+  return hipGetLastError();
+}
+
+}  // namespace lg

@@ -187,6 +187,16 @@ struct sg_handle {
   bool loaded = false;
 };
 
+// accessors for the training path (sg_train.cpp)
+namespace lg {
+const sg_config_t* sg_handle_config(const sg_handle* h) { return &h->cfg; }
+int sg_handle_device(const sg_handle* h) { return h->device; }
+int sg_handle_weight_index(const sg_handle* h, const std::string& name) {
+  auto it = h->index.find(name);
+  return it == h->index.end() ? -1 : it->second;
+}
+}  // namespace lg
+
 extern "C" {
 
 int sg_create(const sg_config_t* cfg, int device, sg_handle_t** out) {

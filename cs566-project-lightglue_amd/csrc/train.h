@@ -6,6 +6,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdint.h>
 
 namespace lg {
 
@@ -131,5 +132,39 @@ hipError_t la_grad_z(const float* z, const float* rs, const float* gd, int rows,
 // sigmoid_log_double_softmax forward: la [B][M+1][N+1] from sim, its row / column LSE and z0 / z1
 hipError_t la_forward(const float* sim, const float* lser, const float* lsec, const float* z0, const float* z1, int B, int M,
                       int N, float* la, hipStream_t st);
+
+// ---- SuperGlue training (sg_train.hip; superglue.py:63-201 in training mode)
+// BatchNorm1d with batch statistics over `rows` rows of C channels (C % 4 == 0, C <= 1024,
+// rows >= 2) followed by ReLU: Y = relu(gamma (X - mean) rstd + beta); stats [3][C] = (mean, rstd,
+// unbiased variance).  Backward: dX from dY (the gradient of the ReLU output); dgamma / dbeta
+// written (accum 0) or added (accum 1).  part: bn_part_floats(rows, C).
+size_t bn_part_floats(int rows, int C);
+hipError_t bn_train_fwd(const float* X, long long ldx, int rows, int C, const float* gamma, const float* beta, float* Y,
+                        long long ldy, float* stats, float* part, hipStream_t st);
+hipError_t bn_train_bwd(const float* X, long long ldx, const float* dY, long long ldy, int rows, int C, const float* stats,
+                        const float* gamma, const float* beta, float* dX, long long lddx, float* dgamma, float* dbeta,
+                        int accum, float* part, hipStream_t st);
+// running = (1 - momentum) running + momentum (mean, unbiased var) of stats
+hipError_t bn_running_update(float* rm, float* rv, const float* stats, int C, float momentum, hipStream_t st);
+// normalize_keypoints + [x, y(, score)] rows: out [B*n][cin]; size [B][2] (w, h) or null -> (w, h)
+hipError_t kenc_input(const float* kpts, const float* scores, const float* size, float w, float h, int B, int n, int cin,
+                      float* out, hipStream_t st);
+// head-major <-> reference channel order of MultiHeadedAttention (channel d*4 + h, :121-127):
+// dst[r][c] = src[perm(r)][c] (by_cols: src[r][perm(c)]), perm(h*64 + d) = d*4 + h; inverse: perm^-1
+hipError_t head_gather(const float* src, int rows, int cols, bool by_cols, bool inverse, float* dst, hipStream_t st);
+// log_optimal_transport (:181-201) keeping every iterate: Cc [B][M+1][N+1] couplings, U [iters][B][M+1]
+// (u_1..u_T), V [iters+1][B][N+1] (v_0 = 0 .. v_T), Z (already + log(M+N)).  alpha: device scalar.
+hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M, int N, int iters, float* Cc, float* U,
+                            float* V, float* Z, hipStream_t st);
+// its backward: d/d cost [B][M][N] (= inner block of d/d Cc, + gext when non-null) and d/d alpha
+// (scalar, overwritten; nullable) from gZ.  ws: sk_train_scratch_floats.
+size_t sk_train_scratch_floats(int B, int M, int N);
+hipError_t sk_train_backward(const float* Cc, const float* U, const float* V, const float* gZ, const float* gext, int B,
+                             int M, int N, int iters, float* gcost, float* galpha, float* ws, hipStream_t st);
+// d/d log_assignment of the NLL (mode 0 SuperGlue.loss, 1 NLLLoss) from d/d (nll, nll_pos, nll_neg)
+// (nullable rows) and the forward's out [5][B]
+hipError_t sg_nll_grad(const uint8_t* gta, const int64_t* gt0, const int64_t* gt1, const float* stats, const float* g_nll,
+                       const float* g_pos, const float* g_neg, int B, int M, int N, int mode, float bal, float* gla,
+                       hipStream_t st);
 
 }  // namespace lg

@@ -13,8 +13,11 @@ Deliberate differences from the reference:
 
 * the trained checkpoint is a download (:248-251); the module starts from PyTorch's default init
   (``weights`` is ignored) and takes weights through ``load_state_dict``;
-* eval only: BatchNorm uses its running statistics; a module in training mode raises (the
-  reference trains through ``torch.utils.checkpoint`` and batch statistics);
+* training mode runs ``sg_train_forward`` / ``sg_train_backward`` (a ``torch.autograd.Function``
+  over raw parameters): BatchNorm with batch statistics per image set and the running-statistics
+  updates of the reference's step, including the second GNN update its
+  ``torch.utils.checkpoint`` recomputation makes (:151-155); ``loss`` is differentiable through
+  ``sg_nll_backward``;
 * ``NLLLoss`` with explicit ``weights`` other than the ground truth's raises NotImplementedError
   (the kernel derives the weights from the ground truth, losses.py:46-73).
 """
@@ -116,7 +119,7 @@ class SuperGlue(nn.Module):
         return tuple((id(m), n, t.data_ptr(), t._version) for m in self.modules()
                      for n, t in list(m._parameters.items()) + list(m._buffers.items()) if t is not None)
 
-    def _ensure_handle(self, device):
+    def _ensure_handle(self, device, upload=True):
         lib = _lib.load()
         if self._handle is not None and self._handle_device != device:
             lib.sg_destroy(self._handle)
@@ -126,6 +129,8 @@ class SuperGlue(nn.Module):
             cfg = self._lib_config()
             _lib.check(lib.sg_create(ctypes.byref(cfg), device.index or 0, ctypes.byref(h)), "sg_create")
             self._handle, self._handle_device, self._weights_key = h, device, None
+        if not upload:
+            return lib
         key = self._weights_signature()
         if key != self._weights_key:
             sd = {k: v for k, v in self.state_dict(keep_vars=True).items() if not k.endswith("num_batches_tracked")}
@@ -174,8 +179,6 @@ class SuperGlue(nn.Module):
         ``gnn_descriptors0/1`` [B, N, D] (a check point for tests; not a reference output)."""
         for k in self.required_data_keys:
             assert k in data, f"Missing key {k} in data"
-        if self.training:
-            raise NotImplementedError("lightglue_amd.SuperGlue is eval-only (BatchNorm running statistics)")
         c = self.conf
         kpts0, kpts1 = data["keypoints0"], data["keypoints1"]
         if kpts0.shape[1] == 0 or kpts1.shape[1] == 0:  # no keypoints (:257-264)
@@ -213,6 +216,10 @@ class SuperGlue(nn.Module):
         d0, d1 = f32(data["descriptors0"]), f32(data["descriptors1"])
         sc0 = f32(data["keypoint_scores0"]) if c.use_scores else None
         sc1 = f32(data["keypoint_scores1"]) if c.use_scores else None
+        if self.training:
+            inp = _lib.SGInputs(B, M, N, _ptr(k0), _ptr(k1), _ptr(d0), _ptr(d1), _ptr(sc0), _ptr(sc1), _ptr(s0), _ptr(s1),
+                                w0, h0, w1, h1)
+            return self._forward_train(device, inp, (k0, k1, d0, d1, sc0, sc1, s0, s1), return_descriptors)
         lib = self._ensure_handle(device)
         ws, nb = self._workspace(lib, device, B, M, N)
         m0 = torch.empty((B, M), dtype=torch.int64, device=device)
@@ -234,15 +241,132 @@ class SuperGlue(nn.Module):
             pred["gnn_descriptors0"], pred["gnn_descriptors1"] = g0, g1
         return pred
 
+    # ------------------------------------------------------------ training (superglue.py:148-155,253-307)
+    def _schema_tensors(self):
+        """(name, tensor) in the library's schema order: parameters and BatchNorm running buffers."""
+        lib = _lib.load()
+        sd = dict(self.named_parameters())
+        sd.update({n: b for n, b in self.named_buffers() if not n.endswith("num_batches_tracked")})
+        out = []
+        for i in range(lib.sg_weight_count(self._handle)):
+            n = lib.sg_weight_name(self._handle, i).decode()
+            out.append((n, sd[n]))
+        return out
+
+    def _forward_train(self, device, inp, keep, return_descriptors):
+        self._ensure_handle(device, upload=False)
+        self._weights_key = None  # the eval path re-uploads: parameters / running stats change in place
+        named = self._schema_tensors()
+        for n, t in named:
+            if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
+                raise RuntimeError(f"lightglue_amd.SuperGlue: tensor {n} must be contiguous fp32 on {device}")
+        params = [t for _, t in named if isinstance(t, nn.Parameter)]
+        la, cost, m0, m1, ms0, ms1, g0, g1 = _SGTrain.apply(self, (inp, keep, named, return_descriptors), keep[2], keep[3],
+                                                            *params)
+        for m in self.modules():  # one running-statistics update per image set (:274-275, :160-170)
+            if isinstance(m, nn.BatchNorm1d) and m.num_batches_tracked is not None:
+                m.num_batches_tracked.add_(2)
+        pred = {"sinkhorn_cost": cost, "log_assignment": la, "matches0": m0, "matches1": m1, "matching_scores0": ms0,
+                "matching_scores1": ms1}
+        if return_descriptors:
+            pred["gnn_descriptors0"], pred["gnn_descriptors1"] = g0, g1
+        return pred
+
     def loss(self, pred, data):
-        """superglue.py:309-339 (forward values; no backward)."""
-        out = _nll(pred["log_assignment"], data, 0, float(self.conf.loss.nll_balancing))
+        """superglue.py:309-339; differentiable in ``pred["log_assignment"]`` (sg_nll_backward)."""
+        la = pred["log_assignment"]
+        bal = float(self.conf.loss.nll_balancing)
+        out = _SGNLL.apply(la, data, 0, bal) if la.requires_grad else _nll(la, data, 0, bal)
         losses = {"total": out[0], "assignment_nll": out[0], "nll_pos": out[1], "nll_neg": out[2],
                   "num_matchable": out[3], "num_unmatchable": out[4], "bin_score": self.bin_score[None]}
         return losses
 
     def metrics(self, pred, data):
         raise NotImplementedError
+
+
+class _SGTrain(torch.autograd.Function):
+    """sg_train_forward / sg_train_backward over the raw parameters (schema order)."""
+
+    @staticmethod
+    def forward(ctx, model, feed, d0, d1, *params):
+        inp, keep, named, want_desc = feed
+        lib = _lib.load()
+        h = model._handle
+        B, M, N = inp.B, inp.M, inp.N
+        dev = d0.device
+        nb = ctypes.c_size_t()
+        _lib.check(lib.sg_train_saved_bytes(h, B, M, N, ctypes.byref(nb)), "sg_train_saved_bytes")
+        saved = torch.empty(nb.value, dtype=torch.uint8, device=dev)
+        la = torch.empty((B, M + 1, N + 1), device=dev)
+        cost = torch.empty((B, M, N), device=dev)
+        m0 = torch.empty((B, M), dtype=torch.int64, device=dev)
+        m1 = torch.empty((B, N), dtype=torch.int64, device=dev)
+        ms0 = torch.empty((B, M), device=dev)
+        ms1 = torch.empty((B, N), device=dev)
+        g0 = torch.empty((B, M, 256), device=dev) if want_desc else None
+        g1 = torch.empty((B, N, 256), device=dev) if want_desc else None
+        out = _lib.SGOutputs(_ptr(m0), _ptr(m1), _ptr(ms0), _ptr(ms1), _ptr(cost), _ptr(la), _ptr(g0), _ptr(g1))
+        ptrs = (ctypes.c_void_p * len(named))(*[t.data_ptr() for _, t in named])
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(lib.sg_train_forward(h, ptrs, ctypes.byref(inp), ctypes.byref(out), _ptr(saved), nb.value, stream),
+                   "sg_train_forward")
+        ctx.model, ctx.inp, ctx.keep, ctx.named, ctx.saved = model, inp, keep, named, saved
+        ctx.keep_desc = (d0, d1)
+        nd = [m0, m1, ms0, ms1] + [t for t in (g0, g1) if t is not None]
+        ctx.mark_non_differentiable(*nd)
+        return la, cost, m0, m1, ms0, ms1, g0, g1
+
+    @staticmethod
+    def backward(ctx, g_la, g_cost, *_):
+        lib = _lib.load()
+        model, inp, named = ctx.model, ctx.inp, ctx.named
+        B, M, N = inp.B, inp.M, inp.N
+        dev = ctx.saved.device
+        grads = [torch.empty_like(t) if isinstance(t, nn.Parameter) else None for _, t in named]
+        gd0 = torch.empty((B, M, 256), device=dev) if ctx.needs_input_grad[2] else None
+        gd1 = torch.empty((B, N, 256), device=dev) if ctx.needs_input_grad[3] else None
+        nb = ctypes.c_size_t()
+        _lib.check(lib.sg_train_scratch_bytes(model._handle, B, M, N, ctypes.byref(nb)), "sg_train_scratch_bytes")
+        scratch = torch.empty(nb.value, dtype=torch.uint8, device=dev)
+        ptrs = (ctypes.c_void_p * len(named))(*[t.data_ptr() for _, t in named])
+        gptrs = (ctypes.c_void_p * len(named))(*[g.data_ptr() if g is not None else None for g in grads])
+        g_la = g_la.float().contiguous() if g_la is not None else None
+        g_cost = g_cost.float().contiguous() if g_cost is not None else None
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(lib.sg_train_backward(model._handle, ptrs, ctypes.byref(inp), _ptr(ctx.saved), ctx.saved.numel(),
+                                         _ptr(g_la), _ptr(g_cost), gptrs, _ptr(gd0), _ptr(gd1), _ptr(scratch), nb.value,
+                                         stream), "sg_train_backward")
+        ctx.saved = None
+        for n, m in model.named_modules():  # the checkpoint recomputation's second GNN update
+            if n.startswith("gnn.") and isinstance(m, nn.BatchNorm1d) and m.num_batches_tracked is not None:
+                m.num_batches_tracked.add_(2)
+        return (None, None, gd0, gd1, *[g for g in grads if g is not None])
+
+
+class _SGNLL(torch.autograd.Function):
+    """sg_nll_loss with its gradient (sg_nll_backward): out [5, B]; rows 0-2 differentiable."""
+
+    @staticmethod
+    def forward(ctx, la, data, mode, balancing):
+        prepared = nll_inputs(data, la.device)
+        out = _nll(la.detach(), data, mode, balancing, prepared)
+        ctx.prepared, ctx.mode, ctx.bal, ctx.shape = prepared, mode, balancing, la.shape
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (out,) = ctx.saved_tensors
+        B, M1, N1 = ctx.shape
+        g = g.float().contiguous()
+        gla = torch.empty((B, M1, N1), device=out.device)
+        gta, g0, g1 = ctx.prepared
+        lib = _lib.load()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(out.device).cuda_stream)
+        _lib.check(lib.sg_nll_backward(_ptr(out), _ptr(g[0]), _ptr(g[1]), _ptr(g[2]), B, M1 - 1, N1 - 1, _ptr(gta),
+                                       _ptr(g0), _ptr(g1), ctx.mode, ctx.bal, _ptr(gla), stream), "sg_nll_backward")
+        return gla, None, None, None
 
 
 def nll_inputs(data, device):
@@ -284,7 +408,7 @@ def nll_weights(la, data):
 
 
 class NLLLoss(nn.Module):
-    """losses.py:26-73 (forward values; no backward): ``forward(pred, data, weights=None) ->
+    """losses.py:26-73, differentiable in ``log_assignment`` (sg_nll_backward): ``forward(pred, data, weights=None) ->
     (nll, weights, metrics)``.  The sums run in ``sg_nll_kernel`` (fp64), which derives the weights
     from the ground truth itself; the returned ``weights`` tensor is the reference's [B, M+1, N+1]
     one (losses.py:52-60).  Explicit ``weights`` must be those ground-truth weights (what
@@ -301,7 +425,8 @@ class NLLLoss(nn.Module):
         derived = nll_weights(la, data)
         if weights is not None and not (weights.shape == derived.shape and torch.equal(weights.to(la.device), derived)):
             raise NotImplementedError("explicit loss weights other than the ground truth's (the kernel derives them)")
-        out = _nll(la, data, 1, float(self.conf.nll_balancing))
+        bal = float(self.conf.nll_balancing)
+        out = _SGNLL.apply(la, data, 1, bal) if la.requires_grad else _nll(la, data, 1, bal)
         metrics = {"assignment_nll": out[0], "nll_pos": out[1], "nll_neg": out[2], "num_matchable": out[3],
                    "num_unmatchable": out[4]}
         return out[0], derived, metrics

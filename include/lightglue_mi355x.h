@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define LG_ABI_VERSION 6
+#define LG_ABI_VERSION 7
 
 enum {
   LG_OK = 0,

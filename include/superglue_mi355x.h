@@ -84,6 +84,43 @@ int sg_nll_loss(const float* log_assignment, int32_t B, int32_t M, int32_t N, co
                 const int64_t* gt_matches0, const int64_t* gt_matches1, int32_t mode, float nll_balancing, float* out,
                 void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Training: SuperGlue's training step as torch autograd runs it in the reference
+ * (gluefactory/train.py:436-450 over superglue.py:253-339).  No reference counterpart as an
+ * interface; these entry points are what a torch.autograd.Function binds.
+ *
+ * `params` are raw fp32 device pointers in the schema order (sg_weight_name(h, i)) and the
+ * reference layouts (Conv1d weights [out][in][1]); gradients come back in the same order and
+ * layouts (`grads[i]` overwritten when non-null; BatchNorm running statistics take none).  All
+ * arithmetic is fp32 (f32-input matrix cores).
+ *
+ * sg_train_forward: the training-mode forward (superglue.py:253-307 with self.training): BatchNorm
+ * with batch statistics per image set, the Sinkhorn iterates kept for the backward in `saved`
+ * (sg_train_saved_bytes; caller-owned, pass it to sg_train_backward).  out->log_assignment is
+ * required; sinkhorn_cost, the matches / scores and descriptors0/1 are written when non-null.
+ * Updates the BatchNorm running statistics IN PLACE (params[] entries running_mean / running_var,
+ * momentum 0.1, unbiased variance), once per image set -- the reference's count.
+ * sg_train_backward: from d(loss)/d(log_assignment) [B][M+1][N+1] and d(loss)/d(sinkhorn_cost)
+ * [B][M][N] (each nullable: zero), writes every parameter gradient (bin_score included) and
+ * grad_desc0/1 [B][M][256] / [B][N][256] (nullable).  It also applies the GNN BatchNorms' second
+ * running-statistics update that the reference's torch.utils.checkpoint recomputation makes
+ * (superglue.py:151-155).  Scratch: sg_train_scratch_bytes.  Both asynchronous; the attention
+ * backward's dQ sums use float atomics (last-bit differences between calls).
+ * sg_nll_backward: d(loss)/d(log_assignment) of sg_nll_loss (mode 0 SuperGlue.loss, 1 NLLLoss)
+ * from d(loss)/d(nll, nll_pos, nll_neg) [B] each (nullable) and the forward's out [5][B].
+ */
+int sg_train_saved_bytes(const sg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+int sg_train_scratch_bytes(const sg_handle_t* h, int32_t B, int32_t M, int32_t N, size_t* bytes);
+int sg_train_forward(sg_handle_t* h, float* const* params, const sg_inputs_t* in, sg_outputs_t* out, void* saved,
+                     size_t saved_bytes, void* stream);
+int sg_train_backward(sg_handle_t* h, float* const* params, const sg_inputs_t* in, const void* saved, size_t saved_bytes,
+                      const float* grad_log_assignment, const float* grad_cost, float* const* grads, float* grad_desc0,
+                      float* grad_desc1, void* scratch, size_t scratch_bytes, void* stream);
+int sg_nll_backward(const float* stats, const float* grad_nll, const float* grad_nll_pos, const float* grad_nll_neg,
+                    int32_t B, int32_t M, int32_t N, const uint8_t* gt_assignment, const int64_t* gt_matches0,
+                    const int64_t* gt_matches1, int32_t mode, float nll_balancing, float* grad_log_assignment,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

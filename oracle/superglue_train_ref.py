@@ -1,0 +1,123 @@
+"""Functional torch-CPU restatement of the reference SuperGlue TRAINING step — TEST ORACLE.
+
+Test infrastructure only (see ``oracle/__init__.py``): the GPU tests differentiate this
+restatement with torch autograd (in float64) and compare every parameter gradient, both
+descriptor gradients and the BatchNorm running statistics with the HIP training path.  It is
+pinned to the reference's own autograd gradients by ``tests/golden/make_sg_grad_golden.py`` /
+``tests/test_oracle_sg_grad.py``.
+
+Restates (paths relative to ``/root/reference``):
+* ``gluefactory_nonfree/superglue.py:63-72`` ``MLP`` with ``nn.BatchNorm1d`` in training mode
+  (batch statistics over (b, n) of each call, biased variance in the normalisation);
+* ``:89-170`` the keypoint encoder and the GNN (each ``AttentionalPropagation`` call is one
+  BatchNorm batch: one image set);
+* ``:173-201`` ``log_optimal_transport``; ``:253-307`` ``_forward``; ``:309-339`` ``loss``;
+* the running-statistics bookkeeping of a training step: momentum 0.1 with the unbiased
+  variance, once per call in the forward, and once more per GNN call when the backward
+  recomputes the checkpointed layers (``:151-155``, ``torch.utils.checkpoint``).
+
+``W`` is a dict name -> torch tensor (reference state-dict keys); tensors that require grad get
+gradients through ``torch.autograd``.
+"""
+import torch
+
+from .lightglue_ref import log_optimal_transport
+from .superglue_ref import BN_EPS, normalize_keypoints, superglue_loss
+
+MOMENTUM = 0.1
+
+
+def _conv1(W, name, x):
+    return torch.einsum("oc,bcn->bon", W[name + ".weight"][:, :, 0], x) + W[name + ".bias"][None, :, None]
+
+
+def _bn_train(W, name, x, calls):
+    """BatchNorm1d forward in training mode on [B, C, n]; records (name, mean, unbiased var)."""
+    mean = x.mean((0, 2))
+    var = x.var((0, 2), unbiased=False)
+    calls.append((name, mean.detach(), x.detach().var((0, 2), unbiased=True)))
+    xh = (x - mean[None, :, None]) / torch.sqrt(var[None, :, None] + BN_EPS)
+    return xh * W[name + ".weight"][None, :, None] + W[name + ".bias"][None, :, None]
+
+
+def mlp_train(W, prefix, channels, x, calls):
+    """superglue.py:63-72 in training mode."""
+    idx = 0
+    for i in range(1, len(channels)):
+        x = _conv1(W, f"{prefix}.{idx}", x)
+        idx += 1
+        if i < len(channels) - 1:
+            x = torch.relu(_bn_train(W, f"{prefix}.{idx}", x, calls))
+            idx += 2
+    return x
+
+
+def _attention(q, k, v):
+    dim = q.shape[1]
+    prob = torch.softmax(torch.einsum("bdhn,bdhm->bhnm", q, k) / dim ** 0.5, dim=-1)
+    return torch.einsum("bhnm,bdhm->bdhn", prob, v)
+
+
+def _propagation(W, p, x, source, calls, heads=4):
+    b, d = x.shape[0], x.shape[1]
+    q, k, v = [_conv1(W, f"{p}.attn.proj.{j}", t).view(b, d // heads, heads, -1) for j, t in enumerate((x, source, source))]
+    msg = _conv1(W, f"{p}.attn.merge", _attention(q, k, v).contiguous().view(b, d, -1))
+    return mlp_train(W, f"{p}.mlp", [2 * d, 2 * d, d], torch.cat([x, msg], dim=1), calls)
+
+
+def sg_train_forward(W, data, conf):
+    """superglue.py:253-307 in training mode.  ``data``: keypoints0/1, descriptors0/1 [B, n, 256],
+    keypoint_scores0/1, and ``image_size`` [B, 2] or ``image_hw``.  Returns (la, cost, calls,
+    (gnn desc0, desc1)) where ``calls`` lists every BatchNorm call in order."""
+    from lightglue_amd.sg_weights import merged_conf
+
+    c = merged_conf(conf)
+    dt = W["bin_score"].dtype
+    k0, k1 = torch.as_tensor(data["keypoints0"]).to(dt), torch.as_tensor(data["keypoints1"]).to(dt)
+    if data.get("image_size") is not None:
+        size = torch.as_tensor(data["image_size"]).to(dt)
+    else:
+        h, w = data["image_hw"]
+        size = torch.tensor([[float(w), float(h)]], dtype=dt)
+    n0, n1 = normalize_keypoints(k0, size), normalize_keypoints(k1, size)
+    enc = [3 if c["use_scores"] else 2] + list(c["keypoint_encoder"]) + [c["descriptor_dim"]]
+    calls = []
+
+    def kenc(kp, sc):  # :89-104
+        inputs = [kp.transpose(1, 2)] + ([torch.as_tensor(sc).to(dt)[:, None]] if c["use_scores"] else [])
+        return mlp_train(W, "kenc.encoder", enc, torch.cat(inputs, dim=1), calls)
+
+    d0 = data["descriptors0"].transpose(1, 2) + kenc(n0, data.get("keypoint_scores0"))
+    d1 = data["descriptors1"].transpose(1, 2) + kenc(n1, data.get("keypoint_scores1"))
+    for i, name in enumerate(c["GNN_layers"]):  # :148-170
+        p = f"gnn.layers.{i}"
+        src0, src1 = (d0, d1) if name == "self" else (d1, d0)
+        e0 = _propagation(W, p, d0, src0, calls)
+        e1 = _propagation(W, p, d1, src1, calls)
+        d0, d1 = d0 + e0, d1 + e1
+    md0, md1 = _conv1(W, "final_proj", d0), _conv1(W, "final_proj", d1)
+    cost = torch.einsum("bdn,bdm->bnm", md0, md1) / c["descriptor_dim"] ** 0.5
+    la = log_optimal_transport(cost, W["bin_score"], c["num_sinkhorn_iterations"])
+    return la, cost, calls, (d0, d1)
+
+
+def sg_train_loss(la, gt, nll_balancing=0.5):
+    """torch.mean(SuperGlue.loss(...)["total"]) (train.py:436 over superglue.py:309-339)."""
+    out = superglue_loss(la, gt["gt_assignment"], gt["gt_matches0"], gt["gt_matches1"], nll_balancing)
+    return torch.mean(out["total"]), out
+
+
+def running_stats_after_step(W, calls, momentum=MOMENTUM):
+    """The BatchNorm running statistics after one training step: every call updates its module's
+    statistics in order; the GNN's calls update them a second time in the backward (the
+    checkpoint recomputation, :151-155).  Returns {buffer name: tensor}."""
+    out = {}
+    for n in {name for name, _, _ in calls}:
+        out[n + ".running_mean"] = W[n + ".running_mean"].detach().clone()
+        out[n + ".running_var"] = W[n + ".running_var"].detach().clone()
+    replay = [cl for cl in calls if cl[0].startswith("gnn.")]
+    for name, mean, varu in calls + replay:
+        rm, rv = out[name + ".running_mean"], out[name + ".running_var"]
+        out[name + ".running_mean"] = (1 - momentum) * rm + momentum * mean
+        out[name + ".running_var"] = (1 - momentum) * rv + momentum * varu
+    return out

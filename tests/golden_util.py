@@ -16,7 +16,7 @@ def case_names(prefix=""):
     return sorted(
         os.path.basename(p)[:-4]
         for p in glob.glob(os.path.join(HERE, "*.npz"))
-        if os.path.basename(p).startswith(prefix) and not os.path.basename(p).startswith(("sinkhorn", "sp_", "sg_", "loss_", "grad_", "configs4"))
+        if os.path.basename(p).startswith(prefix) and not os.path.basename(p).startswith(("sinkhorn", "sp_", "sg_", "loss_", "grad_", "configs4", "sgtrain_"))
     )
 
 

@@ -1,0 +1,67 @@
+"""SuperGlue training-step golden fixtures (tests/golden/sgtrain_*.npz, make_sg_grad_golden.py):
+loading, input regeneration (the SuperGlue golden recipes, sg_golden_util.sg_case) and the float64
+oracle step (oracle/superglue_train_ref.py) they pin."""
+import glob
+import json
+import os
+
+import numpy as np
+import torch
+
+from sg_golden_util import GOLDEN, sg_case  # noqa: F401
+from sp_golden_util import sha
+
+
+def sgtrain_names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "sgtrain_*.npz")))
+
+
+def load_sgtrain(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    g = {k: z[k] for k in z.files if k != "meta_json"}
+    return g, json.loads(str(z["meta_json"]))
+
+
+def sgtrain_case(meta):
+    """(conf, state dict, data, gt) exactly as make_sg_grad_golden.py built them (SHA-checked)."""
+    conf, sd, data, gt = sg_case(meta)
+    inp = {k: v for k, v in data.items() if k != "image_hw"}
+    assert sha(inp) == meta["inputs_sha256"], "input recipe drifted"
+    assert sha(sd) == meta["weights_sha256"], "weight recipe drifted"
+    assert sha(gt) == meta["gt_sha256"], "ground-truth recipe drifted"
+    return conf, sd, data, gt
+
+
+def is_buffer(name):
+    return name.endswith(("running_mean", "running_var", "num_batches_tracked"))
+
+
+def oracle_sg_step(conf, sd, data, gt, dtype=torch.float64):
+    """The oracle's training step: (loss, {param: grad}, gdesc0, gdesc1, {buffer: running stat},
+    la) -- d mean(total) / d (parameters, descriptors) and the running statistics after it."""
+    from lightglue_amd.sg_weights import merged_conf
+    from oracle.superglue_train_ref import running_stats_after_step, sg_train_forward, sg_train_loss
+
+    W = {}
+    for k, v in sd.items():
+        if k.endswith("num_batches_tracked"):
+            continue
+        t = torch.from_numpy(np.asarray(v).copy()).to(dtype)
+        W[k] = t if is_buffer(k) else t.requires_grad_()
+    feed = {k: (torch.from_numpy(v).to(dtype) if isinstance(v, np.ndarray) else v) for k, v in data.items()}
+    d0 = feed["descriptors0"].clone().requires_grad_()
+    d1 = feed["descriptors1"].clone().requires_grad_()
+    feed["descriptors0"], feed["descriptors1"] = d0, d1
+    la, _, calls, _ = sg_train_forward(W, feed, conf)
+    bal = merged_conf(conf)["loss"]["nll_balancing"]
+    loss, _ = sg_train_loss(la, {k: torch.from_numpy(v) for k, v in gt.items()}, bal)
+    loss.backward()
+    grads = {k: (w.grad if w.grad is not None else torch.zeros_like(w)).double().numpy()
+             for k, w in W.items() if not is_buffer(k)}
+    stats = {k: v.double().numpy() for k, v in running_stats_after_step(W, calls).items()}
+    return float(loss.detach()), grads, d0.grad.double().numpy(), d1.grad.double().numpy(), stats, la.detach()
+
+
+def golden_entries(g, name):
+    idx = g.get(f"gidx:{name}")
+    return (None if idx is None else idx.astype(np.int64)), g[f"g64:{name}"]

@@ -1,0 +1,156 @@
+"""SuperGlue TRAINING step on the GPU (lightglue_amd.SuperGlue in training mode -> sg_train_forward /
+sg_train_backward / sg_nll_backward of liblightglue_mi355x.so) against the reference's own autograd
+step (tests/golden/sgtrain_*.npz, make_sg_grad_golden.py) and the float64 oracle
+(oracle/superglue_train_ref.py) -- needs an MI355X.
+
+Bars, per parameter tensor: max |g_gpu - g64| <= 8 spread32 + 1e-6 max|g64| + 1e-12, where
+spread32 is the distance of the reference's own float32 autograd gradient from float64 (stored in
+the golden; for a case without a golden, the oracle's float32 run gives it).  The HIP step is fp32
+arithmetic like the reference's float32 run with other summation orders (and float-atomic dQ
+sums).  The same bar holds the descriptor gradients, the BatchNorm running statistics after the
+step (the GNN's updated twice per step: forward and the checkpoint recomputation,
+superglue.py:151-155) and the log assignment of the training forward.
+"""
+import numpy as np
+import pytest
+import torch
+
+from sg_golden_util import ground_truth
+from sg_grad_golden_util import golden_entries, load_sgtrain, oracle_sg_step, sgtrain_case, sgtrain_names
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def gpu_step(conf, sd, data, gt):
+    from lightglue_amd import SuperGlue
+
+    m = SuperGlue(conf).to(DEV)
+    full = m.state_dict()
+    full.update({k: torch.from_numpy(np.asarray(v).copy()) for k, v in sd.items()})
+    m.load_state_dict(full, strict=True)
+    m.train()
+    B = data["keypoints0"].shape[0]
+    feed = {k: torch.from_numpy(v).to(DEV) for k, v in data.items() if k not in ("image_size", "image_hw")}
+    d0 = feed["descriptors0"].clone().requires_grad_()
+    d1 = feed["descriptors1"].clone().requires_grad_()
+    feed["descriptors0"], feed["descriptors1"] = d0, d1
+    hw = data.get("image_hw", (480, 640))
+    view = {"image": torch.zeros(B, 1, *hw, device=DEV)}
+    if data.get("image_size") is not None:
+        view["image_size"] = torch.from_numpy(np.asarray(data["image_size"], np.float32)).to(DEV)
+    feed.update({"view0": view, "view1": dict(view)})
+    feed.update({k: torch.from_numpy(v).to(DEV) for k, v in gt.items()})
+    pred = m(feed)
+    losses = m.loss(pred, feed)
+    loss = torch.mean(losses["total"])  # train.py:436
+    loss.backward()  # train.py:450
+    torch.cuda.synchronize()
+    grads = {n: (p.grad.detach().double().cpu().numpy() if p.grad is not None else None) for n, p in m.named_parameters()}
+    bufs = {n: b.detach().double().cpu().numpy() for n, b in m.named_buffers() if not n.endswith("num_batches_tracked")}
+    nbt = {n: int(b) for n, b in m.named_buffers() if n.endswith("num_batches_tracked")}
+    return (float(loss.detach()), grads, d0.grad.double().cpu().numpy(), d1.grad.double().cpu().numpy(), bufs, nbt,
+            pred["log_assignment"].detach().double().cpu().numpy())
+
+
+def _check(tag, got, ref, tol, worst, bad):
+    e = float(np.abs(got - ref).max())
+    worst.append((e / tol, tag))
+    if e > tol:
+        bad.append((tag, e, tol))
+
+
+@pytest.mark.parametrize("name", sgtrain_names())
+def test_sg_training_step_matches_reference_and_oracle(name):
+    g, meta = load_sgtrain(name)
+    conf, sd, data, gt = sgtrain_case(meta)
+    loss, grads, gd0, gd1, bufs, nbt, la = gpu_step(conf, sd, data, gt)
+    assert abs(loss - float(g["loss64"])) <= 1e-5 * abs(float(g["loss64"]))
+    oloss, og, ogd0, ogd1, ostats, ola = oracle_sg_step(conf, sd, data, gt)
+    worst, bad = [], []
+    for n in meta["names"]:
+        assert grads[n] is not None, f"no gradient for {n}"
+        tol = 8 * float(g[f"spread32:{n}"]) + 1e-6 * float(g[f"max64:{n}"]) + 1e-12
+        idx, ref = golden_entries(g, n)
+        flat = grads[n].reshape(-1)
+        _check(n, flat if idx is None else flat[idx], ref, tol, worst, bad)
+        _check(n + " (oracle)", flat, og[n].reshape(-1), tol, worst, bad)
+    for got, key in ((gd0, "gdesc0"), (gd1, "gdesc1")):
+        tol = 8 * float(g[f"spread_{key}"]) + 1e-6 * np.abs(g[key]).max() + 1e-12
+        _check(key, got, g[key], tol, worst, bad)
+    for n, v in bufs.items():
+        ref = g[f"buf64:{n}"]
+        tol = 8 * float(g[f"bufspread:{n}"]) + 1e-6 * np.abs(ref).max() + 1e-12
+        _check(n, v, ref, tol, worst, bad)
+        _check(n + " (oracle)", v, ostats[n], tol, worst, bad)
+    assert nbt == meta["num_batches_tracked"]
+    worst.sort(reverse=True)
+    print(name, "loss", loss, "worst err/tol:", [(n, round(r, 3)) for r, n in worst[:6]])
+    assert not bad, bad[:12]
+    # the training forward's log assignment against the oracle's (float32 oracle run for the scale)
+    _, _, _, _, _, ola32 = oracle_sg_step(conf, sd, data, gt, dtype=torch.float32)
+    spread = float(np.abs(ola32.double().numpy() - ola.numpy()).max())
+    np.testing.assert_allclose(la, ola.numpy(), atol=max(1e-5, 8 * spread), rtol=0)
+
+
+@pytest.mark.parametrize("B,M,N,layers,iters", [(3, 50, 37, ["self", "cross"], 10), (1, 33, 70, ["cross"], 7)])
+def test_sg_training_step_ragged_against_oracle(B, M, N, layers, iters):
+    """Shapes the goldens do not cover (odd sizes, M != N, B = 1 and 3) against the float64 oracle;
+    the bar's spread comes from the oracle's own float32 step."""
+    from lightglue_amd.sg_weights import superglue_state_dict, synthetic_scores
+    from lightglue_amd.weights import synthetic_pair
+
+    conf = {"GNN_layers": layers, "num_sinkhorn_iterations": iters, "keypoint_encoder": [16, 32]}
+    sd = superglue_state_dict(conf, seed=11)
+    p = synthetic_pair(B, M, N, seed=12, width=640, height=480)
+    data = {"keypoints0": p["keypoints0"], "keypoints1": p["keypoints1"], "descriptors0": p["descriptors0"],
+            "descriptors1": p["descriptors1"], "keypoint_scores0": synthetic_scores(B, M, seed=13),
+            "keypoint_scores1": synthetic_scores(B, N, seed=14), "image_hw": (480, 640)}
+    gt = ground_truth(B, M, N, 15)
+    loss, grads, gd0, gd1, bufs, nbt, la = gpu_step(conf, sd, data, gt)
+    l64, og, ogd0, ogd1, ostats, _ = oracle_sg_step(conf, sd, data, gt)
+    l32, og32, o32d0, o32d1, ostats32, _ = oracle_sg_step(conf, sd, data, gt, dtype=torch.float32)
+    assert abs(loss - l64) <= 1e-5 * abs(l64)
+    worst, bad = [], []
+    for n, ref in og.items():
+        tol = 8 * float(np.abs(og32[n] - ref).max()) + 1e-6 * float(np.abs(ref).max()) + 1e-12
+        _check(n, grads[n], ref, tol, worst, bad)
+    for got, ref, r32, key in ((gd0, ogd0, o32d0, "gdesc0"), (gd1, ogd1, o32d1, "gdesc1")):
+        _check(key, got, ref, 8 * float(np.abs(r32 - ref).max()) + 1e-6 * np.abs(ref).max() + 1e-12, worst, bad)
+    for n, ref in ostats.items():
+        _check(n, bufs[n], ref, 8 * float(np.abs(ostats32[n] - ref).max()) + 1e-6 * np.abs(ref).max() + 1e-12, worst, bad)
+    worst.sort(reverse=True)
+    print("ragged", B, M, N, "worst err/tol:", [(n, round(r, 3)) for r, n in worst[:6]])
+    assert not bad, bad[:12]
+    assert all(v == (4 if n.startswith("gnn.") else 2) for n, v in nbt.items())
+
+
+def test_nll_losses_are_differentiable():
+    """SuperGlue.loss (mode 0) and NLLLoss (mode 1) backward (sg_nll_backward) against torch autograd
+    of the oracle restatements (float64), including gradients of nll_pos / nll_neg."""
+    from lightglue_amd import SuperGlue
+    from lightglue_amd.superglue import NLLLoss
+    from oracle.superglue_ref import nll_loss, superglue_loss
+
+    B, M = 3, 40
+    gt = ground_truth(B, M, M, 4)
+    rng = np.random.Generator(np.random.PCG64(9))
+    la0 = (rng.standard_normal((B, M + 1, M + 1)) - 3.0).astype(np.float32)
+    gtd = {k: torch.from_numpy(v).to(DEV) for k, v in gt.items()}
+    w = torch.from_numpy(rng.standard_normal((3, B)).astype(np.float32))
+    # SuperGlue.loss
+    la = torch.from_numpy(la0).to(DEV).requires_grad_()
+    out = SuperGlue({"GNN_layers": []}).to(DEV).loss({"log_assignment": la}, gtd)
+    (w[0].to(DEV) * out["total"] + w[1].to(DEV) * out["nll_pos"] + w[2].to(DEV) * out["nll_neg"]).sum().backward()
+    la64 = torch.from_numpy(la0).double().requires_grad_()
+    ref = superglue_loss(la64, gt["gt_assignment"], gt["gt_matches0"], gt["gt_matches1"])
+    (w[0].double() * ref["total"] + w[1].double() * ref["nll_pos"] + w[2].double() * ref["nll_neg"]).sum().backward()
+    np.testing.assert_allclose(la.grad.cpu().double().numpy(), la64.grad.numpy(), atol=1e-7, rtol=1e-5)
+    # NLLLoss (losses.py), M == N
+    la = torch.from_numpy(la0).to(DEV).requires_grad_()
+    total, _, metrics = NLLLoss({"nll_balancing": 0.3})({"log_assignment": la}, gtd)
+    (w[0].to(DEV) * total + w[1].to(DEV) * metrics["nll_pos"]).sum().backward()
+    la64 = torch.from_numpy(la0).double().requires_grad_()
+    t64, m64 = nll_loss(la64, gt["gt_assignment"], gt["gt_matches0"], gt["gt_matches1"], 0.3)
+    (w[0].double() * t64 + w[1].double() * m64["nll_pos"]).sum().backward()
+    np.testing.assert_allclose(la.grad.cpu().double().numpy(), la64.grad.numpy(), atol=1e-7, rtol=1e-5)

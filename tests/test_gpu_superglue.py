@@ -158,7 +158,8 @@ def test_superglue_matches_oracle(B, M, N, conf):
 
 
 def test_superglue_weight_reload_and_errors():
-    """Replacing a parameter / buffer reloads the packed weights; CPU inputs and training raise."""
+    """Replacing a parameter / buffer reloads the packed weights; a training step (running statistics
+    updated in place) is picked up by the next eval forward."""
     from lightglue_amd.sg_weights import superglue_state_dict
     from lightglue_amd.weights import synthetic_pair
 
@@ -175,9 +176,15 @@ def test_superglue_weight_reload_and_errors():
     assert not torch.equal(a["gnn_descriptors0"], b["gnn_descriptors0"])
     ref = superglue_forward({k: (v if k != "gnn.layers.1.mlp.1.running_var" else v * 4) for k, v in sd.items()}, data, conf)
     np.testing.assert_allclose(b["gnn_descriptors0"].numpy(), ref["gnn_desc0"].transpose(1, 2).numpy(), atol=1e-4)
-    m.train()
-    with pytest.raises(NotImplementedError):
-        run(m, data)
+    m.train()  # batch statistics (sg_train_forward); the step updates the running statistics in place
+    t = run(m, data)
+    assert torch.isfinite(t["log_assignment"]).all()
+    m.eval()  # ... so the eval path re-uploads them
+    c = run(m, data)
+    sd2 = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    assert not np.array_equal(sd2["gnn.layers.1.mlp.1.running_var"], sd["gnn.layers.1.mlp.1.running_var"] * 4)
+    ref = superglue_forward(sd2, data, conf)
+    np.testing.assert_allclose(c["gnn_descriptors0"].numpy(), ref["gnn_desc0"].transpose(1, 2).numpy(), atol=1e-4)
 
 
 @pytest.mark.parametrize("tile", ["big", "medium", "small"])

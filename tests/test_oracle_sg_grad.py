@@ -1,0 +1,40 @@
+"""Pin the float64 SuperGlue training step of the oracle (oracle/superglue_train_ref.py) to the
+reference's own autograd step (tests/golden/sgtrain_*.npz, make_sg_grad_golden.py).
+
+Both sides are float64 torch-CPU autograd over the same algorithm, so the bar is tight:
+|d| <= 1e-9 max|g| + 1e-12 per tensor.  Several gradients are exactly zero mathematically (the key
+projection's bias shifts every score of a query equally, :107-111; a bias feeding a batch-norm
+is removed by its mean, :63-72): both sides hold ~1e-17 of rounding there, inside the 1e-12.
+The running statistics after the step are compared too (the GNN's updated twice: forward and the
+checkpoint recomputation, :151-155), and the step's num_batches_tracked bookkeeping.
+"""
+import numpy as np
+import pytest
+
+from sg_grad_golden_util import golden_entries, is_buffer, load_sgtrain, oracle_sg_step, sgtrain_case, sgtrain_names
+
+
+@pytest.mark.parametrize("name", sgtrain_names())
+def test_oracle_sg_training_step_matches_reference(name):
+    g, meta = load_sgtrain(name)
+    conf, sd, data, gt = sgtrain_case(meta)
+    loss, og, gd0, gd1, stats, _ = oracle_sg_step(conf, sd, data, gt)
+    assert abs(loss - float(g["loss64"])) <= 1e-10 * abs(float(g["loss64"]))
+    assert abs(float(g["loss32"]) - loss) <= 1e-5 * abs(loss)
+    assert list(og) == meta["names"]
+    for n in meta["names"]:
+        idx, ref = golden_entries(g, n)
+        got = og[n].reshape(-1)
+        got = got if idx is None else got[idx]
+        tol = 1e-9 * float(g[f"max64:{n}"]) + 1e-12
+        assert np.abs(got - ref).max() <= tol, n
+    for gd, key in ((gd0, "gdesc0"), (gd1, "gdesc1")):
+        assert np.abs(gd - g[key]).max() <= 1e-9 * np.abs(g[key]).max() + 1e-12, key
+    bufs = [k[len("buf64:"):] for k in g if k.startswith("buf64:")]
+    assert sorted(bufs) == sorted(stats)
+    for n in bufs:
+        ref = g[f"buf64:{n}"]
+        assert np.abs(stats[n] - ref).max() <= 1e-12 * max(np.abs(ref).max(), 1.0), n
+    for n, v in meta["num_batches_tracked"].items():  # two image sets per call site, GNN replayed
+        assert v == (4 if n.startswith("gnn.") else 2), n
+    assert all(is_buffer(k) or k in og for k in sd if not k.endswith("num_batches_tracked"))

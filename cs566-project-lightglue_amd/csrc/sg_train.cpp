@@ -91,7 +91,7 @@ struct Lay {
   float *WQKV, *BQKV, *WM, *QKV, *LSE, *O, *CAT, *H1, *ST, *G, *Y;
 };
 struct Saved {
-  float *KIN, *X0, *MD, *COST, *CC, *U, *V, *FWS, *PART;
+  float *KIN, *X0, *MD, *COST, *CC, *U, *V, *FWS, *PART, *SKP;
   std::vector<Enc> enc;
   std::vector<Lay> lay;
   size_t bytes;
@@ -138,6 +138,7 @@ Saved carve_saved(char* base, const Dims& d) {
   size_t p = bn_part_floats(rmax, 2 * D);
   for (size_t i = 1; i + 1 < d.ch.size(); ++i) p = std::max(p, bn_part_floats(rmax, d.ch[i]));
   s.PART = c.f(p + 64);
+  s.SKP = c.f(sk_train_part_floats(d.B, d.M, d.N) + 64);
   s.bytes = c.off;
   return s;
 }
@@ -357,7 +358,7 @@ int sg_train_forward(sg_handle_t* h, float* const* params, const sg_inputs_t* in
   }
   if (out->sinkhorn_cost)
     ST_HIP(hipMemcpyAsync(out->sinkhorn_cost, s.COST, (size_t)B * M * N * 4, hipMemcpyDeviceToDevice, c.st));
-  ST_HIP(sk_train_forward(s.COST, P.w("bin_score"), B, M, N, d.T, s.CC, s.U, s.V, out->log_assignment, c.st));
+  ST_HIP(sk_train_forward(s.COST, P.w("bin_score"), B, M, N, d.T, s.CC, s.U, s.V, out->log_assignment, s.SKP, c.st));
   if (out->matches0 && out->matches1 && out->matching_scores0 && out->matching_scores1)
     ST_HIP(filter_from_scores(out->log_assignment, B, M, N, sg_handle_config(h)->filter_threshold, s.FWS, out->matches0,
                               out->matches1, out->matching_scores0, out->matching_scores1, c.st));

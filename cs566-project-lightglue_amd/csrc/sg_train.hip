@@ -88,17 +88,32 @@ __global__ __launch_bounds__(256) void bn_part_kernel(const float* X, long long 
   }
 }
 
-// Ordered sum of the partials.  mode 0: mean; 1: rstd = 1 / sqrt(var + eps) and the unbiased
-// variance (running statistics); 2: s0 = sum dy', s1 = sum dy' xhat, dbeta / dgamma (+)= them.
+// Ordered sum of the partials: a workgroup = 16 columns x 16 partial groups (group g sums partials
+// g, g + 16, ...; the groups combine in order).  mode 0: mean; 1: rstd = 1 / sqrt(var + eps) and
+// the unbiased variance (running statistics); 2: s0 = sum dy', s1 = sum dy' xhat, dbeta / dgamma
+// (+)= them.
 __global__ __launch_bounds__(256) void bn_final_kernel(const float* part0, const float* part1, int nb, int C, int rows,
                                                        int mode, float* mean, float* rstd, float* varu, float* s0,
                                                        float* s1, float* dgamma, float* dbeta, int accum) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float r0[16][16], r1[16][16];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float a = 0.f, b = 0.f;
-  for (int i = 0; i < nb; ++i) {
-    a += part0[(long long)i * C + c];
-    if (mode == 2) b += part1[(long long)i * C + c];
+  if (c < C) {
+    for (int i = g; i < nb; i += 16) {
+      a += part0[(long long)i * C + c];
+      if (mode == 2) b += part1[(long long)i * C + c];
+    }
+  }
+  r0[g][cl] = a;
+  r1[g][cl] = b;
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  a = 0.f;
+  b = 0.f;
+  for (int q = 0; q < 16; ++q) {
+    a += r0[q][cl];
+    b += r1[q][cl];
   }
   if (mode == 0) {
     mean[c] = a / (float)rows;
@@ -242,24 +257,30 @@ __global__ __launch_bounds__(256) void sk_row_kernel(const float* Cc, int B, int
   if (l == 0) out[row] = mode == 1 ? (base ? base[row] : 0.f) - acc : acc;
 }
 
-// v[b][j] = lnu_j - logsumexp_i (C[b][i][j] + u[b][i])          (:177; 64 columns x 4 row groups)
+// v[b][j] = lnu_j - logsumexp_i (C[b][i][j] + u[b][i])          (:177)
 // mode 1 (backward of step t): with u = u_t, v = v_t, vp = v_{t-1}, gu = d/d u_t, gv = d/d v_t:
 //   pr = exp(C + vp_j + u_i - lmu_i) (u_t's softmax), pc = exp(C + u_i + v_j - lnu_j) (v_t's)
 //   out[j] = d/d v_{t-1} = -sum_i gu_i pr;  gC -= gv_j pc + gu_i pr  (in place)
 // mode 2: colsum[b][j] = sum_i C[b][i][j]
-__global__ __launch_bounds__(256) void sk_col_kernel(const float* Cc, int B, int M1, int N1, const float* u,
-                                                     const float* v, const float* vp, const float* gu, const float* gv,
-                                                     float* gC, float norm, float lmu_last, float lnu_last, int mode,
-                                                     float* out) {
+// Pass 1: a workgroup = 64 columns x SK_CH rows of one pair (4 row groups of 64 lanes), so a launch
+// has (N+1)/64 x (M+1)/SK_CH x B workgroups; it writes one (max, sum) or sum per column and chunk.
+// Pass 2 combines the chunks of a column in order.
+constexpr int SK_CH = 128;
+
+__global__ __launch_bounds__(256) void sk_col_part_kernel(const float* Cc, int B, int M1, int N1, const float* u,
+                                                          const float* v, const float* vp, const float* gu,
+                                                          const float* gv, float* gC, float norm, float lmu_last,
+                                                          float lnu_last, int mode, float* part) {
   __shared__ float sm[4][64], ss[4][64];
-  const int b = blockIdx.y, j = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  const int b = blockIdx.z, ch = blockIdx.y, j = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
   const bool ok = j < N1;
   const long long base = (long long)b * M1 * N1;
+  const int i0 = ch * SK_CH, i1 = min(M1, i0 + SK_CH);
   float m = -INFINITY, s = 0.f;
   if (ok) {
     if (mode == 0) {
       const float* ub = u + (long long)b * M1;
-      for (int i = grp; i < M1; i += 4) lse_push(Cc[base + (long long)i * N1 + j] + ub[i], m, s);
+      for (int i = i0 + grp; i < i1; i += 4) lse_push(Cc[base + (long long)i * N1 + j] + ub[i], m, s);
     } else if (mode == 1) {
       const float* ub = u + (long long)b * M1;
       const float* gub = gu + (long long)b * M1;
@@ -267,7 +288,7 @@ __global__ __launch_bounds__(256) void sk_col_kernel(const float* Cc, int B, int
       const float vpj = vp ? vp[(long long)b * N1 + j] : 0.f;
       const float lnu = j < N1 - 1 ? norm : lnu_last;
       float acc = 0.f;
-      for (int i = grp; i < M1; i += 4) {
+      for (int i = i0 + grp; i < i1; i += 4) {
         const long long k = base + (long long)i * N1 + j;
         const float cij = Cc[k], ui = ub[i], gui = gub[i];
         const float pr = expf(cij + vpj + ui - (i < M1 - 1 ? norm : lmu_last));
@@ -277,7 +298,7 @@ __global__ __launch_bounds__(256) void sk_col_kernel(const float* Cc, int B, int
       }
       s = -acc;
     } else {
-      for (int i = grp; i < M1; i += 4) s += Cc[base + (long long)i * N1 + j];
+      for (int i = i0 + grp; i < i1; i += 4) s += Cc[base + (long long)i * N1 + j];
     }
   }
   sm[grp][threadIdx.x & 63] = m;
@@ -285,14 +306,38 @@ __global__ __launch_bounds__(256) void sk_col_kernel(const float* Cc, int B, int
   __syncthreads();
   if (grp != 0 || !ok) return;
   const int c = threadIdx.x & 63;
+  float mo = -INFINITY, so;
+  if (mode == 0) {
+    for (int q = 0; q < 4; ++q) mo = fmaxf(mo, sm[q][c]);
+    so = 0.f;
+    for (int q = 0; q < 4; ++q) so += mo == -INFINITY ? 0.f : ss[q][c] * expf(sm[q][c] - mo);
+  } else {
+    so = ((ss[0][c] + ss[1][c]) + ss[2][c]) + ss[3][c];
+  }
+  const long long o = ((long long)b * gridDim.y + ch) * N1 + j;
+  part[2 * o] = mo;
+  part[2 * o + 1] = so;
+}
+
+__global__ void sk_col_final_kernel(const float* part, int B, int N1, int nch, float norm, float lnu_last, int mode,
+                                    float* out) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)B * N1) return;
+  const int b = (int)(t / N1), j = (int)(t - (long long)b * N1);
+  const float* p = part + 2 * ((long long)b * nch * N1 + j);
   if (mode == 0) {
     float mx = -INFINITY;
-    for (int q = 0; q < 4; ++q) mx = fmaxf(mx, sm[q][c]);
-    float t = 0.f;
-    for (int q = 0; q < 4; ++q) t += mx == -INFINITY ? 0.f : ss[q][c] * expf(sm[q][c] - mx);
-    out[(long long)b * N1 + j] = (j < N1 - 1 ? norm : lnu_last) - (mx + logf(t));
+    for (int c = 0; c < nch; ++c) mx = fmaxf(mx, p[2 * (long long)c * N1]);
+    float sum = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      const float mc = p[2 * (long long)c * N1];
+      sum += mc == -INFINITY ? 0.f : p[2 * (long long)c * N1 + 1] * expf(mc - mx);
+    }
+    out[t] = (j < N1 - 1 ? norm : lnu_last) - (mx + logf(sum));
   } else {
-    out[(long long)b * N1 + j] = ((ss[0][c] + ss[1][c]) + ss[2][c]) + ss[3][c];
+    float sum = 0.f;
+    for (int c = 0; c < nch; ++c) sum += p[2 * (long long)c * N1 + 1];
+    out[t] = sum;
   }
 }
 
@@ -376,6 +421,20 @@ __global__ void sg_nll_grad_kernel(const uint8_t* gta, const int64_t* gt0, const
 
 inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
+
+// column pass (pass 1 + pass 2); part: sk_col_part_floats
+size_t sk_col_part_floats(int B, int M, int N) { return 2 * (size_t)B * cdiv(M + 1, SK_CH) * (N + 1); }
+
+void sk_col(const float* Cc, int B, int M1, int N1, const float* u, const float* v, const float* vp, const float* gu,
+            const float* gv, float* gC, float norm, float lmu_last, float lnu_last, int mode, float* part, float* out,
+            hipStream_t st) {
+  const int nch = cdiv(M1, SK_CH);
+  hipLaunchKernelGGL(sk_col_part_kernel, dim3(cdiv(N1, 64), nch, B), dim3(256), 0, st, Cc, B, M1, N1, u, v, vp, gu, gv,
+                     gC, norm, lmu_last, lnu_last, mode, part);
+  hipLaunchKernelGGL(sk_col_final_kernel, dim3(cdiv((long long)B * N1, 256)), dim3(256), 0, st, part, B, N1, nch, norm,
+                     lnu_last, mode, out);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -388,11 +447,11 @@ hipError_t bn_train_fwd(const float* X, long long ldx, int rows, int C, const fl
   float *mean = stats, *rstd = stats + C, *varu = stats + 2 * C;
   hipLaunchKernelGGL(bn_part_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rows, C, 0, nullptr, nullptr, nullptr, nullptr,
                      nullptr, 0ll, part, nullptr);
-  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nullptr, nb, C, rows, 0, mean, nullptr,
+  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 16)), dim3(256), 0, st, part, nullptr, nb, C, rows, 0, mean, nullptr,
                      nullptr, nullptr, nullptr, nullptr, nullptr, 0);
   hipLaunchKernelGGL(bn_part_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rows, C, 1, mean, nullptr, nullptr, nullptr,
                      nullptr, 0ll, part, nullptr);
-  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nullptr, nb, C, rows, 1, nullptr, rstd,
+  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 16)), dim3(256), 0, st, part, nullptr, nb, C, rows, 1, nullptr, rstd,
                      varu, nullptr, nullptr, nullptr, nullptr, 0);
   hipLaunchKernelGGL(bn_apply_fwd_kernel, dim3(cdiv((long long)rows * (C / 4), 256)), dim3(256), 0, st, X, ldx, rows, C,
                      mean, rstd, gamma, beta, Y, ldy);
@@ -410,7 +469,7 @@ hipError_t bn_train_bwd(const float* X, long long ldx, const float* dY, long lon
   float* s01 = part + 2 * (size_t)nb * C;  // [2][C]: sum dy', sum dy' xhat
   hipLaunchKernelGGL(bn_part_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rows, C, 2, mean, rstd, gamma, beta, dY, ldy, p0,
                      p1);
-  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, p0, p1, nb, C, rows, 2, nullptr, nullptr,
+  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 16)), dim3(256), 0, st, p0, p1, nb, C, rows, 2, nullptr, nullptr,
                      nullptr, s01, s01 + C, dgamma, dbeta, accum);
   hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(cdiv((long long)rows * (C / 4), 256)), dim3(256), 0, st, X, ldx, dY, ldy,
                      rows, C, mean, rstd, gamma, beta, s01, s01 + C, dX, lddx);
@@ -435,8 +494,10 @@ hipError_t head_gather(const float* src, int rows, int cols, bool by_cols, bool 
   return hipGetLastError();
 }
 
+size_t sk_train_part_floats(int B, int M, int N) { return sk_col_part_floats(B, M, N); }
+
 hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M, int N, int iters, float* Cc, float* U,
-                            float* V, float* Z, hipStream_t st) {
+                            float* V, float* Z, float* part, hipStream_t st) {
   const int M1 = M + 1, N1 = N + 1;
   const float norm = -logf((float)(M + N)), lmu_last = logf((float)N) + norm, lnu_last = logf((float)M) + norm;
   const long long tot = (long long)B * M1 * N1;
@@ -449,8 +510,7 @@ hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M,
     float* v = V + (size_t)t * B * N1;
     hipLaunchKernelGGL(sk_row_kernel, dim3(cdiv((long long)B * M1, 4)), dim3(256), 0, st, Cc, B, M1, N1, nullptr, vprev,
                        nullptr, nullptr, norm, lmu_last, lnu_last, 0, u);
-    hipLaunchKernelGGL(sk_col_kernel, dim3(cdiv(N1, 64), B), dim3(256), 0, st, Cc, B, M1, N1, u, nullptr, nullptr, nullptr,
-                       nullptr, nullptr, norm, lmu_last, lnu_last, 0, v);
+    sk_col(Cc, B, M1, N1, u, nullptr, nullptr, nullptr, nullptr, nullptr, norm, lmu_last, lnu_last, 0, part, v, st);
   }
   const float* uT = iters > 0 ? U + (size_t)(iters - 1) * B * M1 : nullptr;
   if (!uT) {  // no iterations: u = v = 0
@@ -464,7 +524,7 @@ hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M,
 }
 
 size_t sk_train_scratch_floats(int B, int M, int N) {
-  return (size_t)B * (M + 1) * (N + 1) + 4 * (size_t)B * (M + N + 2) + B + 64;
+  return (size_t)B * (M + 1) * (N + 1) + 4 * (size_t)B * (M + N + 2) + B + sk_col_part_floats(B, M, N) + 256;
 }
 
 hipError_t sk_train_backward(const float* Cc, const float* U, const float* V, const float* gZ, const float* gext, int B,
@@ -478,13 +538,13 @@ hipError_t sk_train_backward(const float* Cc, const float* U, const float* V, co
   float* gv = gu + (size_t)B * M1;          // [B][N1]: d/d v_t
   float* gv2 = gv + (size_t)B * N1;         // [B][N1]: d/d v_{t-1}
   float* part = gv2 + (size_t)B * N1;       // [B]
+  float* cpart = part + B + 64;              // column-pass partials
   hipError_t e = hipMemcpyAsync(gC, gZ, tot * sizeof(float), hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return e;
   // Z = C + u_T + v_T - norm: d/d u_T = row sums of gZ, d/d v_T = column sums
   hipLaunchKernelGGL(sk_row_kernel, dim3(cdiv((long long)B * M1, 4)), dim3(256), 0, st, gZ, B, M1, N1, nullptr, nullptr,
                      nullptr, nullptr, norm, lmu_last, lnu_last, 2, base);
-  hipLaunchKernelGGL(sk_col_kernel, dim3(cdiv(N1, 64), B), dim3(256), 0, st, gZ, B, M1, N1, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, norm, lmu_last, lnu_last, 2, gv);
+  sk_col(gZ, B, M1, N1, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, norm, lmu_last, lnu_last, 2, cpart, gv, st);
   for (int t = iters; t >= 1; --t) {
     const float* u = U + (size_t)(t - 1) * B * M1;
     const float* v = V + (size_t)t * B * N1;
@@ -493,8 +553,7 @@ hipError_t sk_train_backward(const float* Cc, const float* U, const float* V, co
     hipLaunchKernelGGL(sk_row_kernel, dim3(cdiv((long long)B * M1, 4)), dim3(256), 0, st, Cc, B, M1, N1, u, v, gv,
                        t == iters ? base : nullptr, norm, lmu_last, lnu_last, 1, gu);
     // u_t = lmu - LSE_j(C + v_{t-1}): d/d v_{t-1}, and both steps' d/d C
-    hipLaunchKernelGGL(sk_col_kernel, dim3(cdiv(N1, 64), B), dim3(256), 0, st, Cc, B, M1, N1, u, v, vp, gu, gv, gC, norm,
-                       lmu_last, lnu_last, 1, gv2);
+    sk_col(Cc, B, M1, N1, u, v, vp, gu, gv, gC, norm, lmu_last, lnu_last, 1, cpart, gv2, st);
     std::swap(gv, gv2);
   }
   const long long per = (long long)M * N;

@@ -154,8 +154,10 @@ hipError_t kenc_input(const float* kpts, const float* scores, const float* size,
 hipError_t head_gather(const float* src, int rows, int cols, bool by_cols, bool inverse, float* dst, hipStream_t st);
 // log_optimal_transport (:181-201) keeping every iterate: Cc [B][M+1][N+1] couplings, U [iters][B][M+1]
 // (u_1..u_T), V [iters+1][B][N+1] (v_0 = 0 .. v_T), Z (already + log(M+N)).  alpha: device scalar.
+// part: sk_train_part_floats (column-pass partials)
+size_t sk_train_part_floats(int B, int M, int N);
 hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M, int N, int iters, float* Cc, float* U,
-                            float* V, float* Z, hipStream_t st);
+                            float* V, float* Z, float* part, hipStream_t st);
 // its backward: d/d cost [B][M][N] (= inner block of d/d Cc, + gext when non-null) and d/d alpha
 // (scalar, overwritten; nullable) from gZ.  ws: sk_train_scratch_floats.
 size_t sk_train_scratch_floats(int B, int M, int N);

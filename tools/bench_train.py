@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
-"""One timed LightGlue TRAINING step on one MI355X (reference gluefactory/train.py:430-470:
-forward in training mode, LightGlue.loss, torch.mean(total), backward, optimizer step).
+"""One timed TRAINING step on one MI355X (reference gluefactory/train.py:430-470: forward in
+training mode, model.loss, torch.mean(total), backward, optimizer step) -- LightGlue (default) or
+SuperGlue (``--model superglue``: the 18-layer GNN, 50 Sinkhorn iterations, SuperGlue.loss).
 
 Default shape = BASELINE configs[2] (N = 2048 keypoints, 9 layers, 32 pairs per step), synthetic
 inputs (SURVEY §8d recipe) and a seeded one-to-one ground truth, random-init weights of the
 reference architecture.  Prints one JSON line: ms per step (forward / loss / backward / optimizer
 split from HIP events), pairs/s, peak memory, and the algorithmic TFLOP/s of the step.
 
-    python tools/bench_train.py [--batch 32] [--npts 2048] [--steps 5] [--warmup 2]
+    python tools/bench_train.py [--model lightglue|superglue] [--batch 32] [--npts 2048] [--steps 5] [--warmup 2]
 """
 import argparse
 import json
@@ -36,8 +37,19 @@ def step_flops(B, N, L, d=256):
     return B * (3 * lin + att + fwd_head + bwd_head)
 
 
+def sg_step_flops(B, N, L=18, T=50, d=256):
+    """SuperGlue: per layer and image set q/k/v/merge (4 N d^2 x 2) + mlp (2 N (2d)^2 + 2 N 2d d)
+    forward, 3x for fwd + bwd; attention 4 N^2 d fwd + 10 N^2 d bwd per image; final_proj + cost;
+    the Sinkhorn's exp work is not counted (memory-bound)."""
+    lin = L * 2 * (2 * 4 * N * d * d + 2 * N * 4 * d * d + 2 * N * 2 * d * d)
+    att = L * 2 * 14 * N * N * d
+    head = 3 * (2 * 2 * N * d * d + 2 * N * N * d)
+    return B * (3 * lin + att + head)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--model", choices=["lightglue", "superglue"], default="lightglue")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--npts", type=int, default=2048)
     ap.add_argument("--layers", type=int, default=9)
@@ -53,11 +65,23 @@ def main():
 
     dev = torch.device("cuda", 0)
     B, N, L = a.batch, a.npts, a.layers
-    conf = {"filter_threshold": 0.1, "n_layers": L}
-    model = LightGlue(conf).to(dev)
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(conf, seed=0).items()})
+    if a.model == "lightglue":
+        conf = {"filter_threshold": 0.1, "n_layers": L}
+        model = LightGlue(conf).to(dev)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(conf, seed=0).items()})
+    else:
+        from lightglue_amd import SuperGlue
+        from lightglue_amd.sg_weights import superglue_state_dict, synthetic_scores
+
+        model = SuperGlue({}).to(dev)
+        full = model.state_dict()
+        full.update({k: torch.from_numpy(v) for k, v in superglue_state_dict({}, seed=0).items()})
+        model.load_state_dict(full)
     model.train()
     pair = synthetic_pair(B=B, M=N, seed=1)
+    if a.model == "superglue":
+        pair["keypoint_scores0"] = synthetic_scores(B, N, seed=2)
+        pair["keypoint_scores1"] = synthetic_scores(B, N, seed=3)
     gt = ground_truth(B, N, N, 7)
     data = {k: torch.from_numpy(v).to(dev) for k, v in pair.items() if not k.startswith("image_size")}
     data["view0"] = {"image_size": torch.from_numpy(pair["image_size0"]).to(dev)}
@@ -72,7 +96,8 @@ def main():
         opt.zero_grad(set_to_none=True)
         pred = model(data)
         e[1].record()
-        losses, _ = model.loss(pred, data)
+        losses = model.loss(pred, data)
+        losses = losses[0] if isinstance(losses, tuple) else losses
         loss = torch.mean(losses["total"])
         e[2].record()
         loss.backward()
@@ -98,9 +123,9 @@ def main():
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1) / a.steps
     split = np.mean([[e[i].elapsed_time(e[i + 1]) for i in range(4)] for e in times], axis=0)
-    fl = step_flops(B, N, L)
+    fl = step_flops(B, N, L) if a.model == "lightglue" else sg_step_flops(B, N)
     out = {
-        "metric": "training step (forward + LightGlue.loss + backward + Adam)",
+        "metric": f"training step (forward + {'LightGlue' if a.model == 'lightglue' else 'SuperGlue'}.loss + backward + Adam)",
         "ms_per_step": round(ms, 2),
         "pairs_per_s": round(B * 1000.0 / ms, 2),
         "split_ms": {"forward": round(float(split[0]), 2), "loss": round(float(split[1]), 2),
@@ -109,7 +134,9 @@ def main():
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
         "loss": float(loss.detach()),
         "dtype": "f32 (f32-input MFMA)",
-        "config": {"workload": f"configs[2] shape: N={N}, {L} layers, {B} pairs per step", "data": "synthetic"},
+        "config": {"workload": (f"configs[2] shape: N={N}, {L} layers, {B} pairs per step" if a.model == "lightglue"
+                                else f"SuperGlue outdoor architecture (18 GNN layers, 50 Sinkhorn iterations), N={N}, "
+                                     f"{B} pairs per step"), "data": "synthetic"},
     }
     print(json.dumps(out), flush=True)
 

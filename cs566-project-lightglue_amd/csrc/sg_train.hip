@@ -202,14 +202,18 @@ __global__ void head_gather_kernel(const float* src, int rows, int cols, int by_
 
 // ---------------------------------------------------------------- Sinkhorn (training)
 // couplings [B][M+1][N+1]: the cost with the dustbin score alpha (:185-192)
-__global__ void sk_couplings_kernel(const float* cost, const float* alpha, int B, int M, int N, float* Cc) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long per = (long long)(M + 1) * (N + 1);
-  if (i >= per * B) return;
-  const int b = (int)(i / per);
-  const long long e = i - b * per;
-  const int r = (int)(e / (N + 1)), c = (int)(e - (long long)r * (N + 1));
-  Cc[i] = (r < M && c < N) ? cost[((long long)b * M + r) * N + c] : alpha[0];
+__global__ __launch_bounds__(256) void sk_couplings_kernel(const float* cost, const float* alpha, int B, int M, int N,
+                                                           float* Cc) {
+  const int row = blockIdx.x, b = row / (M + 1), i = row - b * (M + 1);  // one workgroup per row
+  float* out = Cc + (long long)row * (N + 1);
+  const float a = alpha[0];
+  if (i < M) {
+    const float* c = cost + ((long long)b * M + i) * N;
+    for (int j = threadIdx.x; j < N; j += 256) out[j] = c[j];
+    if (threadIdx.x == 0) out[N] = a;
+  } else {
+    for (int j = threadIdx.x; j <= N; j += 256) out[j] = a;
+  }
 }
 
 // online logsumexp of one lane's stream, then a wave reduction
@@ -341,15 +345,15 @@ __global__ void sk_col_final_kernel(const float* part, int B, int N1, int nch, f
   }
 }
 
-// Z = C + u_i + v_j - norm (:178,200)
-__global__ void sk_out_kernel(const float* Cc, const float* u, const float* v, int B, int M1, int N1, float norm, float* Z) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long per = (long long)M1 * N1;
-  if (i >= per * B) return;
-  const int b = (int)(i / per);
-  const long long e = i - b * per;
-  const int r = (int)(e / N1), c = (int)(e - (long long)r * N1);
-  Z[i] = Cc[i] + u[(long long)b * M1 + r] + v[(long long)b * N1 + c] - norm;
+// Z = C + u_i + v_j - norm (:178,200), one workgroup per row
+__global__ __launch_bounds__(256) void sk_out_kernel(const float* Cc, const float* u, const float* v, int B, int M1, int N1,
+                                                     float norm, float* Z) {
+  const int row = blockIdx.x, b = row / M1;
+  const float ui = u[row];
+  const float* vb = v + (long long)b * N1;
+  const float* c = Cc + (long long)row * N1;
+  float* z = Z + (long long)row * N1;
+  for (int j = threadIdx.x; j < N1; j += 256) z[j] = c[j] + ui + vb[j] - norm;
 }
 
 // d/d cost = gC's inner block (+ gext); part[b] = sum of gC over pair b's dustbin entries
@@ -393,30 +397,26 @@ __global__ void sk_alpha_kernel(const float* part, int B, float* galpha) {
 // out [5][B] (num_matchable, num_unmatchable).  Linear in la: gLA = -(c_in * positive) on the
 // inner block, -(c_dust * negative) on the dustbins (NLLLoss: the column dustbin written at
 // [:, -1, :m], losses.py:72), 0 elsewhere.
-__global__ void sg_nll_grad_kernel(const uint8_t* gta, const int64_t* gt0, const int64_t* gt1, const float* stats,
-                                   const float* g_nll, const float* g_pos, const float* g_neg, int B, int M, int N,
-                                   int mode, float bal, float* gla) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long M1 = M + 1, N1 = N + 1, per = M1 * N1;
-  if (i >= per * B) return;
-  const int b = (int)(i / per);
-  const long long e = i - b * per;
-  const int r = (int)(e / N1), c = (int)(e - (long long)r * N1);
+__global__ __launch_bounds__(256) void sg_nll_grad_kernel(const uint8_t* gta, const int64_t* gt0, const int64_t* gt1,
+                                                          const float* stats, const float* g_nll, const float* g_pos,
+                                                          const float* g_neg, int B, int M, int N, int mode, float bal,
+                                                          float* gla) {
+  const int row = blockIdx.x, b = row / (M + 1), r = row - b * (M + 1);  // one workgroup per row
   const float gn = g_nll ? g_nll[b] : 0.f;
   const float num_pos = stats[3 * B + b];
   const float num_neg = mode == 0 ? stats[4 * B + b] : 2.f * stats[4 * B + b];
   const float c_in = (bal * gn + (g_pos ? g_pos[b] : 0.f)) / num_pos;
   const float c_dust = ((1.f - bal) * gn + (g_neg ? g_neg[b] : 0.f)) / num_neg;
-  float w = 0.f;
-  if (r < M && c < N) {
-    w = gta[((long long)b * M + r) * N + c] ? c_in : 0.f;
-  } else if (r < M && c == N) {
-    w = gt0[(long long)b * M + r] == -1 ? c_dust : 0.f;
-  } else if (r == M && c < N) {
+  float* out = gla + (long long)row * (N + 1);
+  if (r < M) {
+    const uint8_t* a = gta + ((long long)b * M + r) * N;
+    for (int c = threadIdx.x; c < N; c += 256) out[c] = a[c] ? -c_in : -0.f;
+    if (threadIdx.x == 0) out[N] = gt0[(long long)b * M + r] == -1 ? -c_dust : -0.f;
+  } else {
     // NLLLoss writes the column dustbins at [:, -1, :m] from gt_matches1 (M == N there)
-    w = gt1[(long long)b * N + c] == -1 ? c_dust : 0.f;
+    for (int c = threadIdx.x; c < N; c += 256) out[c] = gt1[(long long)b * N + c] == -1 ? -c_dust : -0.f;
+    if (threadIdx.x == 0) out[N] = -0.f;
   }
-  gla[i] = -w;
 }
 
 inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
@@ -500,8 +500,7 @@ hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M,
                             float* V, float* Z, float* part, hipStream_t st) {
   const int M1 = M + 1, N1 = N + 1;
   const float norm = -logf((float)(M + N)), lmu_last = logf((float)N) + norm, lnu_last = logf((float)M) + norm;
-  const long long tot = (long long)B * M1 * N1;
-  hipLaunchKernelGGL(sk_couplings_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, st, cost, alpha, B, M, N, Cc);
+    hipLaunchKernelGGL(sk_couplings_kernel, dim3(B * M1), dim3(256), 0, st, cost, alpha, B, M, N, Cc);
   hipError_t e = hipMemsetAsync(V, 0, (size_t)B * N1 * sizeof(float), st);  // v_0 = 0 (:175)
   if (e != hipSuccess) return e;
   for (int t = 1; t <= iters; ++t) {
@@ -518,8 +517,8 @@ hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M,
     if (e != hipSuccess) return e;
     uT = U;
   }
-  hipLaunchKernelGGL(sk_out_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, st, Cc, uT, V + (size_t)iters * B * N1, B, M1, N1,
-                     norm, Z);
+  hipLaunchKernelGGL(sk_out_kernel, dim3(B * M1), dim3(256), 0, st, Cc, uT, V + (size_t)iters * B * N1, B, M1, N1, norm,
+                     Z);
   return hipGetLastError();
 }
 
@@ -567,8 +566,9 @@ hipError_t sg_nll_grad(const uint8_t* gta, const int64_t* gt0, const int64_t* gt
                        const float* g_pos, const float* g_neg, int B, int M, int N, int mode, float bal, float* gla,
                        hipStream_t st) {
   const long long tot = (long long)B * (M + 1) * (N + 1);
-  hipLaunchKernelGGL(sg_nll_grad_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, st, gta, gt0, gt1, stats, g_nll, g_pos, g_neg,
-                     B, M, N, mode, bal, gla);
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(sg_nll_grad_kernel, dim3(B * (M + 1)), dim3(256), 0, st, gta, gt0, gt1, stats, g_nll, g_pos, g_neg, B,
+                     M, N, mode, bal, gla);
   return hipGetLastError();
 }
 

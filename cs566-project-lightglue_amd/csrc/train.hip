@@ -883,22 +883,24 @@ __global__ __launch_bounds__(256) void la_col_final_kernel(const float* part, in
   gd1[(long long)b * N + j] = T[(long long)b * (M + 1) * (N + 1) + (long long)M * (N + 1) + j] * (s_dust ? s_dust[b] : 1.f);
 }
 
+// one workgroup per similarity row (b, i): per-row values loaded once, the row swept by 256 lanes
 __global__ __launch_bounds__(256) void la_grad_sim_kernel(float* sim, const float* T, const float* s_in,
                                                           const float* lser, const float* lsec, const float* rs,
                                                           const float* cs, const float* gext, int B, int M, int N) {
-  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long MN = (long long)M * N;
-  if (id >= MN * B) return;
-  const int b = (int)(id / MN);
-  const long long e = id - b * MN;
-  const int i = (int)(e / N), j = (int)(e - (long long)i * N);
-  const float g = T[((long long)b * (M + 1) + i) * (N + 1) + j] * (s_in ? s_in[b] : 1.f);
-  const float s = sim[id];
-  const long long ri = (long long)b * M + i, cj = (long long)b * N + j;
-  // la = s - lse_row + s - lse_col + ...  (lightglue.py:288-293)
-  float v = 2.f * g - expf(s - lser[ri]) * rs[ri] - expf(s - lsec[cj]) * cs[cj];
-  if (gext) v += gext[id];
-  sim[id] = v;
+  const int row = blockIdx.x, b = row / M, i = row - b * M;
+  const float sc = s_in ? s_in[b] : 1.f, lr = lser[row], r = rs[row];
+  const float* t = T + ((long long)b * (M + 1) + i) * (N + 1);
+  const float* lc = lsec + (long long)b * N;
+  const float* c = cs + (long long)b * N;
+  float* s = sim + (long long)row * N;
+  const float* ge = gext ? gext + (long long)row * N : nullptr;
+  for (int j = threadIdx.x; j < N; j += 256) {
+    const float g = t[j] * sc, x = s[j];
+    // la = s - lse_row + s - lse_col + ...  (lightglue.py:288-293)
+    float v = 2.f * g - expf(x - lr) * r - expf(x - lc[j]) * c[j];
+    if (ge) v += ge[j];
+    s[j] = v;
+  }
 }
 
 // sigmoid_log_double_softmax (lightglue.py:284-296) from sim [B][M][N], its row / column
@@ -906,25 +908,24 @@ __global__ __launch_bounds__(256) void la_grad_sim_kernel(float* sim, const floa
 __global__ __launch_bounds__(256) void la_forward_kernel(const float* sim, const float* lser, const float* lsec,
                                                          const float* z0, const float* z1, int B, int M, int N,
                                                          float* la) {
-  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long per = (long long)(M + 1) * (N + 1);
-  if (id >= per * B) return;
-  const int b = (int)(id / per);
-  const long long e = id - b * per;
-  const int i = (int)(e / (N + 1)), j = (int)(e - (long long)i * (N + 1));
-  float v;
-  if (i < M && j < N) {
-    const float s = sim[((long long)b * M + i) * N + j];
-    const float cert = log_sigmoid(z0[(long long)b * M + i]) + log_sigmoid(z1[(long long)b * N + j]);
-    v = ((s - lser[(long long)b * M + i]) + (s - lsec[(long long)b * N + j])) + cert;
-  } else if (i < M) {
-    v = log_sigmoid(-z0[(long long)b * M + i]);
-  } else if (j < N) {
-    v = log_sigmoid(-z1[(long long)b * N + j]);
+  const int row = blockIdx.x, b = row / (M + 1), i = row - b * (M + 1);  // one workgroup per la row
+  float* out = la + (long long)row * (N + 1);
+  const float* zb = z1 + (long long)b * N;
+  if (i < M) {
+    const long long ri = (long long)b * M + i;
+    const float* s = sim + ri * N;
+    const float* lc = lsec + (long long)b * N;
+    const float lr = lser[ri], l0 = log_sigmoid(z0[ri]);
+    for (int j = threadIdx.x; j < N; j += 256) {
+      const float x = s[j];
+      const float cert = l0 + log_sigmoid(zb[j]);
+      out[j] = ((x - lr) + (x - lc[j])) + cert;
+    }
+    if (threadIdx.x == 0) out[N] = log_sigmoid(-z0[ri]);
   } else {
-    v = 0.f;
+    for (int j = threadIdx.x; j < N; j += 256) out[j] = log_sigmoid(-zb[j]);
+    if (threadIdx.x == 0) out[N] = 0.f;
   }
-  la[id] = v;
 }
 
 // d/dz of logsigmoid(z) (inner entries, summed: rs) and logsigmoid(-z) (the dustbin entry gd)
@@ -1184,8 +1185,8 @@ hipError_t la_grad_sim(float* sim, const float* T, const float* s_in, const floa
                        const float* rs, const float* cs, const float* gsim_ext, int B, int M, int N, hipStream_t st) {
   const long long n = (long long)B * M * N;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(la_grad_sim_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, sim, T, s_in, lser, lsec, rs, cs, gsim_ext,
-                     B, M, N);
+  hipLaunchKernelGGL(la_grad_sim_kernel, dim3(B * M), dim3(256), 0, st, sim, T, s_in, lser, lsec, rs, cs, gsim_ext, B, M,
+                     N);
   return hipGetLastError();
 }
 
@@ -1193,7 +1194,7 @@ hipError_t la_forward(const float* sim, const float* lser, const float* lsec, co
                       int N, float* la, hipStream_t st) {
   const long long n = (long long)B * (M + 1) * (N + 1);
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(la_forward_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, sim, lser, lsec, z0, z1, B, M, N, la);
+  hipLaunchKernelGGL(la_forward_kernel, dim3(B * (M + 1)), dim3(256), 0, st, sim, lser, lsec, z0, z1, B, M, N, la);
   return hipGetLastError();
 }
 

@@ -216,15 +216,7 @@ __global__ __launch_bounds__(256) void sk_couplings_kernel(const float* cost, co
   }
 }
 
-// online logsumexp of one lane's stream, then a wave reduction
-__device__ __forceinline__ void lse_push(float x, float& m, float& s) {
-  if (x > m) {
-    s = s * expf(m - x) + 1.f;  // s == 0 while m == -inf
-    m = x;
-  } else {
-    s += expf(x - m);
-  }
-}
+// (max, sum exp(x - max)) of a lane, reduced over the wave
 __device__ __forceinline__ float lse_wave(float m, float s) {
   const float mx = wave_max(m);
   const float t = mx == -INFINITY ? 0.f : s * expf(m - mx);
@@ -243,8 +235,25 @@ __global__ __launch_bounds__(256) void sk_row_kernel(const float* Cc, int B, int
   const float* c = Cc + (long long)row * N1;
   const float* vb = v ? v + (long long)b * N1 : nullptr;
   if (mode == 0) {
+    // chunks of 8 values per lane: the chunk max first, then one exponential per value
     float m = -INFINITY, s = 0.f;
-    for (int j = l; j < N1; j += 64) lse_push(c[j] + vb[j], m, s);
+    for (int j0 = 0; j0 < N1; j0 += 512) {
+      float x[8];
+      float cm = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int j = j0 + l + 64 * q;
+        x[q] = j < N1 ? c[j] + vb[j] : -INFINITY;
+        cm = fmaxf(cm, x[q]);
+      }
+      if (cm == -INFINITY) continue;
+      const float mn = fmaxf(m, cm);
+      float t = s * expf(m - mn);  // s == 0 while m == -inf
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += expf(x[q] - mn);
+      m = mn;
+      s = t;
+    }
     const float lse = lse_wave(m, s);
     if (l == 0) out[row] = (i < M1 - 1 ? norm : lmu_last) - lse;
     return;
@@ -284,7 +293,23 @@ __global__ __launch_bounds__(256) void sk_col_part_kernel(const float* Cc, int B
   if (ok) {
     if (mode == 0) {
       const float* ub = u + (long long)b * M1;
-      for (int i = i0 + grp; i < i1; i += 4) lse_push(Cc[base + (long long)i * N1 + j] + ub[i], m, s);
+      for (int i = i0 + grp; i < i1; i += 32) {  // chunks of 8 rows per thread
+        float x[8];
+        float cm = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = i + 4 * q;
+          x[q] = r < i1 ? Cc[base + (long long)r * N1 + j] + ub[r] : -INFINITY;
+          cm = fmaxf(cm, x[q]);
+        }
+        if (cm == -INFINITY) continue;
+        const float mn = fmaxf(m, cm);
+        float t = s * expf(m - mn);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t += expf(x[q] - mn);
+        m = mn;
+        s = t;
+      }
     } else if (mode == 1) {
       const float* ub = u + (long long)b * M1;
       const float* gub = gu + (long long)b * M1;

@@ -180,26 +180,27 @@ struct Ctx {
   float* ws;
   size_t ws_floats;
   float* part;
+  bool x6 = true;  // the trunk's linears may take the bf16x6 GEMM; the heads stay on f32 MFMA
 };
 
 // y[M,N] = alpha (x[M,K] W[N,K]^T + b) + beta y
 hipError_t linear(const Ctx& c, const float* x, long long ldx, int rows, int K, const float* W, const float* b, int N,
                   float* y, long long ldy, float beta = 0.f, float alpha = 1.f) {
   TGemm g{x, W, y, ldx, K, ldy, 0, 0, 0, rows, N, K, 1, alpha, beta, b};
-  return tgemm(g, false, true, c.ws, c.ws_floats, c.st);
+  return tgemm(g, false, true, c.ws, c.ws_floats, c.st, c.x6);
 }
 // dx[M,K] (+)= dy[M,N] W[N,K]
 hipError_t linear_dgrad(const Ctx& c, const float* dy, long long lddy, int rows, int N, const float* W, int K, float* dx,
                         long long lddx, float beta = 0.f) {
   TGemm g{dy, W, dx, lddy, K, lddx, 0, 0, 0, rows, K, N, 1, 1.f, beta, nullptr};
-  return tgemm(g, false, false, c.ws, c.ws_floats, c.st);
+  return tgemm(g, false, false, c.ws, c.ws_floats, c.st, c.x6);
 }
 // dW[N,K] = dy[rows,N]^T x[rows,K]; db[N] = colsum(dy)
 hipError_t linear_wgrad(const Ctx& c, const float* dy, long long lddy, const float* x, long long ldx, int rows, int N,
                         int K, float* dW, float* db) {
   if (dW) {
     TGemm g{dy, x, dW, lddy, ldx, K, 0, 0, 0, N, K, rows, 1, 1.f, 0.f, nullptr};
-    hipError_t e = tgemm(g, true, false, c.ws, c.ws_floats, c.st);
+    hipError_t e = tgemm(g, true, false, c.ws, c.ws_floats, c.st, c.x6);
     if (e != hipSuccess) return e;
   }
   if (db) return colsum(dy, lddy, rows, N, nullptr, c.part, db, c.st);
@@ -525,7 +526,7 @@ int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, 
   HeadScratch s = carve_head_scratch((char*)scratch, B, M, N);
   if (scratch_bytes < s.bytes) return fail(LG_E_WORKSPACE, "scratch too small: need " + std::to_string(s.bytes));
   TR_HIP(hipSetDevice(handle_device(h)));
-  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART};
+  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART, false};
   const Params P{h, params, grads};
   const std::string a = "log_assignment." + std::to_string(layer);
   const int R0 = B * M, R = B * (M + N);
@@ -539,7 +540,7 @@ int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, 
   TR_HIP(gemv256(s.X, R, wm, P.w(a + ".matchability.bias"), s.Z, c.st));
   {
     TGemm g{s.MD, s.MD + o1, s.SIM, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B, 1.f, 0.f, nullptr};
-    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st));
+    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st, c.x6));
   }
   TR_HIP(sim_lse(s.SIM, B, M, N, s.LSER, s.LSEC, c.part, c.st));
   // sigmoid_log_double_softmax backward (:284-296)
@@ -549,11 +550,11 @@ int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, 
   // d/d(final_proj output) = d/d(md) / 4: gmd0 = gsim md1, gmd1 = gsim^T md0
   {
     TGemm g{s.SIM, s.MD + o1, s.GMD, N, D, D, (long long)M * N, (long long)N * D, (long long)M * D, M, D, N, B, 0.25f, 0.f, nullptr};
-    TR_HIP(tgemm(g, false, false, c.ws, c.ws_floats, c.st));
+    TR_HIP(tgemm(g, false, false, c.ws, c.ws_floats, c.st, c.x6));
   }
   {
     TGemm g{s.SIM, s.MD, s.GMD + o1, N, D, D, (long long)M * N, (long long)M * D, (long long)N * D, N, D, M, B, 0.25f, 0.f, nullptr};
-    TR_HIP(tgemm(g, true, false, c.ws, c.ws_floats, c.st));
+    TR_HIP(tgemm(g, true, false, c.ws, c.ws_floats, c.st, c.x6));
   }
   TR_HIP(linear_wgrad(c, s.GMD, D, s.X, D, R, D, D, P.gr(a + ".final_proj.weight"), P.gr(a + ".final_proj.bias")));
   if (float* g = P.gr(a + ".matchability.weight")) TR_HIP(colsum(s.X, D, R, D, s.GZ, c.part, g, c.st));
@@ -592,7 +593,7 @@ int lg_head_forward(lg_handle_t* h, const float* const* params, int32_t layer, c
   HeadScratch s = carve_head_scratch((char*)scratch, B, M, N);
   if (scratch_bytes < s.bytes) return fail(LG_E_WORKSPACE, "scratch too small: need " + std::to_string(s.bytes));
   TR_HIP(hipSetDevice(handle_device(h)));
-  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART};
+  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART, false};
   const Params P{h, params, nullptr};
   const std::string a = "log_assignment." + std::to_string(layer);
   const int R0 = B * M, R = B * (M + N);
@@ -605,7 +606,7 @@ int lg_head_forward(lg_handle_t* h, const float* const* params, int32_t layer, c
   TR_HIP(gemv256(s.X, R, P.w(a + ".matchability.weight"), P.w(a + ".matchability.bias"), s.Z, c.st));
   {
     TGemm g{s.MD, s.MD + o1, sim, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B, 1.f, 0.f, nullptr};
-    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st));
+    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st, c.x6));
   }
   TR_HIP(sim_lse(sim, B, M, N, s.LSER, s.LSEC, c.part, c.st));
   TR_HIP(la_forward(sim, s.LSER, s.LSEC, s.Z, s.Z + R0, B, M, N, log_assignment, c.st));
@@ -620,7 +621,8 @@ int lg_head_forward(lg_handle_t* h, const float* const* params, int32_t layer, c
 // ------------------------------------------------------------------ kernel-level entries (tests)
 int lg_train_gemm_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t batch, size_t* bytes) {
   if (!bytes || M < 0 || N < 0 || K < 0 || batch < 0) return fail(LG_E_INVALID, "bad argument");
-  *bytes = tgemm_ws_floats(M, N, K, batch) * sizeof(float);
+  // split-k partials, or the transposed B of an input-gradient product (tgemm's bf16x6 route)
+  *bytes = std::max(tgemm_ws_floats(M, N, K, batch), (size_t)N * K + 4) * sizeof(float);
   return LG_OK;
 }
 

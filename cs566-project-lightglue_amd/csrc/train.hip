@@ -11,6 +11,7 @@
 #include <cmath>
 
 #include "common.h"
+#include "kernels.h"
 #include "train.h"
 
 namespace lg {
@@ -970,8 +971,68 @@ size_t tgemm_ws_floats(int M, int N, int K, int batch) {
   return ks > 1 ? (size_t)ks * M * N * batch : 0;
 }
 
-hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st) {
+#ifndef LG_TG_X6_FWD
+#define LG_TG_X6_FWD 0  // 1: forward products (ta = 0, tb = 1) too (moves the forward's rounding: see DESIGN §10c)
+#endif
+#ifndef LG_TG_X6
+#define LG_TG_X6 1  // route k-contiguous products to the bf16x6 GEMM (LG_TG_X6=0 at run time: f32 MFMA only)
+#endif
+static bool tg_x6_enabled() {
+  static const int v = [] {
+    const char* e = getenv("LG_TG_X6");
+    return e ? atoi(e) : LG_TG_X6;
+  }();
+  return v != 0;
+}
+
+// The products whose operands both run along k in memory -- a linear layer's forward
+// (ta = 0, tb = 1), and its input gradient (ta = 0, tb = 0) once the weight is transposed into
+// `ws` -- go to gemm.hip's bf16x6 kernel: both fp32 operands split into three bf16 pieces, six
+// v_mfma_f32_32x32x16_bf16 per 32 x 32 x 16 block (the fp32-accurate product of common.h at
+// 2.5 PF/s bf16 instead of the 157 TF/s f32 MFMA); error per product ~2^-24 like an f32 fma chain.
+static bool tgemm_x6(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st, hipError_t& err) {
+  if (!tg_x6_enabled() || ta || g.K < 16 || g.K % 16 || (g.beta != 0.f && g.beta != 1.f)) return false;
+  if (tb && !LG_TG_X6_FWD) return false;
+  auto al = [](const void* ptr, long long ld, long long sb) {
+    return ((uintptr_t)ptr % 16 == 0) && ld % 4 == 0 && sb % 4 == 0;
+  };
+  GemmArgs x{};
+  x.A0 = g.A;
+  x.lda0 = (int)g.lda;
+  x.K0 = g.K;
+  x.K = g.K;
+  x.bias = g.bias;
+  x.res = g.beta != 0.f ? g.C : nullptr;  // Y = C + (acc + bias) alpha
+  x.ldr = (int)g.ldc;
+  x.Y = g.C;
+  x.ldy = (int)g.ldc;
+  x.out_scale = g.alpha;
+  x.R = g.M;
+  x.Nout = g.N;
+  x.sA = g.sA;
+  x.sY = g.sC;
+  if (!al(g.A, g.lda, g.sA)) return false;
+  if (tb) {
+    if (!al(g.B, g.ldb, g.sB)) return false;
+    x.W = g.B;
+    x.ldw = (int)g.ldb;
+    x.sW = g.sB;
+  } else {
+    // B [K][N] -> B^T [N][K] in ws (a weight: small)
+    if (g.batch != 1 || g.ldb != g.N || !ws || ws_floats < (size_t)g.N * g.K + 4) return false;
+    err = sg_transpose(g.B, g.K, g.N, ws, st);
+    if (err != hipSuccess) return true;
+    x.W = ws;
+    x.ldw = g.K;
+  }
+  err = gemm_x6(x, EPI_STORE, g.batch, st);
+  return true;
+}
+
+hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st, bool x6) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return hipSuccess;
+  hipError_t xe = hipSuccess;
+  if (x6 && tgemm_x6(g, ta, tb, ws, ws_floats, st, xe)) return xe;
   TGemmK p{};
   p.g = g;
   int kc = 0;

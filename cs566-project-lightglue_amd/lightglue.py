@@ -15,8 +15,8 @@ Deliberate behaviour differences from the reference:
   raising ``UnboundLocalError`` (:452-455);
 * ``ref_descriptors*`` is ``[B, 1, M', 256]`` in eval mode and ``[B, L, M, 256]`` (every layer) in
   training mode, as the reference (:521-524,572); training mode also turns early stop and pruning
-  off (:502-503).  There is no autograd: a training-mode call with gradients enabled raises, and
-  :meth:`LightGlue.loss` returns forward values only.
+  off (:502-503).  The training path computes in fp32 whatever ``mp`` says (the reference's
+  autocast is not mirrored).
 * with pruning and B > 1, ``log_assignment`` and ``ref_descriptors*`` are per-pair LISTS (pair b's
   kept block; the reference asserts B == 1, :528,533); ``kept0/1`` and ``stop_layer`` give the
   per-pair counts.

@@ -25,6 +25,16 @@ is unchanged):
             LightGlue forward -> its final similarity -> log-domain Sinkhorn (superglue.py:173-201,
             50 iterations, dustbin score 1.0) -> mutual filter (superglue.py:288-298, threshold 0.2)
 
+Training steps (reference gluefactory/train.py:430-470) through the same launch:
+  train     LightGlue in training mode on the configs[2] shape (N=2048, 9 layers, 32 pairs per GPU):
+            forward, LightGlue.loss, torch.mean(total), backward, gradient all-reduce (RCCL, one
+            flat bucket, N > 1), Adam -- the hand-written HIP backward
+  train_sg  the same step for SuperGlue (outdoor architecture: 18 GNN layers, 50 Sinkhorn
+            iterations)
+  (seeded one-to-one ground truth from the synthetic pairs' own correspondence; their roofline
+  object is the whole step's algorithmic flops against the f32 MFMA peak, and their CPU baseline
+  the oracle's training step on one pair)
+
 Prints ONE JSON line on rank 0 with the metric, the attention kernel's roofline (in-library HIP
 events around every attention launch in the timed region; algorithmic flops per launch) and the
 CPU oracle's throughput on this host (rank 0, N=1 only, bounded sample).
@@ -182,7 +192,120 @@ WORKLOADS = {
     "configs4": (8, 4096, "configs[4]: N=4096 d=256, Sinkhorn assignment (50 iterations), 8 pairs per GPU "
                           "(batch 64 over 8 GPUs)"),
 }
+WORKLOADS["train"] = (32, 2048, "training step, configs[2] shape: LightGlue N=2048, 9 layers, 32 pairs per GPU "
+                               "(forward + LightGlue.loss + backward + Adam)")
+WORKLOADS["train_sg"] = (32, 2048, "training step: SuperGlue outdoor architecture (18 GNN layers, 50 Sinkhorn "
+                                   "iterations), N=2048, 32 pairs per GPU (forward + SuperGlue.loss + backward + Adam)")
 SINKHORN_ITERS, SINKHORN_ALPHA, SINKHORN_THRESHOLD = 50, 1.0, 0.2  # superglue.py:214-215, bin_score init 1.0
+
+
+def train_flops_per_pair(N, sg=False, d=256, L=9):
+    """Algorithmic flops of one training step per pair (forward + backward): linear layers 3x their
+    forward flops (y, dx, dW), attention 4 N^2 d forward + 10 N^2 d backward per softmax direction,
+    the assignment heads' products (LightGlue: every layer's head is evaluated by the loss)."""
+    if sg:
+        lin = 18 * 2 * (8 * N * d * d + 8 * N * d * d + 4 * N * d * d)
+        return 3 * lin + 18 * 2 * 14 * N * N * d + 3 * (4 * N * d * d + 2 * N * N * d)
+    lin = L * 76 * N * d * d
+    att = L * 28 * N * N * d
+    head = L * (4 * N * d * d + 2 * N * N * d)
+    bwd_head = L * (6 * N * N * d + 6 * N * d * d)
+    return 3 * lin + att + head + bwd_head
+
+
+def gpu_ground_truth(data, seed):
+    """One-to-one ground truth of gpu_pairs' correspondence (image-1 point j is image-0 point
+    perm[j], recovered from the keypoints), a third of each side left unmatched."""
+    k0, k1 = data["keypoints0"], data["keypoints1"]
+    B, M = k0.shape[:2]
+    dev = k0.device
+    near = torch.cdist(k1, k0).argmin(-1)  # [B, N] -> image-0 index
+    g = torch.Generator(device=dev).manual_seed(seed)
+    keep = torch.rand((B, k1.shape[1]), generator=g, device=dev) < 0.67
+    m1 = torch.where(keep, near, torch.full_like(near, -1))
+    m0 = torch.full((B, M), -1, dtype=torch.int64, device=dev)
+    bi, ji = torch.nonzero(m1 > -1, as_tuple=True)
+    m0[bi, m1[bi, ji]] = ji
+    m1 = torch.full_like(m1, -1)  # keep the pairs one-to-one after collisions
+    bi, ii = torch.nonzero(m0 > -1, as_tuple=True)
+    m1[bi, m0[bi, ii]] = ii
+    a = torch.zeros((B, M, k1.shape[1]), dtype=torch.bool, device=dev)
+    a[bi, ii, m0[bi, ii]] = True
+    return {"gt_matches0": m0, "gt_matches1": m1, "gt_assignment": a}
+
+
+def cpu_baseline_train(npts, budget_s, sg):
+    """The CPU oracle's training step (torch-CPU restatement of the reference forward in training
+    mode + its loss, differentiated by torch autograd in fp32) on one pair, on this host's cores:
+    one warm-up step, then timed steps until `budget_s` (at least one)."""
+    from lightglue_amd.weights import synthetic_pair
+
+    torch.set_num_threads(cpu_threads())
+    pair = synthetic_pair(B=1, M=npts, seed=1)
+    k0, k1 = pair["keypoints0"], pair["keypoints1"]
+    d2 = ((k1[0][:, None, :] - k0[0][None, :, :]) ** 2).sum(-1)
+    near = d2.argmin(-1)
+    m1 = np.where(np.arange(npts) % 3 != 0, near, -1)[None]
+    m0 = -np.ones((1, npts), np.int64)
+    for j, i in enumerate(m1[0]):
+        if i >= 0:
+            m0[0, i] = j
+    m1 = -np.ones((1, npts), np.int64)
+    for i, j in enumerate(m0[0]):
+        if j >= 0:
+            m1[0, j] = i
+    a = np.zeros((1, npts, npts), bool)
+    for i, j in enumerate(m0[0]):
+        if j >= 0:
+            a[0, i, j] = True
+    gt = {"gt_matches0": m0, "gt_matches1": m1, "gt_assignment": a}
+    if sg:
+        from oracle.superglue_train_ref import sg_train_forward, sg_train_loss
+        from lightglue_amd.sg_weights import superglue_state_dict, synthetic_scores
+
+        sd = superglue_state_dict({}, seed=0)
+
+        def one():
+            W = {k: torch.from_numpy(np.asarray(v).copy()).float().requires_grad_(
+                not k.endswith(("running_mean", "running_var"))) for k, v in sd.items()
+                 if not k.endswith("num_batches_tracked")}
+            data = {"keypoints0": torch.from_numpy(k0), "keypoints1": torch.from_numpy(k1),
+                    "descriptors0": torch.from_numpy(pair["descriptors0"]),
+                    "descriptors1": torch.from_numpy(pair["descriptors1"]),
+                    "keypoint_scores0": synthetic_scores(1, npts, seed=2), "keypoint_scores1": synthetic_scores(1, npts, seed=3),
+                    "image_size": pair["image_size0"]}
+            la, _, _, _ = sg_train_forward(W, data, {})
+            loss, _ = sg_train_loss(la, {k: torch.from_numpy(v) for k, v in gt.items()})
+            loss.backward()
+        what = "oracle/superglue_train_ref.py (18 GNN layers, 50 Sinkhorn iterations)"
+    else:
+        from oracle.lightglue_train_ref import train_loss
+
+        conf = {"filter_threshold": 0.1}
+        sd = synthetic_state_dict(conf, seed=0)
+
+        def one():
+            W = {k: torch.from_numpy(np.asarray(v).copy()).float().requires_grad_() for k, v in sd.items()}
+            data = {k: torch.from_numpy(v) for k, v in pair.items()}
+            loss, _ = train_loss(W, data, gt, conf, torch.float32)
+            loss.backward()
+        what = "oracle/lightglue_train_ref.py (9 layers, LightGlue.loss over every layer's head)"
+    one()  # warm-up
+    times, t_start = [], time.perf_counter()
+    while not times or (time.perf_counter() - t_start) < budget_s:
+        t0 = time.perf_counter()
+        one()
+        times.append((time.perf_counter() - t0) * 1e3)
+    t = np.array(times)
+    return {
+        "value": 1000.0 / t.mean(),
+        "unit": "image-pairs/s",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "mean_ms": round(float(t.mean()), 2),
+        "sample": f"1 warm-up + {len(t)} timed training steps (forward + loss + autograd backward, fp32) of 1 pair "
+                  f"x N={npts}, torch-CPU {what}, {torch.get_num_threads()} threads",
+    }
 
 
 def parse_args(argv=None):
@@ -247,6 +370,8 @@ def run(args):
 
     B, N = args.batch, args.npts
     wl = args.workload
+    if wl in ("train", "train_sg"):
+        return run_train(args, world, rank, local, distributed)
     conf = {"filter_threshold": 0.1}
     if wl == "configs3":
         conf.update(width_confidence=0.95, depth_confidence=0.95)
@@ -419,6 +544,113 @@ def run(args):
         result["config"]["pruning"] = "width 0.95, depth 0.95 (weights: weights.prune_recipe_state_dict)"
     if rank == 0 and world == 1 and args.cpu_budget > 0 and wl == "configs2":
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+def run_train(args, world, rank, local, distributed):
+    """--workload train / train_sg: one data-parallel training step per timed step (train.py:430-470)."""
+    if args.selftest_cpu:
+        raise SystemExit("bench.py: the training workloads need the HIP library (no CPU self-test)")
+    B, N, sg = args.batch, args.npts, args.workload == "train_sg"
+    device = torch.device("cuda", local)
+    if sg:
+        from lightglue_amd import SuperGlue
+        from lightglue_amd.sg_weights import superglue_state_dict
+
+        model = SuperGlue({}).to(device)
+        full = model.state_dict()
+        full.update({k: torch.from_numpy(v) for k, v in superglue_state_dict({}, seed=0).items()})
+        model.load_state_dict(full, strict=True)
+    else:
+        from lightglue_amd import LightGlue
+
+        conf = {"filter_threshold": 0.1}
+        model = LightGlue(conf).to(device)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(conf, seed=0).items()}, strict=True)
+    model.train()
+    # this rank's B pairs (its shard of the global batch: every rank draws its own seeded pairs)
+    data = gpu_pairs(B, N, 256, seed=1 + rank, device=device)
+    data.update(gpu_ground_truth(data, seed=7 + rank))
+    if sg:
+        g = torch.Generator(device=device).manual_seed(11 + rank)
+        data["keypoint_scores0"] = torch.rand((B, N), generator=g, device=device)
+        data["keypoint_scores1"] = torch.rand((B, N), generator=g, device=device)
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = torch.optim.Adam(params, lr=1e-4)
+    flat = torch.empty(sum(p.numel() for p in params), device=device) if distributed else None
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        pred = model(data)
+        losses = model.loss(pred, data)
+        losses = losses[0] if isinstance(losses, tuple) else losses
+        loss = torch.mean(losses["total"])  # train.py:436
+        loss.backward()  # train.py:450
+        if distributed:  # data-parallel gradient exchange: one flat bucket, one RCCL all-reduce
+            o = 0
+            for p in params:
+                n = p.numel()
+                flat[o:o + n].copy_(p.grad.reshape(-1))
+                o += n
+            dist.all_reduce(flat)
+            flat.div_(world)
+            o = 0
+            for p in params:
+                n = p.numel()
+                p.grad.copy_(flat[o:o + n].view_as(p.grad))
+                o += n
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    pairs = B * args.steps * world
+    tf = train_flops_per_pair(N, sg) * pairs / el / 1e12
+    result = {
+        "metric": f"training image-pairs/sec ({'SuperGlue' if sg else 'LightGlue'} forward + loss + backward + Adam)",
+        "value": round(pairs / el, 3),
+        "unit": "image-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * el / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SuperPoint-shaped keypoints/descriptors, seeded one-to-one ground truth, random-init weights)",
+        "config": {"workload": WORKLOADS[args.workload][2] if (B, N) == WORKLOADS[args.workload][:2]
+                   else f"{args.workload} shape, N={N}, batch={B} per GPU",
+                   "npts": N, "pairs_per_gpu_per_step": B, "global_batch": B * world,
+                   "parallelism": f"data-parallel x{world}" + (" (RCCL all-reduce of one flat gradient bucket)" if distributed else "")},
+        "roofline": {"kernel": "whole training step (every kernel; f32-input MFMA, bf16x6 input gradients)", "bound": "mfma",
+                     "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "note": "step-average over all kernels (algorithmic flops of bench.train_flops_per_pair); per-kernel "
+                             "rates in DESIGN.md §10c/§10d and profiles/r04"},
+        "loss": float(loss.detach()),
+        "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
+    }
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        result["cpu_baseline"] = cpu_baseline_train(N, args.cpu_budget, sg)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:

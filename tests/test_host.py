@@ -209,3 +209,23 @@ def test_superglue_registry_and_cpu_inputs_raise():
     assert out["matches0"].dtype == torch.int32 and (out["matches0"] == -1).all() and out["matches1"].shape == (1, 0)
     with pytest.raises(ValueError):
         SuperGlue({"GNN_layers": ["self", "both"]})
+
+
+def test_bench_training_ground_truth_is_one_to_one():
+    """bench.py --workload train*: the seeded ground truth of the synthetic pairs is one-to-one,
+    consistent across gt_matches0 / gt_matches1 / gt_assignment, and leaves about a third unmatched;
+    the training flop model counts the forward linears three times (y, dx, dW)."""
+    import bench
+
+    d = bench.gpu_pairs(3, 96, 256, 1, torch.device("cpu"))
+    g = bench.gpu_ground_truth(d, 7)
+    m0, m1, a = g["gt_matches0"], g["gt_matches1"], g["gt_assignment"]
+    b, i = torch.nonzero(m0 > -1, as_tuple=True)
+    assert (m1[b, m0[b, i]] == i).all()
+    b, j = torch.nonzero(m1 > -1, as_tuple=True)
+    assert (m0[b, m1[b, j]] == j).all()
+    assert int(a.sum()) == int((m0 > -1).sum()) == int((m1 > -1).sum())
+    assert (a.sum(2) <= 1).all() and (a.sum(1) <= 1).all()
+    frac = float((m0 > -1).float().mean())
+    assert 0.45 < frac < 0.8
+    assert bench.train_flops_per_pair(2048) > 3 * 9 * 76 * 2048 * 256 * 256

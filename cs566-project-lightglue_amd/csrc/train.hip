@@ -168,6 +168,114 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemmK p) {
     }
 }
 
+// Weight-gradient product on bf16 matrix cores: C[M][N] = alpha (sum_k A[k][m] B[k][n]) (+ ...)
+// for (ta, tb) = (1, 0), both operands stored k-major (k = the rows the gradient sums over).  A
+// 16-deep k-tile of each operand is loaded one m (or n) column per thread -- eight scalar loads
+// down k, coalesced across the lanes -- split into three bf16 pieces (common.h split3) and
+// written m-major to LDS as one 16-byte chunk of 8 consecutive k per piece (the eval GEMM's
+// chunk swizzle), so a lane reads its MFMA operand with one ds_read_b128; each 32 x 32 block
+// takes the six v_mfma_f32_32x32x16_bf16 of mfma_x6.  Split-k partials as tgemm_kernel.
+constexpr int X6_BM = 128, X6_BN = 128, X6_BK = 16;
+
+__global__ __launch_bounds__(256) void tgemm_x6t_kernel(TGemmK p) {
+  // [stage][operand][piece][128 rows][16 k] bf16 = 2 x 2 x 3 x 4 KiB
+  __shared__ __attribute__((aligned(16))) __bf16 S[2][2][3][X6_BM * X6_BK];
+  const TGemm& g = p.g;
+  const int t = threadIdx.x;
+  const int z = blockIdx.z, bat = z / p.ksplit, ks = z - bat * p.ksplit;
+  const float* A = g.A + bat * g.sA;
+  const float* B = g.B + bat * g.sB;
+  const int m0 = blockIdx.x * X6_BM, n0 = blockIdx.y * X6_BN;
+  const int kbeg = ks * p.kchunk, kend = min(g.K, kbeg + p.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + X6_BK - 1) / X6_BK : 0;
+  const int w = t >> 6, l = t & 63, half = l >> 5, l32 = l & 31;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  // staging: thread t owns column c = t & 127 of the tile and k-half kh = t >> 7 (8 rows)
+  const int sc = t & 127, kh = t >> 7;
+  const bool am = m0 + sc < g.M, bn = n0 + sc < g.N;
+  float ra[8], rb[8];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + 8 * kh + j;
+      const bool kin = k < kend;
+      ra[j] = (kin && am) ? A[(long long)k * g.lda + m0 + sc] : 0.f;
+      rb[j] = (kin && bn) ? B[(long long)k * g.ldb + n0 + sc] : 0.f;
+    }
+  };
+  auto sstore = [&](int st) {
+    const int off = sc * X6_BK + ((kh ^ ((sc >> 3) & 1)) * 8);
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const float* r = o ? rb : ra;
+      bf16x8 h, m, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 a, b, c;
+        split3(r[e], a, b, c);
+        h[e] = a;
+        m[e] = b;
+        lo[e] = c;
+      }
+      *reinterpret_cast<bf16x8*>(&S[st][o][0][off]) = h;
+      *reinterpret_cast<bf16x8*>(&S[st][o][1][off]) = m;
+      *reinterpret_cast<bf16x8*>(&S[st][o][2][off]) = lo;
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+  if (nk > 0) {
+    gload(kbeg);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kbeg + (kt + 1) * X6_BK);
+    bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ra_ = wm + 32 * i + l32, rb_ = wn + 32 * i + l32;
+        fa[i][pc] = *reinterpret_cast<const bf16x8*>(&S[cur][0][pc][ra_ * X6_BK + ((half ^ ((ra_ >> 3) & 1)) * 8)]);
+        fb[i][pc] = *reinterpret_cast<const bf16x8*>(&S[cur][1][pc][rb_ * X6_BK + ((half ^ ((rb_ >> 3) & 1)) * 8)]);
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = mfma_x6(fa[i][0], fa[i][1], fa[i][2], fb[j][0], fb[j][1], fb[j][2], acc[i][j]);
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* C = g.C + bat * g.sC;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + l32;
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + row32(r, half);
+        if (row >= g.M) continue;
+        const float v = acc[i][j][r];
+        if (p.ksplit > 1) {
+          p.part[((long long)z * g.M + row) * g.N + col] = v;
+        } else {
+          float o = g.alpha * (g.bias ? v + g.bias[col] : v);
+          float* cp = C + (long long)row * g.ldc + col;
+          if (g.beta != 0.f) o = fmaf(g.beta, *cp, o);
+          *cp = o;
+        }
+      }
+    }
+}
+
 __global__ __launch_bounds__(256) void tgemm_reduce_kernel(TGemmK p) {
   const TGemm& g = p.g;
   const long long MN = (long long)g.M * g.N;
@@ -974,6 +1082,9 @@ size_t tgemm_ws_floats(int M, int N, int K, int batch) {
 #ifndef LG_TG_X6_FWD
 #define LG_TG_X6_FWD 0  // 1: forward products (ta = 0, tb = 1) too (moves the forward's rounding: see DESIGN §10c)
 #endif
+#ifndef LG_TG_X6_WGRAD
+#define LG_TG_X6_WGRAD 1  // weight gradients (ta = 1, tb = 0) on the bf16x6 kernel tgemm_x6t_kernel
+#endif
 #ifndef LG_TG_X6
 #define LG_TG_X6 1  // route k-contiguous products to the bf16x6 GEMM (LG_TG_X6=0 at run time: f32 MFMA only)
 #endif
@@ -1049,6 +1160,12 @@ hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, 
   p.vecA = aligned(g.A, g.lda, g.sA);
   p.vecB = aligned(g.B, g.ldb, g.sB);
   const dim3 grid(cdiv(g.M, TG_BM), cdiv(g.N, TG_BN), g.batch * p.ksplit);
+  if (x6 && ta && !tb && tg_x6_enabled() && LG_TG_X6_WGRAD) {  // weight gradients on bf16x6
+    hipLaunchKernelGGL(tgemm_x6t_kernel, grid, dim3(256), 0, st, p);
+    if (p.ksplit > 1)
+      hipLaunchKernelGGL(tgemm_reduce_kernel, dim3(cdiv((long long)g.M * g.N * g.batch, 256)), dim3(256), 0, st, p);
+    return hipGetLastError();
+  }
   if (!ta && !tb) hipLaunchKernelGGL((tgemm_kernel<false, false>), grid, dim3(256), 0, st, p);
   else if (!ta && tb) hipLaunchKernelGGL((tgemm_kernel<false, true>), grid, dim3(256), 0, st, p);
   else if (ta && !tb) hipLaunchKernelGGL((tgemm_kernel<true, false>), grid, dim3(256), 0, st, p);

@@ -1,0 +1,7 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_sg_train.py -q -s --timeout 150 --timeout-method thread > gpurun_out/x6w_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "worst|passed|failed|Error" gpurun_out/x6w_tests.log | cut -c1-260; [ $rc -ne 0 ] && exit $rc
+KB_LIBS="default wgoff.so default wgoff.so" bash tools/gpu_kb_tgemm.sh
+AB_LIBS=wgoff.so bash tools/gpu_ab_train.sh

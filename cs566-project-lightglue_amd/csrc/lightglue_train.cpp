@@ -23,6 +23,10 @@ int handle_device(const lg_handle* h);
 int handle_weight_index(const lg_handle* h, const std::string& name);
 }  // namespace lg
 
+#ifndef LG_HEAD_X6
+#define LG_HEAD_X6 0  // 1: the assignment heads' products may take the bf16x6 GEMM too
+#endif
+
 namespace {
 
 using namespace lg;
@@ -526,7 +530,7 @@ int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, 
   HeadScratch s = carve_head_scratch((char*)scratch, B, M, N);
   if (scratch_bytes < s.bytes) return fail(LG_E_WORKSPACE, "scratch too small: need " + std::to_string(s.bytes));
   TR_HIP(hipSetDevice(handle_device(h)));
-  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART, false};
+  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART, LG_HEAD_X6 != 0};
   const Params P{h, params, grads};
   const std::string a = "log_assignment." + std::to_string(layer);
   const int R0 = B * M, R = B * (M + N);
@@ -593,7 +597,7 @@ int lg_head_forward(lg_handle_t* h, const float* const* params, int32_t layer, c
   HeadScratch s = carve_head_scratch((char*)scratch, B, M, N);
   if (scratch_bytes < s.bytes) return fail(LG_E_WORKSPACE, "scratch too small: need " + std::to_string(s.bytes));
   TR_HIP(hipSetDevice(handle_device(h)));
-  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART, false};
+  const Ctx c{(hipStream_t)stream, s.WS, s.ws_floats, s.PART, LG_HEAD_X6 != 0};
   const Params P{h, params, nullptr};
   const std::string a = "log_assignment." + std::to_string(layer);
   const int R0 = B * M, R = B * (M + N);

@@ -325,6 +325,182 @@ __device__ __forceinline__ void load_head_row_frag(const float* row, int h, floa
   }
 }
 
+// The same forward on bf16 matrix cores (bf16x6, common.h): S^T = K Q^T and O^T = V^T P^T as six
+// v_mfma_f32_32x32x16_bf16 per 32 x 32 x 16 block, every operand split into three bf16 pieces
+// (the fp32-accurate product at the bf16 rate).  The query's pieces sit in registers (scaled by
+// scale log2 e before the split, as above); a 64-key tile of K is staged [key][dim] and of V
+// transposed [dim][key] as three bf16 planes each, 16-byte chunks XOR-swizzled by row.  The V^T
+// chunks hold the keys in the accumulator's row32 order, so P^T goes from the S^T accumulators
+// straight into the B operand (split per value).  One LDS buffer: the next tile waits in
+// registers and lands between two barriers.
+__device__ __forceinline__ int x6_sw(int row, int chunk) { return (chunk ^ (row & 7)) * 8; }
+
+__global__ __launch_bounds__(256, 2) void tattn_fwd_x6_kernel(TAttn a) {
+  __shared__ __attribute__((aligned(16))) __bf16 Kp[3][64 * 64];
+  __shared__ __attribute__((aligned(16))) __bf16 Vt[3][64 * 64];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, l32 = l & 31;
+  const int item = blockIdx.y, b = item / a.H, hd = item - b * a.H;
+  const float* Q = a.Q + (long long)b * a.Nq * a.ldq + hd * 64;
+  const float* K = a.K + (long long)b * a.Nk * a.ldk + hd * 64;
+  const float* V = a.V + (long long)b * a.Nk * a.ldv + hd * 64;
+  const int qrow = blockIdx.x * 128 + w * 32 + l32;
+  const bool qv = qrow < a.Nq;
+  const float c = a.scale * kLog2e;
+  bf16x8 qf[4][3];  // dims 16 ks + 8 h .. +7 of this lane's query, three pieces
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+    if (qv) {
+      const float* qp = Q + (long long)qrow * a.ldq + 16 * ks + 8 * h;
+      v0 = *reinterpret_cast<const f32x4*>(qp);
+      v1 = *reinterpret_cast<const f32x4*>(qp + 4);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 x0, x1, x2;
+      split3((e < 4 ? v0[e] : v1[e - 4]) * c, x0, x1, x2);
+      qf[ks][0][e] = x0;
+      qf[ks][1][e] = x1;
+      qf[ks][2][e] = x2;
+    }
+  }
+  // staging: K row t >> 2, dims 16 (t & 3) ..; V^T row (dim) t & 63, key chunks 2 (t >> 6), +1
+  const int kr = t >> 2, kc = t & 3, vd = t & 63, vc = 2 * (t >> 6);
+  f32x4 rk[4];
+  float rv[16];
+  auto chunk_key = [](int ch, int e) {  // key (within the tile) of element e of V^T chunk ch
+    return 32 * (ch >> 2) + row32(8 * ((ch >> 1) & 1) + e, ch & 1);
+  };
+  auto gload = [&](int kt) {
+    const int key = kt * 64 + kr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      rk[q] = key < a.Nk ? *reinterpret_cast<const f32x4*>(K + (long long)key * a.ldk + 16 * kc + 4 * q)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k2 = kt * 64 + chunk_key(vc + cc, e);
+        rv[8 * cc + e] = k2 < a.Nk ? V[(long long)k2 * a.ldv + vd] : 0.f;
+      }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      bf16x8 p0, p1, p2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 x0, x1, x2;
+        split3(rk[2 * hh + (e >> 2)][e & 3], x0, x1, x2);
+        p0[e] = x0;
+        p1[e] = x1;
+        p2[e] = x2;
+      }
+      const int off = kr * 64 + x6_sw(kr, 2 * kc + hh);
+      *reinterpret_cast<bf16x8*>(&Kp[0][off]) = p0;
+      *reinterpret_cast<bf16x8*>(&Kp[1][off]) = p1;
+      *reinterpret_cast<bf16x8*>(&Kp[2][off]) = p2;
+    }
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      bf16x8 p0, p1, p2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 x0, x1, x2;
+        split3(rv[8 * cc + e], x0, x1, x2);
+        p0[e] = x0;
+        p1[e] = x1;
+        p2[e] = x2;
+      }
+      const int off = vd * 64 + x6_sw(vd, vc + cc);
+      *reinterpret_cast<bf16x8*>(&Vt[0][off]) = p0;
+      *reinterpret_cast<bf16x8*>(&Vt[1][off]) = p1;
+      *reinterpret_cast<bf16x8*>(&Vt[2][off]) = p2;
+    }
+  };
+  const int nkt = (a.Nk + 63) / 64;
+  float m = -INFINITY, lsum = 0.f;
+  f32x16 ot[2] = {zero16(), zero16()};
+  gload(0);
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();  // every wave is done with the previous tile
+    sstore();
+    __syncthreads();
+    if (kt + 1 < nkt) gload(kt + 1);
+    f32x16 st[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int row = 32 * tt + l32, off = row * 64 + x6_sw(row, 2 * ks + h);
+        const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(&Kp[0][off]);
+        const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(&Kp[1][off]);
+        const bf16x8 k2 = *reinterpret_cast<const bf16x8*>(&Kp[2][off]);
+        st[tt] = mfma_x6(k0, k1, k2, qf[ks][0], qf[ks][1], qf[ks][2], st[tt]);
+      }
+    if (kt * 64 + 64 > a.Nk) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kt * 64 + 32 * tt + row32(r, h) >= a.Nk) st[tt][r] = -INFINITY;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[tt][r]);
+    mx = max_xor32(mx);
+    const float mn = fmaxf(m, mx);
+    const float base = mn == -INFINITY ? 0.f : mn;
+    const float f = exp2f(m - base);
+    lsum *= f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      ot[0][r] *= f;
+      ot[1][r] *= f;
+    }
+    m = mn;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {  // keys of step s2: st[s2 >> 1][8 (s2 & 1) + e]
+      bf16x8 pb0, pb1, pb2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float pv = exp2f(st[s2 >> 1][8 * (s2 & 1) + e] - base);
+        lsum += pv;
+        __bf16 x0, x1, x2;
+        split3(pv, x0, x1, x2);
+        pb0[e] = x0;
+        pb1[e] = x1;
+        pb2[e] = x2;
+      }
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int row = 32 * dt + l32, off = row * 64 + x6_sw(row, 2 * s2 + h);
+        const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(&Vt[0][off]);
+        const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(&Vt[1][off]);
+        const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(&Vt[2][off]);
+        ot[dt] = mfma_x6(v0, v1, v2, pb0, pb1, pb2, ot[dt]);
+      }
+    }
+  }
+  lsum = sum_xor32(lsum);
+  if (!qv) return;
+  const float inv = 1.f / lsum;
+  float* O = a.O + ((long long)b * a.Nq + qrow) * a.ldo + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = ot[dt][4 * g4 + e] * inv;
+      *reinterpret_cast<f32x4*>(O + 32 * dt + 8 * g4 + 4 * h) = v;
+    }
+  if (h == 0) a.lse[(long long)item * a.Nq + qrow] = m + log2f(lsum);
+}
+
 __global__ __launch_bounds__(256) void tattn_fwd_kernel(TAttn a) {
   __shared__ __attribute__((aligned(16))) float Ks[2][64 * TA_KP];
   __shared__ __attribute__((aligned(16))) float Vs[2][64 * TA_VP];
@@ -1175,8 +1351,23 @@ hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, 
   return hipGetLastError();
 }
 
+#ifndef LG_TA_X6
+#define LG_TA_X6 1  // the training attention forward on bf16x6 (tattn_fwd_x6_kernel); 0: f32 MFMA
+#endif
+static bool ta_x6_enabled() {
+  static const int v = [] {
+    const char* e = getenv("LG_TA_X6");
+    return e ? atoi(e) : LG_TA_X6;
+  }();
+  return v != 0;
+}
+
 hipError_t tattn_forward(const TAttn& a, hipStream_t st) {
   if (a.B * a.H == 0 || a.Nq == 0) return hipSuccess;
+  if (ta_x6_enabled() && a.Nk > 0) {
+    hipLaunchKernelGGL(tattn_fwd_x6_kernel, dim3(cdiv(a.Nq, 128), a.B * a.H), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(tattn_fwd_kernel, dim3(cdiv(a.Nq, 128), a.B * a.H), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -633,7 +633,7 @@ __global__ __launch_bounds__(256) void tattn_fwd_kernel(TAttn a) {
 // segments per instruction).  Against 4 waves x 128 keys with 32 x 32 dQ quarters: a quarter of
 // the atomic bytes, and two waves per SIMD.
 constexpr int TB_W = 8, TB_KEYS = 32 * TB_W;
-constexpr int TB_QP = 66, TB_KP = 80, TB_DP = TB_KEYS + 4;
+constexpr int TB_QP = 66, TB_KP = 80, TB_DP = TB_KEYS + 4, XB_KP = 68;
 
 __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_kernel(TAttn a) {
   // one Q / dO tile buffer: the next tile waits in registers and lands after the barrier that
@@ -757,6 +757,236 @@ __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_kernel(TAttn a) {
       if (qi < a.Nq) atomicAdd(dQ + (long long)qi * a.ldq, qacc[r] * a.scale);
     }
     if (qt + 1 < nqt) store_q();  // every wave is past this tile's reads of Qs / dOs (barrier above)
+    __syncthreads();
+  }
+  if (!kv) return;
+  float* dK = a.dK + ((long long)b * a.Nk + key) * a.ldk + hd * 64;
+  float* dV = a.dV + ((long long)b * a.Nk + key) * a.ldv + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * dt + 8 * g4 + 4 * h;
+      f32x4 vk, vv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        vk[e] = dkt[dt][4 * g4 + e] * a.scale;
+        vv[e] = dvt[dt][4 * g4 + e];
+      }
+      if (a.accum_kv) {
+        vk += *reinterpret_cast<const f32x4*>(dK + d0);
+        vv += *reinterpret_cast<const f32x4*>(dV + d0);
+      }
+      *reinterpret_cast<f32x4*>(dK + d0) = vk;
+      *reinterpret_cast<f32x4*>(dV + d0) = vv;
+    }
+}
+
+// The same backward with S, dP, dV^T and dK^T on bf16 matrix cores (bf16x6, common.h): the key's
+// K (scaled by scale log2 e) and V sit in registers as three bf16 pieces; a query tile is staged
+// [query][dim] (A operand of S = Q K^T and dP = dO V^T) and [dim][query] (A operand of dV^T and
+// dK^T, the queries of each 16-byte chunk in the row32 order the S / dP accumulators hold them
+// in), three bf16 planes each.  P and dS go from the accumulators into the B operands split per
+// value.  dQ stays on v_mfma_f32_16x16x4_f32 over fp32 dS / K exactly as tattn_bwd_kernel.
+__device__ __forceinline__ int x6_swt(int row, int chunk) { return (chunk ^ ((row >> 2) & 3)) * 8; }
+
+__global__ __launch_bounds__(64 * TB_W) void tattn_bwd_x6_kernel(TAttn a) {
+  __shared__ __attribute__((aligned(16))) __bf16 Qp[3][32 * 64];   // [query][dim]
+  __shared__ __attribute__((aligned(16))) __bf16 dOp[3][32 * 64];
+  __shared__ __attribute__((aligned(16))) __bf16 QTp[3][64 * 32];  // [dim][query, row32 chunks]
+  __shared__ __attribute__((aligned(16))) __bf16 dOTp[3][64 * 32];
+  __shared__ __attribute__((aligned(16))) float Kall[TB_KEYS * XB_KP];
+  __shared__ __attribute__((aligned(16))) float dSs[32 * TB_DP];
+  __shared__ float lse_s[32], del_s[32];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, l32 = l & 31;
+  const int item = blockIdx.y, b = item / a.H, hd = item - b * a.H;
+  const float* Q = a.Q + (long long)b * a.Nq * a.ldq + hd * 64;
+  const float* dO = a.dO + (long long)b * a.Nq * a.ldo + hd * 64;
+  const float* K = a.K + (long long)b * a.Nk * a.ldk + hd * 64;
+  const float* V = a.V + (long long)b * a.Nk * a.ldv + hd * 64;
+  const float* lse = a.lse + (long long)item * a.Nq;
+  const float* del = a.delta + (long long)item * a.Nq;
+  const int kb0 = blockIdx.x * TB_KEYS;
+  const int key = kb0 + w * 32 + l32;
+  const bool kv = key < a.Nk;
+  const float c = a.scale * kLog2e;
+  f32x4 kr[4][2], vr[4][2];  // dims 16 ks + 8 h .. +7 of this lane's key (K scaled), split per tile
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0, v0 = k0, v1 = k0;
+    if (kv) {
+      const float* kp = K + (long long)key * a.ldk + 16 * ks + 8 * h;
+      const float* vp = V + (long long)key * a.ldv + 16 * ks + 8 * h;
+      k0 = *reinterpret_cast<const f32x4*>(kp);
+      k1 = *reinterpret_cast<const f32x4*>(kp + 4);
+      v0 = *reinterpret_cast<const f32x4*>(vp);
+      v1 = *reinterpret_cast<const f32x4*>(vp + 4);
+    }
+    kr[ks][0] = k0 * c;
+    kr[ks][1] = k1 * c;
+    vr[ks][0] = v0;
+    vr[ks][1] = v1;
+  }
+  {  // the workgroup's 256 keys (unscaled) for dQ
+    const int sr = t >> 4, sc = (t & 15) * 4;
+#pragma unroll
+    for (int q = 0; q < TB_KEYS / 32; ++q) {
+      const int k = kb0 + sr + 32 * q;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (k < a.Nk) v = *reinterpret_cast<const f32x4*>(K + (long long)k * a.ldk + sc);
+      *reinterpret_cast<f32x4*>(Kall + (sr + 32 * q) * XB_KP + sc) = v;
+    }
+  }
+  // query tiles: thread t -> query sr = t >> 4, dims sc = 4 (t & 15) .. +3; in the transposed
+  // planes query sr sits in chunk 2 (sr >> 4) + ((sr >> 2) & 1) at position (sr & 3) + 4 ((sr >> 3) & 1)
+  const int sr = t >> 4, sc = (t & 15) * 4;
+  const int tch = 2 * (sr >> 4) + ((sr >> 2) & 1), tpos = (sr & 3) + 4 * ((sr >> 3) & 1);
+  f32x4 rq, rd;
+  float rl = 0.f, rdl = 0.f;
+  auto load_q = [&](int qt) {
+    const int qi = qt * 32 + sr;
+    if (qi < a.Nq) {
+      rq = *reinterpret_cast<const f32x4*>(Q + (long long)qi * a.ldq + sc);
+      rd = *reinterpret_cast<const f32x4*>(dO + (long long)qi * a.ldo + sc);
+    } else {
+      rq = f32x4{0.f, 0.f, 0.f, 0.f};
+      rd = rq;
+    }
+    if (t < 32) {
+      const int qj = qt * 32 + t;
+      rl = qj < a.Nq ? lse[qj] : INFINITY;  // padded queries: p = exp2(-inf) = 0
+      rdl = qj < a.Nq ? del[qj] : 0.f;
+    }
+  };
+  auto store_q = [&]() {
+    const int off = sr * 64 + x6_sw(sr, sc >> 3) + (sc & 4);
+    bf16x4 q0, q1, q2, d0, d1, d2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      __bf16 x0, x1, x2;
+      split3(rq[e], x0, x1, x2);
+      q0[e] = x0;
+      q1[e] = x1;
+      q2[e] = x2;
+      const int to = (sc + e) * 32 + x6_swt(sc + e, tch) + tpos;
+      QTp[0][to] = x0;
+      QTp[1][to] = x1;
+      QTp[2][to] = x2;
+      split3(rd[e], x0, x1, x2);
+      d0[e] = x0;
+      d1[e] = x1;
+      d2[e] = x2;
+      dOTp[0][to] = x0;
+      dOTp[1][to] = x1;
+      dOTp[2][to] = x2;
+    }
+    *reinterpret_cast<bf16x4*>(&Qp[0][off]) = q0;
+    *reinterpret_cast<bf16x4*>(&Qp[1][off]) = q1;
+    *reinterpret_cast<bf16x4*>(&Qp[2][off]) = q2;
+    *reinterpret_cast<bf16x4*>(&dOp[0][off]) = d0;
+    *reinterpret_cast<bf16x4*>(&dOp[1][off]) = d1;
+    *reinterpret_cast<bf16x4*>(&dOp[2][off]) = d2;
+    if (t < 32) {
+      lse_s[t] = rl;
+      del_s[t] = rdl;
+    }
+  };
+  f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
+  const int nqt = (a.Nq + 31) / 32;
+  const int qh = w & 1, dq = w >> 1;  // this wave's dQ tile: queries 16 qh .., dims 16 dq ..
+  const int l16 = l & 15, lk = l >> 4;
+  float* dQ = a.dQ + (long long)b * a.Nq * a.ldq + hd * 64 + 16 * dq + l16;
+  load_q(0);
+  store_q();
+  __syncthreads();
+  for (int qt = 0; qt < nqt; ++qt) {
+    if (qt + 1 < nqt) load_q(qt + 1);
+    f32x16 sacc, pacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sacc[r] = -lse_s[row32(r, h)];
+      pacc[r] = -del_s[row32(r, h)];
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int off = l32 * 64 + x6_sw(l32, 2 * ks + h);
+      const bf16x8 q0 = *reinterpret_cast<const bf16x8*>(&Qp[0][off]);
+      const bf16x8 q1 = *reinterpret_cast<const bf16x8*>(&Qp[1][off]);
+      const bf16x8 q2 = *reinterpret_cast<const bf16x8*>(&Qp[2][off]);
+      bf16x8 k0, k1, k2;
+      asm volatile("" : "+v"(kr[ks][0]), "+v"(kr[ks][1]));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 x0, x1, x2;
+        split3(kr[ks][e >> 2][e & 3], x0, x1, x2);
+        k0[e] = x0;
+        k1[e] = x1;
+        k2[e] = x2;
+      }
+      sacc = mfma_x6(q0, q1, q2, k0, k1, k2, sacc);
+      const bf16x8 d0 = *reinterpret_cast<const bf16x8*>(&dOp[0][off]);
+      const bf16x8 d1 = *reinterpret_cast<const bf16x8*>(&dOp[1][off]);
+      const bf16x8 d2 = *reinterpret_cast<const bf16x8*>(&dOp[2][off]);
+      bf16x8 v0, v1, v2;
+      asm volatile("" : "+v"(vr[ks][0]), "+v"(vr[ks][1]));  // split per tile, not hoisted out of the loop
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 x0, x1, x2;
+        split3(vr[ks][e >> 2][e & 3], x0, x1, x2);
+        v0[e] = x0;
+        v1[e] = x1;
+        v2[e] = x2;
+      }
+      pacc = mfma_x6(d0, d1, d2, v0, v1, v2, pacc);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = kv ? exp2f(sacc[r]) : 0.f;
+      sacc[r] = p;
+      pacc[r] *= p;  // dS (w.r.t. the scaled scores)
+      dSs[row32(r, h) * TB_DP + w * 32 + l32] = pacc[r];
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // queries of step s: accumulator values 8 s .. 8 s + 7
+      bf16x8 p0, p1, p2, g0, g1, g2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 x0, x1, x2;
+        split3(sacc[8 * s + e], x0, x1, x2);
+        p0[e] = x0;
+        p1[e] = x1;
+        p2[e] = x2;
+        split3(pacc[8 * s + e], x0, x1, x2);
+        g0[e] = x0;
+        g1[e] = x1;
+        g2[e] = x2;
+      }
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int row = 32 * dt + l32, off = row * 32 + x6_swt(row, 2 * s + h);
+        const bf16x8 o0 = *reinterpret_cast<const bf16x8*>(&dOTp[0][off]);
+        const bf16x8 o1 = *reinterpret_cast<const bf16x8*>(&dOTp[1][off]);
+        const bf16x8 o2 = *reinterpret_cast<const bf16x8*>(&dOTp[2][off]);
+        dvt[dt] = mfma_x6(o0, o1, o2, p0, p1, p2, dvt[dt]);
+        const bf16x8 q0 = *reinterpret_cast<const bf16x8*>(&QTp[0][off]);
+        const bf16x8 q1 = *reinterpret_cast<const bf16x8*>(&QTp[1][off]);
+        const bf16x8 q2 = *reinterpret_cast<const bf16x8*>(&QTp[2][off]);
+        dkt[dt] = mfma_x6(q0, q1, q2, g0, g1, g2, dkt[dt]);
+      }
+    }
+    __syncthreads();
+    f32x4 qacc = {0.f, 0.f, 0.f, 0.f};
+    const float* ds_row = dSs + (16 * qh + l16) * TB_DP + lk;
+    const float* k_col = Kall + lk * XB_KP + 16 * dq + l16;
+#pragma unroll 16
+    for (int s = 0; s < TB_KEYS / 4; ++s)
+      qacc = __builtin_amdgcn_mfma_f32_16x16x4f32(ds_row[4 * s], k_col[4 * s * XB_KP], qacc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qi = qt * 32 + 16 * qh + 4 * lk + r;
+      if (qi < a.Nq) atomicAdd(dQ + (long long)qi * a.ldq, qacc[r] * a.scale);
+    }
+    if (qt + 1 < nqt) store_q();  // every wave is past this tile's reads (barrier above)
     __syncthreads();
   }
   if (!kv) return;
@@ -1372,8 +1602,23 @@ hipError_t tattn_forward(const TAttn& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+#ifndef LG_TB_X6
+#define LG_TB_X6 1  // the training attention backward on bf16x6 (tattn_bwd_x6_kernel); 0: f32 MFMA
+#endif
+static bool tb_x6_enabled() {
+  static const int v = [] {
+    const char* e = getenv("LG_TB_X6");
+    return e ? atoi(e) : LG_TB_X6;
+  }();
+  return v != 0;
+}
+
 hipError_t tattn_backward(const TAttn& a, hipStream_t st) {
   if (a.B * a.H == 0 || a.Nk == 0) return hipSuccess;
+  if (tb_x6_enabled() && a.Nq > 0) {
+    hipLaunchKernelGGL(tattn_bwd_x6_kernel, dim3(cdiv(a.Nk, TB_KEYS), a.B * a.H), dim3(64 * TB_W), 0, st, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(tattn_bwd_kernel, dim3(cdiv(a.Nk, TB_KEYS), a.B * a.H), dim3(64 * TB_W), 0, st, a);
   return hipGetLastError();
 }

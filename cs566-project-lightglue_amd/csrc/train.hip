@@ -633,7 +633,7 @@ __global__ __launch_bounds__(256) void tattn_fwd_kernel(TAttn a) {
 // segments per instruction).  Against 4 waves x 128 keys with 32 x 32 dQ quarters: a quarter of
 // the atomic bytes, and two waves per SIMD.
 constexpr int TB_W = 8, TB_KEYS = 32 * TB_W;
-constexpr int TB_QP = 66, TB_KP = 80, TB_DP = TB_KEYS + 4, XB_KP = 68;
+constexpr int TB_QP = 66, TB_KP = 80, TB_DP = TB_KEYS + 4;
 
 __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_kernel(TAttn a) {
   // one Q / dO tile buffer: the next tile waits in registers and lands after the barrier that
@@ -795,7 +795,7 @@ __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_x6_kernel(TAttn a) {
   __shared__ __attribute__((aligned(16))) __bf16 dOp[3][32 * 64];
   __shared__ __attribute__((aligned(16))) __bf16 QTp[3][64 * 32];  // [dim][query, row32 chunks]
   __shared__ __attribute__((aligned(16))) __bf16 dOTp[3][64 * 32];
-  __shared__ __attribute__((aligned(16))) float Kall[TB_KEYS * XB_KP];
+  __shared__ __attribute__((aligned(16))) float KT[64 * TB_DP];  // the workgroup's keys, [dim][key]
   __shared__ __attribute__((aligned(16))) float dSs[32 * TB_DP];
   __shared__ float lse_s[32], del_s[32];
   const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, l32 = l & 31;
@@ -810,7 +810,8 @@ __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_x6_kernel(TAttn a) {
   const int key = kb0 + w * 32 + l32;
   const bool kv = key < a.Nk;
   const float c = a.scale * kLog2e;
-  f32x4 kr[4][2], vr[4][2];  // dims 16 ks + 8 h .. +7 of this lane's key (K scaled), split per tile
+  bf16x8 kf[4][3];  // dims 16 ks + 8 h .. +7 of this lane's key: K (scaled) in three pieces,
+  f32x4 vr[4][2];   // V in fp32, split per query tile
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0, v0 = k0, v1 = k0;
@@ -822,19 +823,26 @@ __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_x6_kernel(TAttn a) {
       v0 = *reinterpret_cast<const f32x4*>(vp);
       v1 = *reinterpret_cast<const f32x4*>(vp + 4);
     }
-    kr[ks][0] = k0 * c;
-    kr[ks][1] = k1 * c;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 x0, x1, x2;
+      split3((e < 4 ? k0[e] : k1[e - 4]) * c, x0, x1, x2);
+      kf[ks][0][e] = x0;
+      kf[ks][1][e] = x1;
+      kf[ks][2][e] = x2;
+    }
     vr[ks][0] = v0;
     vr[ks][1] = v1;
   }
-  {  // the workgroup's 256 keys (unscaled) for dQ
+  {  // the workgroup's 256 keys (unscaled) for dQ, transposed
     const int sr = t >> 4, sc = (t & 15) * 4;
 #pragma unroll
     for (int q = 0; q < TB_KEYS / 32; ++q) {
       const int k = kb0 + sr + 32 * q;
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < a.Nk) v = *reinterpret_cast<const f32x4*>(K + (long long)k * a.ldk + sc);
-      *reinterpret_cast<f32x4*>(Kall + (sr + 32 * q) * XB_KP + sc) = v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) KT[(sc + e) * TB_DP + sr + 32 * q] = v[e];
     }
   }
   // query tiles: thread t -> query sr = t >> 4, dims sc = 4 (t & 15) .. +3; in the transposed
@@ -900,7 +908,6 @@ __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_x6_kernel(TAttn a) {
   store_q();
   __syncthreads();
   for (int qt = 0; qt < nqt; ++qt) {
-    if (qt + 1 < nqt) load_q(qt + 1);
     f32x16 sacc, pacc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -913,17 +920,7 @@ __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_x6_kernel(TAttn a) {
       const bf16x8 q0 = *reinterpret_cast<const bf16x8*>(&Qp[0][off]);
       const bf16x8 q1 = *reinterpret_cast<const bf16x8*>(&Qp[1][off]);
       const bf16x8 q2 = *reinterpret_cast<const bf16x8*>(&Qp[2][off]);
-      bf16x8 k0, k1, k2;
-      asm volatile("" : "+v"(kr[ks][0]), "+v"(kr[ks][1]));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        __bf16 x0, x1, x2;
-        split3(kr[ks][e >> 2][e & 3], x0, x1, x2);
-        k0[e] = x0;
-        k1[e] = x1;
-        k2[e] = x2;
-      }
-      sacc = mfma_x6(q0, q1, q2, k0, k1, k2, sacc);
+      sacc = mfma_x6(q0, q1, q2, kf[ks][0], kf[ks][1], kf[ks][2], sacc);
       const bf16x8 d0 = *reinterpret_cast<const bf16x8*>(&dOp[0][off]);
       const bf16x8 d1 = *reinterpret_cast<const bf16x8*>(&dOp[1][off]);
       const bf16x8 d2 = *reinterpret_cast<const bf16x8*>(&dOp[2][off]);
@@ -941,7 +938,7 @@ __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_x6_kernel(TAttn a) {
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float p = kv ? exp2f(sacc[r]) : 0.f;
+      const float p = kv ? __builtin_amdgcn_exp2f(sacc[r]) : 0.f;  // v_exp_f32 (tiny p flush to 0)
       sacc[r] = p;
       pacc[r] *= p;  // dS (w.r.t. the scaled scores)
       dSs[row32(r, h) * TB_DP + w * 32 + l32] = pacc[r];
@@ -975,12 +972,17 @@ __global__ __launch_bounds__(64 * TB_W) void tattn_bwd_x6_kernel(TAttn a) {
       }
     }
     __syncthreads();
-    f32x4 qacc = {0.f, 0.f, 0.f, 0.f};
-    const float* ds_row = dSs + (16 * qh + l16) * TB_DP + lk;
-    const float* k_col = Kall + lk * XB_KP + 16 * dq + l16;
-#pragma unroll 16
-    for (int s = 0; s < TB_KEYS / 4; ++s)
-      qacc = __builtin_amdgcn_mfma_f32_16x16x4f32(ds_row[4 * s], k_col[4 * s * XB_KP], qacc, 0, 0, 0);
+    if (qt + 1 < nqt) load_q(qt + 1);  // lands under the dQ products
+    f32x4 qacc = {0.f, 0.f, 0.f, 0.f};  // k index lk of step s: key 64 lk + s (16-byte reads of 4 steps)
+    const float* ds_row = dSs + (16 * qh + l16) * TB_DP + 64 * lk;
+    const float* k_row = KT + (16 * dq + l16) * TB_DP + 64 * lk;
+#pragma unroll 4
+    for (int s4 = 0; s4 < TB_KEYS / 16; ++s4) {
+      const f32x4 dv = *reinterpret_cast<const f32x4*>(ds_row + 4 * s4);
+      const f32x4 kv4 = *reinterpret_cast<const f32x4*>(k_row + 4 * s4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qacc = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[e], kv4[e], qacc, 0, 0, 0);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int qi = qt * 32 + 16 * qh + 4 * lk + r;

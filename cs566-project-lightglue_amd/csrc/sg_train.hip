@@ -216,6 +216,11 @@ __global__ __launch_bounds__(256) void sk_couplings_kernel(const float* cost, co
   }
 }
 
+// exp on the hardware exp2 (v_exp_f32): the passes' arguments are <= 0 up to rounding (log-domain
+// values minus a running max or a normaliser), where the product's rounding (|x| log2 e 2^-24
+// relative) only touches terms that are already tiny; expf's range fix-ups cost ~10 VALU per value
+__device__ __forceinline__ float exp_fast(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
 // (max, sum exp(x - max)) of a lane, reduced over the wave
 __device__ __forceinline__ float lse_wave(float m, float s) {
   const float mx = wave_max(m);
@@ -248,9 +253,9 @@ __global__ __launch_bounds__(256) void sk_row_kernel(const float* Cc, int B, int
       }
       if (cm == -INFINITY) continue;
       const float mn = fmaxf(m, cm);
-      float t = s * expf(m - mn);  // s == 0 while m == -inf
+      float t = s * exp_fast(m - mn);  // s == 0 while m == -inf
 #pragma unroll
-      for (int q = 0; q < 8; ++q) t += expf(x[q] - mn);
+      for (int q = 0; q < 8; ++q) t += exp_fast(x[q] - mn);
       m = mn;
       s = t;
     }
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(256) void sk_row_kernel(const float* Cc, int B, int
   if (mode == 1) {
     const float ui = u[row];
     const float* gb = g + (long long)b * N1;
-    for (int j = l; j < N1; j += 64) acc = fmaf(gb[j], expf(c[j] + ui + vb[j] - (j < N1 - 1 ? norm : lnu_last)), acc);
+    for (int j = l; j < N1; j += 64) acc = fmaf(gb[j], exp_fast(c[j] + ui + vb[j] - (j < N1 - 1 ? norm : lnu_last)), acc);
   } else {
     for (int j = l; j < N1; j += 64) acc += c[j];
   }
@@ -304,9 +309,9 @@ __global__ __launch_bounds__(256) void sk_col_part_kernel(const float* Cc, int B
         }
         if (cm == -INFINITY) continue;
         const float mn = fmaxf(m, cm);
-        float t = s * expf(m - mn);
+        float t = s * exp_fast(m - mn);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) t += expf(x[q] - mn);
+        for (int q = 0; q < 8; ++q) t += exp_fast(x[q] - mn);
         m = mn;
         s = t;
       }
@@ -320,8 +325,8 @@ __global__ __launch_bounds__(256) void sk_col_part_kernel(const float* Cc, int B
       for (int i = i0 + grp; i < i1; i += 4) {
         const long long k = base + (long long)i * N1 + j;
         const float cij = Cc[k], ui = ub[i], gui = gub[i];
-        const float pr = expf(cij + vpj + ui - (i < M1 - 1 ? norm : lmu_last));
-        const float pc = expf(cij + ui + vj - lnu);
+        const float pr = exp_fast(cij + vpj + ui - (i < M1 - 1 ? norm : lmu_last));
+        const float pc = exp_fast(cij + ui + vj - lnu);
         acc = fmaf(gui, pr, acc);
         gC[k] -= fmaf(gvj, pc, gui * pr);
       }

@@ -454,7 +454,7 @@ __global__ __launch_bounds__(256, 2) void tattn_fwd_x6_kernel(TAttn a) {
     mx = max_xor32(mx);
     const float mn = fmaxf(m, mx);
     const float base = mn == -INFINITY ? 0.f : mn;
-    const float f = exp2f(m - base);
+    const float f = __builtin_amdgcn_exp2f(m - base);  // v_exp_f32; exp2(-inf) = 0
     lsum *= f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256, 2) void tattn_fwd_x6_kernel(TAttn a) {
       bf16x8 pb0, pb1, pb2;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float pv = exp2f(st[s2 >> 1][8 * (s2 & 1) + e] - base);
+        const float pv = __builtin_amdgcn_exp2f(st[s2 >> 1][8 * (s2 & 1) + e] - base);
         lsum += pv;
         __bf16 x0, x1, x2;
         split3(pv, x0, x1, x2);

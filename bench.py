@@ -641,7 +641,7 @@ def run_train(args, world, rank, local, distributed):
                    else f"{args.workload} shape, N={N}, batch={B} per GPU",
                    "npts": N, "pairs_per_gpu_per_step": B, "global_batch": B * world,
                    "parallelism": f"data-parallel x{world}" + (" (RCCL all-reduce of one flat gradient bucket)" if distributed else "")},
-        "roofline": {"kernel": "whole training step (every kernel; f32-input MFMA, bf16x6 input gradients)", "bound": "mfma",
+        "roofline": {"kernel": "whole training step (every kernel; f32-input MFMA, bf16x6 attention and input / weight gradients)", "bound": "mfma",
                      "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
                      "note": "step-average over all kernels (algorithmic flops of bench.train_flops_per_pair); per-kernel "

@@ -375,6 +375,87 @@ __global__ void sk_col_final_kernel(const float* part, int B, int N1, int nch, f
   }
 }
 
+// One backward step t in ONE read of C (N1 <= 64 SKF_Q): a workgroup owns SKF_R rows of one pair,
+// a wave one row at a time held in registers (lane: columns l + 64 q).  The row's
+// gu_i = base_i - sum_j gv_j pc_ij (pc = v_t's softmax weights, kept in registers) is
+// sk_row_kernel mode 1's sum in the same order; with gu_i known the same registers give
+// pr_ij (u_t's weights), the in-place gC -= gv_j pc + gu_i pr, and the wave's column sums of
+// gu_i pr, combined over the four waves in order and written per workgroup: d/d v_{t-1} is then
+// minus the ordered sum of the partials (sk_bwd_colsum_kernel).  Against the row + column pair of
+// passes: C is read once instead of twice per step and pc is not recomputed.
+constexpr int SKF_Q = 33, SKF_R = 32;
+
+__global__ __launch_bounds__(256) void sk_bwd_fused_kernel(const float* Cc, int M1, int N1, const float* u,
+                                                           const float* v, const float* vp, const float* gv,
+                                                           const float* base, float* gC, float norm, float lmu_last,
+                                                           float lnu_last, float* gu_out, float* part) {
+  __shared__ float v_s[64 * SKF_Q], vp_s[64 * SKF_Q], gv_s[64 * SKF_Q];
+  __shared__ float red[4][64 * SKF_Q];
+  const int b = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const long long pb = (long long)b * N1;
+  for (int j = threadIdx.x; j < N1; j += 256) {
+    v_s[j] = v[pb + j];
+    vp_s[j] = vp ? vp[pb + j] : 0.f;
+    gv_s[j] = gv[pb + j];
+  }
+  __syncthreads();
+  float cs[SKF_Q];
+#pragma unroll
+  for (int q = 0; q < SKF_Q; ++q) cs[q] = 0.f;
+  const int i0 = blockIdx.x * SKF_R, i1 = min(M1, i0 + SKF_R);
+  for (int i = i0 + w; i < i1; i += 4) {
+    const long long row = (long long)b * M1 + i;
+    const float* c = Cc + row * N1;
+    float* g = gC + row * N1;
+    const float ui = u[row], lmu = i < M1 - 1 ? norm : lmu_last;
+    float x[SKF_Q], pc[SKF_Q], gx[SKF_Q];  // the gC row is read with C (its latency under the sums)
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < SKF_Q; ++q) {
+      const int j = l + 64 * q;
+      x[q] = j < N1 ? c[j] : 0.f;
+      gx[q] = j < N1 ? g[j] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < SKF_Q; ++q) {
+      const int j = l + 64 * q;
+      pc[q] = 0.f;
+      if (j < N1) {
+        pc[q] = exp_fast(x[q] + ui + v_s[j] - (j < N1 - 1 ? norm : lnu_last));
+        acc = fmaf(gv_s[j], pc[q], acc);
+      }
+    }
+    acc = wave_sum(acc);
+    const float gui = (base ? base[row] : 0.f) - acc;
+    if (l == 0) gu_out[row] = gui;
+#pragma unroll
+    for (int q = 0; q < SKF_Q; ++q) {
+      const int j = l + 64 * q;
+      if (j < N1) {
+        const float pr = exp_fast(x[q] + vp_s[j] + ui - lmu);
+        cs[q] = fmaf(gui, pr, cs[q]);
+        g[j] = gx[q] - fmaf(gv_s[j], pc[q], gui * pr);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < SKF_Q; ++q) red[w][l + 64 * q] = cs[q];
+  __syncthreads();
+  float* pp = part + ((long long)b * gridDim.x + blockIdx.x) * N1;
+  for (int j = threadIdx.x; j < N1; j += 256) pp[j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+}
+
+// d/d v_{t-1}[b][j] = -(ordered sum over the workgroups' partials)
+__global__ void sk_bwd_colsum_kernel(const float* part, int B, int N1, int nwg, float* out) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)B * N1) return;
+  const int b = (int)(t / N1), j = (int)(t - (long long)b * N1);
+  const float* p = part + (long long)b * nwg * N1 + j;
+  float s = 0.f;
+  for (int k = 0; k < nwg; ++k) s += p[(long long)k * N1];
+  out[t] = -s;
+}
+
 // Z = C + u_i + v_j - norm (:178,200), one workgroup per row
 __global__ __launch_bounds__(256) void sk_out_kernel(const float* Cc, const float* u, const float* v, int B, int M1, int N1,
                                                      float norm, float* Z) {
@@ -552,8 +633,12 @@ hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M,
   return hipGetLastError();
 }
 
+static bool skf_ok(int N1) { return N1 <= 64 * SKF_Q; }
+static size_t skf_part_floats(int B, int M, int N) { return (size_t)B * cdiv(M + 1, SKF_R) * (N + 1); }
+
 size_t sk_train_scratch_floats(int B, int M, int N) {
-  return (size_t)B * (M + 1) * (N + 1) + 4 * (size_t)B * (M + N + 2) + B + sk_col_part_floats(B, M, N) + 256;
+  return (size_t)B * (M + 1) * (N + 1) + 4 * (size_t)B * (M + N + 2) + B +
+         std::max(sk_col_part_floats(B, M, N), skf_part_floats(B, M, N)) + 256;
 }
 
 hipError_t sk_train_backward(const float* Cc, const float* U, const float* V, const float* gZ, const float* gext, int B,
@@ -578,6 +663,15 @@ hipError_t sk_train_backward(const float* Cc, const float* U, const float* V, co
     const float* u = U + (size_t)(t - 1) * B * M1;
     const float* v = V + (size_t)t * B * N1;
     const float* vp = t > 1 ? V + (size_t)(t - 1) * B * N1 : nullptr;  // v_0 = 0
+    if (skf_ok(N1)) {  // both halves of the step in one pass over C
+      const unsigned nwg = cdiv(M1, SKF_R);
+      hipLaunchKernelGGL(sk_bwd_fused_kernel, dim3(nwg, B), dim3(256), 0, st, Cc, M1, N1, u, v, vp, gv,
+                         t == iters ? base : nullptr, gC, norm, lmu_last, lnu_last, gu, cpart);
+      hipLaunchKernelGGL(sk_bwd_colsum_kernel, dim3(cdiv((long long)B * N1, 256)), dim3(256), 0, st, cpart, B, N1, (int)nwg,
+                         gv2);
+      std::swap(gv, gv2);
+      continue;
+    }
     // v_t = lnu - LSE_i(C + u_t): d/d u_t = base (t = T) - sum_j gv_j pc
     hipLaunchKernelGGL(sk_row_kernel, dim3(cdiv((long long)B * M1, 4)), dim3(256), 0, st, Cc, B, M1, N1, u, v, gv,
                        t == iters ? base : nullptr, norm, lmu_last, lnu_last, 1, gu);

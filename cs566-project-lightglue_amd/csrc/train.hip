@@ -1308,6 +1308,47 @@ __global__ __launch_bounds__(256) void sim_lse_col_part_kernel(const float* sim,
     part[((long long)b * gridDim.y + blockIdx.y) * N + c] = make_float2(mm, ss);
   }
 }
+// the same partials with four columns per thread (16-byte loads; N % 4 == 0): every column sees
+// exactly the operations of sim_lse_col_part_kernel in the same order
+__global__ __launch_bounds__(256) void sim_lse_col_part4_kernel(const float* sim, int M, int N, float2* part) {
+  __shared__ f32x4 redm[4][64], reds[4][64];
+  const int c = 4 * (blockIdx.x * 64 + (threadIdx.x & 63)), g = threadIdx.x >> 6, b = blockIdx.z;
+  const int r0 = blockIdx.y * LSE_ROWS, r1 = min(M, r0 + LSE_ROWS);
+  f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    const float* s = sim + (long long)b * M * N + c;
+    for (int r = r0 + g; r < r1; r += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(s + (long long)r * N);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (v[e] > m[e]) {
+          acc[e] = acc[e] * expf(m[e] - v[e]) + 1.f;
+          m[e] = v[e];
+        } else {
+          acc[e] += expf(v[e] - m[e]);
+        }
+      }
+    }
+  }
+  redm[g][threadIdx.x & 63] = m;
+  reds[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g == 0 && c < N) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float mm = -INFINITY, ss = 0.f;
+      for (int k = 0; k < 4; ++k) {
+        const float ox = redm[k][threadIdx.x][e], oy = reds[k][threadIdx.x][e];
+        const float mx = fmaxf(mm, ox);
+        if (mx > -INFINITY) {
+          ss = ss * expf(mm - mx) + oy * expf(ox - mx);
+          mm = mx;
+        }
+      }
+      part[((long long)b * gridDim.y + blockIdx.y) * N + c + e] = make_float2(mm, ss);
+    }
+  }
+}
 __global__ __launch_bounds__(256) void sim_lse_col_final_kernel(const float2* part, int nch, int B, int N, float* lsec) {
   const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
   if (id >= (long long)B * N) return;
@@ -1366,11 +1407,24 @@ __global__ __launch_bounds__(256) void sim_lse_row_kernel(const float* sim, int 
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
   if (row >= rows) return;
   const float* s = sim + (long long)row * N;
-  float m = -INFINITY;
-  for (int j = l; j < N; j += 64) m = fmaxf(m, s[j]);
-  m = wave_max(m);
-  float acc = 0.f;
-  for (int j = l; j < N; j += 64) acc += expf(s[j] - m);
+  float m = -INFINITY, acc = 0.f;
+  if (N <= 2048) {  // the row read once into registers; the same operations in the same order
+    float x[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int j = l + 64 * q;
+      x[q] = j < N ? s[j] : -INFINITY;
+      m = fmaxf(m, x[q]);
+    }
+    m = wave_max(m);
+#pragma unroll
+    for (int q = 0; q < 32; ++q)
+      if (l + 64 * q < N) acc += expf(x[q] - m);
+  } else {
+    for (int j = l; j < N; j += 64) m = fmaxf(m, s[j]);
+    m = wave_max(m);
+    for (int j = l; j < N; j += 64) acc += expf(s[j] - m);
+  }
   acc = wave_sum(acc);
   if (l == 0) lser[row] = m + logf(acc);
 }
@@ -1442,6 +1496,40 @@ __global__ __launch_bounds__(256) void la_forward_kernel(const float* sim, const
   } else {
     for (int j = threadIdx.x; j < N; j += 256) out[j] = log_sigmoid(-zb[j]);
     if (threadIdx.x == 0) out[N] = 0.f;
+  }
+}
+
+// the same with LA_R rows of one pair per workgroup (N <= LA_NMAX): the column terms lsec and
+// logsigmoid(z1) staged once in LDS instead of a logsigmoid per element; identical arithmetic
+constexpr int LA_R = 8, LA_NMAX = 4096;
+__global__ __launch_bounds__(256) void la_forward_rows_kernel(const float* sim, const float* lser, const float* lsec,
+                                                              const float* z0, const float* z1, int B, int M, int N,
+                                                              float* la) {
+  __shared__ float lc_s[LA_NMAX], ls_s[LA_NMAX];
+  const int b = blockIdx.y, i0 = blockIdx.x * LA_R, i1 = min(M + 1, i0 + LA_R);
+  const float* zb = z1 + (long long)b * N;
+  const float* lcb = lsec + (long long)b * N;
+  for (int j = threadIdx.x; j < N; j += 256) {
+    lc_s[j] = lcb[j];
+    ls_s[j] = log_sigmoid(zb[j]);
+  }
+  __syncthreads();
+  for (int i = i0; i < i1; ++i) {
+    float* out = la + ((long long)b * (M + 1) + i) * (N + 1);
+    if (i < M) {
+      const long long ri = (long long)b * M + i;
+      const float* s = sim + ri * N;
+      const float lr = lser[ri], l0 = log_sigmoid(z0[ri]);
+      for (int j = threadIdx.x; j < N; j += 256) {
+        const float x = s[j];
+        const float cert = l0 + ls_s[j];
+        out[j] = ((x - lr) + (x - lc_s[j])) + cert;
+      }
+      if (threadIdx.x == 0) out[N] = log_sigmoid(-z0[ri]);
+    } else {
+      for (int j = threadIdx.x; j < N; j += 256) out[j] = log_sigmoid(-zb[j]);
+      if (threadIdx.x == 0) out[N] = 0.f;
+    }
   }
 }
 
@@ -1765,7 +1853,10 @@ hipError_t sim_lse(const float* sim, int B, int M, int N, float* lser, float* ls
   hipLaunchKernelGGL(sim_lse_row_kernel, dim3(cdiv((long long)B * M, 4)), dim3(256), 0, st, sim, B * M, N, lser);
   const int nch = (int)cdiv(M, LSE_ROWS);
   float2* p2 = reinterpret_cast<float2*>(part);
-  hipLaunchKernelGGL(sim_lse_col_part_kernel, dim3(cdiv(N, 64), nch, B), dim3(256), 0, st, sim, M, N, p2);
+  if (N % 4 == 0 && (reinterpret_cast<uintptr_t>(sim) & 15) == 0)
+    hipLaunchKernelGGL(sim_lse_col_part4_kernel, dim3(cdiv(N, 256), nch, B), dim3(256), 0, st, sim, M, N, p2);
+  else
+    hipLaunchKernelGGL(sim_lse_col_part_kernel, dim3(cdiv(N, 64), nch, B), dim3(256), 0, st, sim, M, N, p2);
   hipLaunchKernelGGL(sim_lse_col_final_kernel, dim3(cdiv((long long)B * N, 256)), dim3(256), 0, st, p2, nch, B, N, lsec);
   return hipGetLastError();
 }
@@ -1810,7 +1901,11 @@ hipError_t la_forward(const float* sim, const float* lser, const float* lsec, co
                       int N, float* la, hipStream_t st) {
   const long long n = (long long)B * (M + 1) * (N + 1);
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(la_forward_kernel, dim3(B * (M + 1)), dim3(256), 0, st, sim, lser, lsec, z0, z1, B, M, N, la);
+  if (N <= LA_NMAX)
+    hipLaunchKernelGGL(la_forward_rows_kernel, dim3(cdiv(M + 1, LA_R), B), dim3(256), 0, st, sim, lser, lsec, z0, z1, B, M,
+                       N, la);
+  else
+    hipLaunchKernelGGL(la_forward_kernel, dim3(B * (M + 1)), dim3(256), 0, st, sim, lser, lsec, z0, z1, B, M, N, la);
   return hipGetLastError();
 }
 

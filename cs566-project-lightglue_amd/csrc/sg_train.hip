@@ -9,6 +9,7 @@
 // one image set (the reference's [b, C, n] batch statistics over (b, n)).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 #include "train.h"
@@ -382,7 +383,10 @@ __global__ void sk_col_final_kernel(const float* part, int B, int N1, int nch, f
 // pr_ij (u_t's weights), the in-place gC -= gv_j pc + gu_i pr, and the wave's column sums of
 // gu_i pr, combined over the four waves in order and written per workgroup: d/d v_{t-1} is then
 // minus the ordered sum of the partials (sk_bwd_colsum_kernel).  Against the row + column pair of
-// passes: C is read once instead of twice per step and pc is not recomputed.
+// passes: C is read once instead of twice per step.  The C and gC rows are loaded unconditionally
+// (columns past N1 read the next row or the 64 floats of slack every couplings-shaped buffer
+// carries, and are never used) so all 66 loads are in flight at once; pc is recomputed rather
+// than kept, which holds the kernel at two waves per SIMD.
 constexpr int SKF_Q = 33, SKF_R = 32;
 
 __global__ __launch_bounds__(256) void sk_bwd_fused_kernel(const float* Cc, int M1, int N1, const float* u,
@@ -408,22 +412,17 @@ __global__ __launch_bounds__(256) void sk_bwd_fused_kernel(const float* Cc, int 
     const float* c = Cc + row * N1;
     float* g = gC + row * N1;
     const float ui = u[row], lmu = i < M1 - 1 ? norm : lmu_last;
-    float x[SKF_Q], pc[SKF_Q], gx[SKF_Q];  // the gC row is read with C (its latency under the sums)
+    float x[SKF_Q], gx[SKF_Q];  // the gC row is read with C (its latency under the sums)
     float acc = 0.f;
 #pragma unroll
-    for (int q = 0; q < SKF_Q; ++q) {
-      const int j = l + 64 * q;
-      x[q] = j < N1 ? c[j] : 0.f;
-      gx[q] = j < N1 ? g[j] : 0.f;
+    for (int q = 0; q < SKF_Q; ++q) {  // unconditional loads (one base, immediate offsets): all in flight
+      x[q] = c[l + 64 * q];             // past the row end: the next row / the buffers' 64-float slack,
+      gx[q] = g[l + 64 * q];            // never used
     }
 #pragma unroll
     for (int q = 0; q < SKF_Q; ++q) {
       const int j = l + 64 * q;
-      pc[q] = 0.f;
-      if (j < N1) {
-        pc[q] = exp_fast(x[q] + ui + v_s[j] - (j < N1 - 1 ? norm : lnu_last));
-        acc = fmaf(gv_s[j], pc[q], acc);
-      }
+      if (j < N1) acc = fmaf(gv_s[j], exp_fast(x[q] + ui + v_s[j] - (j < N1 - 1 ? norm : lnu_last)), acc);
     }
     acc = wave_sum(acc);
     const float gui = (base ? base[row] : 0.f) - acc;
@@ -433,8 +432,9 @@ __global__ __launch_bounds__(256) void sk_bwd_fused_kernel(const float* Cc, int 
       const int j = l + 64 * q;
       if (j < N1) {
         const float pr = exp_fast(x[q] + vp_s[j] + ui - lmu);
+        const float pc = exp_fast(x[q] + ui + v_s[j] - (j < N1 - 1 ? norm : lnu_last));  // recomputed: registers
         cs[q] = fmaf(gui, pr, cs[q]);
-        g[j] = gx[q] - fmaf(gv_s[j], pc[q], gui * pr);
+        g[j] = gx[q] - fmaf(gv_s[j], pc, gui * pr);
       }
     }
   }
@@ -443,6 +443,85 @@ __global__ __launch_bounds__(256) void sk_bwd_fused_kernel(const float* Cc, int 
   __syncthreads();
   float* pp = part + ((long long)b * gridDim.x + blockIdx.x) * N1;
   for (int j = threadIdx.x; j < N1; j += 256) pp[j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+}
+
+// One forward iteration in ONE read of C (N1 <= 64 SKF_Q; the eval path's scaled column
+// statistics, sinkhorn.hip): a wave holds row i of C + v_{t-1} in registers, takes its max m_i and
+// s_i = sum_j e_ij with e_ij = exp(C_ij + v_{t-1,j} - m_i) <= 1 and writes
+// u_i = lmu_i - (m_i + log s_i); with a_i = exp(lmu_i) / s_i, e_ij a_i = exp(C_ij + u_i + v_{t-1,j}),
+// so the column statistic is the plain sum S_j = sum_i e_ij a_i (no per-column max, no second
+// exponential) and v_j = lnu_j + v_{t-1,j} - log S_j.  e_ij a_i <= exp(lmu_i) never overflows; a
+// column whose S_j falls below 1e-20 (underflowed terms could matter) is recomputed exactly by
+// sk_fwd_colfinal_kernel.  Partials per workgroup as in the backward.
+__global__ __launch_bounds__(256) void sk_fwd_fused_kernel(const float* Cc, int M1, int N1, const float* vprev,
+                                                           float norm, float lmu_last, float* u_out, float* part) {
+  __shared__ float v_s[64 * SKF_Q];
+  __shared__ float red[4][64 * SKF_Q];
+  const int b = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const long long pb = (long long)b * N1;
+  for (int j = threadIdx.x; j < N1; j += 256) v_s[j] = vprev[pb + j];
+  __syncthreads();
+  float cs[SKF_Q];
+#pragma unroll
+  for (int q = 0; q < SKF_Q; ++q) cs[q] = 0.f;
+  const int i0 = blockIdx.x * SKF_R, i1 = min(M1, i0 + SKF_R);
+  for (int i = i0 + w; i < i1; i += 4) {
+    const long long row = (long long)b * M1 + i;
+    const float* c = Cc + row * N1;
+    const float lmu = i < M1 - 1 ? norm : lmu_last;
+    float x[SKF_Q];
+    float m = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < SKF_Q; ++q) x[q] = c[l + 64 * q];  // unconditional (slack past the end), all in flight
+#pragma unroll
+    for (int q = 0; q < SKF_Q; ++q) {
+      const int j = l + 64 * q;
+      x[q] = j < N1 ? x[q] + v_s[j] : -INFINITY;
+      m = fmaxf(m, x[q]);
+    }
+    m = wave_max(m);
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < SKF_Q; ++q) {
+      x[q] = exp_fast(x[q] - m);  // 0 on the padding
+      sum += x[q];
+    }
+    sum = wave_sum(sum);
+    if (l == 0) u_out[row] = lmu - (m + logf(sum));
+    const float a = expf(lmu) / sum;
+#pragma unroll
+    for (int q = 0; q < SKF_Q; ++q) cs[q] = fmaf(x[q], a, cs[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < SKF_Q; ++q) red[w][l + 64 * q] = cs[q];
+  __syncthreads();
+  float* pp = part + ((long long)b * gridDim.x + blockIdx.x) * N1;
+  for (int j = threadIdx.x; j < N1; j += 256) pp[j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+}
+
+// v_j = lnu_j + v_{t-1,j} - log(ordered sum of the partials); exact two-pass LSE_i(C_ij + u_i) over
+// the column when that sum is below thr (1e-20; LG_SKF_EXACT=1 in the environment: every column,
+// which is how the tests reach this path -- the dustbin row keeps S_j near 1 / (M + N) in practice)
+__global__ void sk_fwd_colfinal_kernel(const float* part, const float* Cc, const float* u, const float* vprev, int B,
+                                       int M1, int N1, int nwg, float norm, float lnu_last, float thr, float* v) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)B * N1) return;
+  const int b = (int)(t / N1), j = (int)(t - (long long)b * N1);
+  const float* p = part + (long long)b * nwg * N1 + j;
+  float S = 0.f;
+  for (int k = 0; k < nwg; ++k) S += p[(long long)k * N1];
+  const float lnu = j < N1 - 1 ? norm : lnu_last;
+  if (S >= thr) {
+    v[t] = lnu + vprev[t] - logf(S);
+    return;
+  }
+  const float* c = Cc + (long long)b * M1 * N1 + j;
+  const float* ub = u + (long long)b * M1;
+  float mx = -INFINITY;
+  for (int i = 0; i < M1; ++i) mx = fmaxf(mx, c[(long long)i * N1] + ub[i]);
+  float s = 0.f;
+  for (int i = 0; i < M1; ++i) s += expf(c[(long long)i * N1] + ub[i] - mx);
+  v[t] = lnu - (mx + logf(s));
 }
 
 // d/d v_{t-1}[b][j] = -(ordered sum over the workgroups' partials)
@@ -605,7 +684,10 @@ hipError_t head_gather(const float* src, int rows, int cols, bool by_cols, bool 
   return hipGetLastError();
 }
 
-size_t sk_train_part_floats(int B, int M, int N) { return sk_col_part_floats(B, M, N); }
+static bool skf_ok(int N1) { return N1 <= 64 * SKF_Q; }
+static size_t skf_part_floats(int B, int M, int N) { return (size_t)B * cdiv(M + 1, SKF_R) * (N + 1); }
+
+size_t sk_train_part_floats(int B, int M, int N) { return std::max(sk_col_part_floats(B, M, N), skf_part_floats(B, M, N)); }
 
 hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M, int N, int iters, float* Cc, float* U,
                             float* V, float* Z, float* part, hipStream_t st) {
@@ -614,10 +696,19 @@ hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M,
     hipLaunchKernelGGL(sk_couplings_kernel, dim3(B * M1), dim3(256), 0, st, cost, alpha, B, M, N, Cc);
   hipError_t e = hipMemsetAsync(V, 0, (size_t)B * N1 * sizeof(float), st);  // v_0 = 0 (:175)
   if (e != hipSuccess) return e;
+  const char* ex = getenv("LG_SKF_EXACT");
+  const float thr = ex && atoi(ex) ? INFINITY : 1e-20f;
   for (int t = 1; t <= iters; ++t) {
     float* u = U + (size_t)(t - 1) * B * M1;
     const float* vprev = V + (size_t)(t - 1) * B * N1;
     float* v = V + (size_t)t * B * N1;
+    if (skf_ok(N1)) {  // both halves of the iteration in one pass over C
+      const unsigned nwg = cdiv(M1, SKF_R);
+      hipLaunchKernelGGL(sk_fwd_fused_kernel, dim3(nwg, B), dim3(256), 0, st, Cc, M1, N1, vprev, norm, lmu_last, u, part);
+      hipLaunchKernelGGL(sk_fwd_colfinal_kernel, dim3(cdiv((long long)B * N1, 256)), dim3(256), 0, st, part, Cc, u, vprev,
+                         B, M1, N1, (int)nwg, norm, lnu_last, thr, v);
+      continue;
+    }
     hipLaunchKernelGGL(sk_row_kernel, dim3(cdiv((long long)B * M1, 4)), dim3(256), 0, st, Cc, B, M1, N1, nullptr, vprev,
                        nullptr, nullptr, norm, lmu_last, lnu_last, 0, u);
     sk_col(Cc, B, M1, N1, u, nullptr, nullptr, nullptr, nullptr, nullptr, norm, lmu_last, lnu_last, 0, part, v, st);
@@ -632,9 +723,6 @@ hipError_t sk_train_forward(const float* cost, const float* alpha, int B, int M,
                      Z);
   return hipGetLastError();
 }
-
-static bool skf_ok(int N1) { return N1 <= 64 * SKF_Q; }
-static size_t skf_part_floats(int B, int M, int N) { return (size_t)B * cdiv(M + 1, SKF_R) * (N + 1); }
 
 size_t sk_train_scratch_floats(int B, int M, int N) {
   return (size_t)B * (M + 1) * (N + 1) + 4 * (size_t)B * (M + N + 2) + B +

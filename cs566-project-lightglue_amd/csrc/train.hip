@@ -1411,9 +1411,10 @@ __global__ __launch_bounds__(256) void sim_lse_row_kernel(const float* sim, int 
   if (N <= 2048) {  // the row read once into registers; the same operations in the same order
     float x[32];
 #pragma unroll
+    for (int q = 0; q < 32; ++q) x[q] = s[min(l + 64 * q, N - 1)];  // unconditional: all in flight
+#pragma unroll
     for (int q = 0; q < 32; ++q) {
-      const int j = l + 64 * q;
-      x[q] = j < N ? s[j] : -INFINITY;
+      if (l + 64 * q >= N) x[q] = -INFINITY;
       m = fmaxf(m, x[q]);
     }
     m = wave_max(m);

@@ -125,6 +125,36 @@ def test_sg_training_step_ragged_against_oracle(B, M, N, layers, iters):
     assert all(v == (4 if n.startswith("gnn.") else 2) for n, v in nbt.items())
 
 
+def test_sg_training_sinkhorn_column_fallback(monkeypatch):
+    """The fused Sinkhorn iteration's column statistic S_j = sum_i e_ij a_i falls back to an exact
+    two-pass LSE over the column when S_j is tiny (sk_fwd_colfinal_kernel); LG_SKF_EXACT=1 takes
+    that path for every column.  Both runs match the float64 oracle's log assignment and
+    gradients (the ragged test's bars) and each other's log assignment."""
+    from lightglue_amd.sg_weights import superglue_state_dict, synthetic_scores
+    from lightglue_amd.weights import synthetic_pair
+
+    conf = {"GNN_layers": ["self", "cross"], "num_sinkhorn_iterations": 12, "keypoint_encoder": [16, 32]}
+    sd = superglue_state_dict(conf, seed=31)
+    B, M, N = 2, 45, 61
+    p = synthetic_pair(B, M, N, seed=32, width=640, height=480)
+    data = {"keypoints0": p["keypoints0"], "keypoints1": p["keypoints1"], "descriptors0": p["descriptors0"],
+            "descriptors1": p["descriptors1"], "keypoint_scores0": synthetic_scores(B, M, seed=33),
+            "keypoint_scores1": synthetic_scores(B, N, seed=34), "image_hw": (480, 640)}
+    gt = ground_truth(B, M, N, 35)
+    fused = gpu_step(conf, sd, data, gt)
+    monkeypatch.setenv("LG_SKF_EXACT", "1")
+    exact = gpu_step(conf, sd, data, gt)
+    _, og, _, _, _, ola = oracle_sg_step(conf, sd, data, gt)
+    _, og32, _, _, _, ola32 = oracle_sg_step(conf, sd, data, gt, dtype=torch.float32)
+    spread = float(np.abs(ola32.double().numpy() - ola.numpy()).max())
+    for run in (fused, exact):
+        np.testing.assert_allclose(run[6], ola.numpy(), atol=max(1e-5, 8 * spread), rtol=0)
+        for n, ref in og.items():  # the ragged test's bar, per run
+            tol = 8 * float(np.abs(og32[n] - ref).max()) + 1e-6 * float(np.abs(ref).max()) + 1e-12
+            assert float(np.abs(run[1][n] - ref).max()) <= tol, n
+    np.testing.assert_allclose(fused[6], exact[6], atol=max(1e-5, 8 * spread), rtol=0)
+
+
 def test_nll_losses_are_differentiable():
     """SuperGlue.loss (mode 0) and NLLLoss (mode 1) backward (sg_nll_backward) against torch autograd
     of the oracle restatements (float64), including gradients of nll_pos / nll_neg."""

@@ -335,7 +335,8 @@ __device__ __forceinline__ void load_head_row_frag(const float* row, int h, floa
 // registers and lands between two barriers.
 __device__ __forceinline__ int x6_sw(int row, int chunk) { return (chunk ^ (row & 7)) * 8; }
 
-__global__ __launch_bounds__(256, 2) void tattn_fwd_x6_kernel(TAttn a) {
+template <int W>  // waves per workgroup (32 queries each): every K / V tile is split once per workgroup
+__global__ __launch_bounds__(64 * W, 8 / W) void tattn_fwd_x6_kernel(TAttn a) {
   __shared__ __attribute__((aligned(16))) __bf16 Kp[3][64 * 64];
   __shared__ __attribute__((aligned(16))) __bf16 Vt[3][64 * 64];
   const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, l32 = l & 31;
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(256, 2) void tattn_fwd_x6_kernel(TAttn a) {
   const float* Q = a.Q + (long long)b * a.Nq * a.ldq + hd * 64;
   const float* K = a.K + (long long)b * a.Nk * a.ldk + hd * 64;
   const float* V = a.V + (long long)b * a.Nk * a.ldv + hd * 64;
-  const int qrow = blockIdx.x * 128 + w * 32 + l32;
+  const int qrow = blockIdx.x * (32 * W) + w * 32 + l32;
   const bool qv = qrow < a.Nq;
   const float c = a.scale * kLog2e;
   bf16x8 qf[4][3];  // dims 16 ks + 8 h .. +7 of this lane's query, three pieces
@@ -364,21 +365,24 @@ __global__ __launch_bounds__(256, 2) void tattn_fwd_x6_kernel(TAttn a) {
       qf[ks][2][e] = x2;
     }
   }
-  // staging: K row t >> 2, dims 16 (t & 3) ..; V^T row (dim) t & 63, key chunks 2 (t >> 6), +1
-  const int kr = t >> 2, kc = t & 3, vd = t & 63, vc = 2 * (t >> 6);
-  f32x4 rk[4];
-  float rv[16];
+  // staging, a 64-key tile per step:
+  // W = 4: K row t >> 2, dims 16 (t & 3) ..; V^T row (dim) t & 63, key chunks 2 (t >> 6), +1
+  // W = 8: K row t >> 3, dims 8 (t & 7) ..;  V^T row (dim) t & 63, key chunk t >> 6
+  constexpr int KQ = 16 / W, VC = 8 / W;  // float4 loads of K per thread, V^T chunks per thread
+  const int kr = t / (16 / KQ), kc = t % (16 / KQ), vd = t & 63, vc = VC * (t >> 6);
+  f32x4 rk[KQ];
+  float rv[8 * VC];
   auto chunk_key = [](int ch, int e) {  // key (within the tile) of element e of V^T chunk ch
     return 32 * (ch >> 2) + row32(8 * ((ch >> 1) & 1) + e, ch & 1);
   };
   auto gload = [&](int kt) {
     const int key = kt * 64 + kr;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      rk[q] = key < a.Nk ? *reinterpret_cast<const f32x4*>(K + (long long)key * a.ldk + 16 * kc + 4 * q)
+    for (int q = 0; q < KQ; ++q)
+      rk[q] = key < a.Nk ? *reinterpret_cast<const f32x4*>(K + (long long)key * a.ldk + 4 * KQ * kc + 4 * q)
                          : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc)
+    for (int cc = 0; cc < VC; ++cc)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int k2 = kt * 64 + chunk_key(vc + cc, e);
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(256, 2) void tattn_fwd_x6_kernel(TAttn a) {
   };
   auto sstore = [&]() {
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
+    for (int hh = 0; hh < KQ / 2; ++hh) {
       bf16x8 p0, p1, p2;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -397,13 +401,13 @@ __global__ __launch_bounds__(256, 2) void tattn_fwd_x6_kernel(TAttn a) {
         p1[e] = x1;
         p2[e] = x2;
       }
-      const int off = kr * 64 + x6_sw(kr, 2 * kc + hh);
+      const int off = kr * 64 + x6_sw(kr, (KQ / 2) * kc + hh);
       *reinterpret_cast<bf16x8*>(&Kp[0][off]) = p0;
       *reinterpret_cast<bf16x8*>(&Kp[1][off]) = p1;
       *reinterpret_cast<bf16x8*>(&Kp[2][off]) = p2;
     }
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
+    for (int cc = 0; cc < VC; ++cc) {
       bf16x8 p0, p1, p2;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -1672,6 +1676,9 @@ hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, 
   return hipGetLastError();
 }
 
+#ifndef LG_TA_W
+#define LG_TA_W 8  // waves per workgroup of tattn_fwd_x6_kernel (4 or 8)
+#endif
 #ifndef LG_TA_X6
 #define LG_TA_X6 1  // the training attention forward on bf16x6 (tattn_fwd_x6_kernel); 0: f32 MFMA
 #endif
@@ -1686,7 +1693,10 @@ static bool ta_x6_enabled() {
 hipError_t tattn_forward(const TAttn& a, hipStream_t st) {
   if (a.B * a.H == 0 || a.Nq == 0) return hipSuccess;
   if (ta_x6_enabled() && a.Nk > 0) {
-    hipLaunchKernelGGL(tattn_fwd_x6_kernel, dim3(cdiv(a.Nq, 128), a.B * a.H), dim3(256), 0, st, a);
+    if (LG_TA_W == 8)
+      hipLaunchKernelGGL(tattn_fwd_x6_kernel<8>, dim3(cdiv(a.Nq, 256), a.B * a.H), dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL(tattn_fwd_x6_kernel<4>, dim3(cdiv(a.Nq, 128), a.B * a.H), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(tattn_fwd_kernel, dim3(cdiv(a.Nq, 128), a.B * a.H), dim3(256), 0, st, a);

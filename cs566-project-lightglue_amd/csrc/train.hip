@@ -1525,10 +1525,21 @@ __global__ __launch_bounds__(256) void la_forward_rows_kernel(const float* sim, 
       const long long ri = (long long)b * M + i;
       const float* s = sim + ri * N;
       const float lr = lser[ri], l0 = log_sigmoid(z0[ri]);
-      for (int j = threadIdx.x; j < N; j += 256) {
-        const float x = s[j];
-        const float cert = l0 + ls_s[j];
-        out[j] = ((x - lr) + (x - lc_s[j])) + cert;
+      if (N <= 2048) {  // the thread's 8 values loaded together (clamped column), then written
+        float xv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xv[k] = s[min((int)threadIdx.x + 256 * k, N - 1)];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int j = threadIdx.x + 256 * k;
+          if (j < N) out[j] = ((xv[k] - lr) + (xv[k] - lc_s[j])) + (l0 + ls_s[j]);
+        }
+      } else {
+        for (int j = threadIdx.x; j < N; j += 256) {
+          const float x = s[j];
+          const float cert = l0 + ls_s[j];
+          out[j] = ((x - lr) + (x - lc_s[j])) + cert;
+        }
       }
       if (threadIdx.x == 0) out[N] = log_sigmoid(-z0[ri]);
     } else {

@@ -30,6 +30,7 @@ the NLL of each head into its head's backward (no dense d(loss)/d(log_assignment
 Gradients reach every parameter and both descriptor inputs.
 """
 import ctypes
+import os
 import warnings
 from pathlib import Path
 
@@ -296,6 +297,30 @@ class _HeadNLL(torch.autograd.Function):
         needs = list(ctx.needs_input_grad[7:]) + [ctx.needs_input_grad[5], ctx.needs_input_grad[6]]
         gd0, gd1, grads = _head_backward(ctx.model, ctx.layer, d0, d1, params, needs, w, s_in, s_dust, None, g_t0, g_t1)
         return (None, None, None, None, None, gd0, gd1, *grads)
+
+
+class _LayerSlices(torch.autograd.Function):
+    """``rd`` [B, L, M, D] -> the L layer slices [B, M, D], each contiguous (what the heads take).
+    Backward writes the slice gradients into one [B, L, M, D] tensor; indexing ``rd[:, i]`` per head
+    instead lets autograd zero-fill a full [B, L, M, D] gradient for every slice and add them up."""
+
+    @staticmethod
+    def forward(ctx, rd):
+        ctx.shape = rd.shape
+        return tuple(rd[:, i].contiguous() for i in range(rd.shape[1]))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ref = next((g for g in grads if g is not None), None)
+        if ref is None:
+            return None
+        out = ref.new_empty(ctx.shape)
+        for i, g in enumerate(grads):
+            if g is None:
+                out[:, i].zero_()
+            else:
+                out[:, i].copy_(g)
+        return out
 
 
 class LightGlue(nn.Module):
@@ -764,8 +789,13 @@ class LightGlue(nn.Module):
         # the ground truth's loss weights (losses.py:62-73) once, as the reference (gt_weights, :633)
         gt = (data, nll_weights(rd0.new_empty((b, m + 1, n + 1)), data), nll_inputs(data, rd0.device))
 
+        if os.environ.get("LG_LAYER_SLICES", "1") != "0":
+            sl0, sl1 = _LayerSlices.apply(rd0), _LayerSlices.apply(rd1)
+        else:
+            sl0, sl1 = [rd0[:, i] for i in range(N)], [rd1[:, i] for i in range(N)]
+
         def head(i, tokens):
-            return _HeadNLL.apply(self, i, gt, bal, tokens, rd0[:, i], rd1[:, i], *params)
+            return _HeadNLL.apply(self, i, gt, bal, tokens, sl0[i], sl1[i], *params)
 
         nll, nll_pos, nll_neg, num_pos, num_neg, _, _, _ = head(-1, False)
         losses = {"total": nll, "last": nll.clone().detach(), "assignment_nll": nll, "nll_pos": nll_pos,

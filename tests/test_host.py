@@ -229,3 +229,21 @@ def test_bench_training_ground_truth_is_one_to_one():
     frac = float((m0 > -1).float().mean())
     assert 0.45 < frac < 0.8
     assert bench.train_flops_per_pair(2048) > 3 * 9 * 76 * 2048 * 256 * 256
+
+
+def test_layer_slices_gradient_matches_indexing():
+    """lightglue._LayerSlices (loss(): the per-layer head inputs) gives the same slices and the same
+    [B, L, M, D] gradient as indexing rd[:, i], including layers whose slice gets no gradient."""
+    import torch
+    from lightglue_amd.lightglue import _LayerSlices
+
+    g = torch.Generator().manual_seed(3)
+    rd = torch.randn(2, 4, 5, 3, generator=g, dtype=torch.float64)
+    r = [torch.randn(2, 5, 3, generator=g, dtype=torch.float64) for _ in range(4)]
+    a = rd.clone().requires_grad_()
+    sl = _LayerSlices.apply(a)
+    assert all(s.is_contiguous() and torch.equal(s, rd[:, i]) for i, s in enumerate(sl))
+    sum((sl[i] * r[i]).sum() * (i + 1) for i in (0, 1, 3)).backward()  # layer 2 unused
+    b = rd.clone().requires_grad_()
+    sum((b[:, i] * r[i]).sum() * (i + 1) for i in (0, 1, 3)).backward()
+    assert torch.equal(a.grad, b.grad)

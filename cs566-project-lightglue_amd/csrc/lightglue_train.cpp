@@ -6,6 +6,7 @@
 // Row space: R = B (M + N) rows of 256 -- image-0 rows (pair-major, R0 = B M of them) then image-1
 // rows -- as in the eval forward.  Every activation is row-major fp32; head h of a projection is
 // columns [64h, 64h + 64).
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,6 +24,16 @@ int handle_device(const lg_handle* h);
 int handle_weight_index(const lg_handle* h, const std::string& name);
 }  // namespace lg
 
+#ifndef LG_HEAD_SIM_X6
+#define LG_HEAD_SIM_X6 1  // the heads' similarity md0 md1^T on the bf16x6 GEMM (env LG_HEAD_SIM_X6 overrides)
+#endif
+static bool head_sim_x6() {
+  static const int v = [] {
+    const char* e = getenv("LG_HEAD_SIM_X6");
+    return e ? atoi(e) : LG_HEAD_SIM_X6;
+  }();
+  return v != 0;
+}
 #ifndef LG_HEAD_X6
 #define LG_HEAD_X6 0  // 1: the assignment heads' products may take the bf16x6 GEMM too
 #endif
@@ -544,7 +555,7 @@ int lg_head_backward(lg_handle_t* h, const float* const* params, int32_t layer, 
   TR_HIP(gemv256(s.X, R, wm, P.w(a + ".matchability.bias"), s.Z, c.st));
   {
     TGemm g{s.MD, s.MD + o1, s.SIM, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B, 1.f, 0.f, nullptr};
-    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st, c.x6));
+    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st, head_sim_x6() ? 2 : (int)c.x6));
   }
   TR_HIP(sim_lse(s.SIM, B, M, N, s.LSER, s.LSEC, c.part, c.st));
   // sigmoid_log_double_softmax backward (:284-296)
@@ -610,7 +621,7 @@ int lg_head_forward(lg_handle_t* h, const float* const* params, int32_t layer, c
   TR_HIP(gemv256(s.X, R, P.w(a + ".matchability.weight"), P.w(a + ".matchability.bias"), s.Z, c.st));
   {
     TGemm g{s.MD, s.MD + o1, sim, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B, 1.f, 0.f, nullptr};
-    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st, c.x6));
+    TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st, head_sim_x6() ? 2 : (int)c.x6));
   }
   TR_HIP(sim_lse(sim, B, M, N, s.LSER, s.LSEC, c.part, c.st));
   TR_HIP(la_forward(sim, s.LSER, s.LSEC, s.Z, s.Z + R0, B, M, N, log_assignment, c.st));

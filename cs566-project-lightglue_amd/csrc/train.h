@@ -28,7 +28,8 @@ struct TGemm {
 };
 size_t tgemm_ws_floats(int M, int N, int K, int batch);
 // x6: allow the bf16x6 route for k-contiguous products (train.hip tgemm_x6); false = f32 MFMA only
-hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st, bool x6 = true);
+// x6: 0 f32 MFMA only; 1 the bf16x6 routes the build enables (LG_TG_X6*); 2 also A B^T forms (tb)
+hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st, int x6 = 1);
 
 // Attention on row-major fp32 tensors (row stride ld*, head h at columns [64h, 64h+64)); item
 // (b, h): queries rows [b*Nq, (b+1)*Nq) of Q, keys / values rows [b*Nk, (b+1)*Nk) of K / V.

@@ -1613,9 +1613,10 @@ static bool tg_x6_enabled() {
 // `ws` -- go to gemm.hip's bf16x6 kernel: both fp32 operands split into three bf16 pieces, six
 // v_mfma_f32_32x32x16_bf16 per 32 x 32 x 16 block (the fp32-accurate product of common.h at
 // 2.5 PF/s bf16 instead of the 157 TF/s f32 MFMA); error per product ~2^-24 like an f32 fma chain.
-static bool tgemm_x6(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st, hipError_t& err) {
+static bool tgemm_x6(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st, int mode,
+                     hipError_t& err) {
   if (!tg_x6_enabled() || ta || g.K < 16 || g.K % 16 || (g.beta != 0.f && g.beta != 1.f)) return false;
-  if (tb && !LG_TG_X6_FWD) return false;
+  if (tb && !LG_TG_X6_FWD && mode < 2) return false;
   auto al = [](const void* ptr, long long ld, long long sb) {
     return ((uintptr_t)ptr % 16 == 0) && ld % 4 == 0 && sb % 4 == 0;
   };
@@ -1652,10 +1653,10 @@ static bool tgemm_x6(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floa
   return true;
 }
 
-hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st, bool x6) {
+hipError_t tgemm(const TGemm& g, bool ta, bool tb, float* ws, size_t ws_floats, hipStream_t st, int x6) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return hipSuccess;
   hipError_t xe = hipSuccess;
-  if (x6 && tgemm_x6(g, ta, tb, ws, ws_floats, st, xe)) return xe;
+  if (x6 && tgemm_x6(g, ta, tb, ws, ws_floats, st, x6, xe)) return xe;
   TGemmK p{};
   p.g = g;
   int kc = 0;

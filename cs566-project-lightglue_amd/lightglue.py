@@ -30,7 +30,6 @@ the NLL of each head into its head's backward (no dense d(loss)/d(log_assignment
 Gradients reach every parameter and both descriptor inputs.
 """
 import ctypes
-import os
 import warnings
 from pathlib import Path
 
@@ -789,10 +788,7 @@ class LightGlue(nn.Module):
         # the ground truth's loss weights (losses.py:62-73) once, as the reference (gt_weights, :633)
         gt = (data, nll_weights(rd0.new_empty((b, m + 1, n + 1)), data), nll_inputs(data, rd0.device))
 
-        if os.environ.get("LG_LAYER_SLICES", "1") != "0":
-            sl0, sl1 = _LayerSlices.apply(rd0), _LayerSlices.apply(rd1)
-        else:
-            sl0, sl1 = [rd0[:, i] for i in range(N)], [rd1[:, i] for i in range(N)]
+        sl0, sl1 = _LayerSlices.apply(rd0), _LayerSlices.apply(rd1)
 
         def head(i, tokens):
             return _HeadNLL.apply(self, i, gt, bal, tokens, sl0[i], sl1[i], *params)

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -198,11 +199,22 @@ struct Ctx {
   float* part;
 };
 
+#ifndef SG_TG_X6_FWD
+#define SG_TG_X6_FWD 1  // SuperGlue's forward products (x W^T, the cost) on bf16x6; env SG_TG_X6_FWD overrides
+#endif
+int fwd_x6() {
+  static const int v = [] {
+    const char* e = getenv("SG_TG_X6_FWD");
+    return e ? atoi(e) : SG_TG_X6_FWD;
+  }();
+  return v ? 2 : 1;
+}
+
 // y[rows,N] = alpha (x[rows,K] W[N,K]^T + b) + beta y
 hipError_t linear(const Ctx& c, const float* x, long long ldx, int rows, int K, const float* W, const float* b, int N,
                   float* y, long long ldy, float beta = 0.f) {
   TGemm g{x, W, y, ldx, K, ldy, 0, 0, 0, rows, N, K, 1, 1.f, beta, b};
-  return tgemm(g, false, true, c.ws, c.ws_floats, c.st);
+  return tgemm(g, false, true, c.ws, c.ws_floats, c.st, fwd_x6());
 }
 // dx[rows,K] (+)= dy[rows,N] W[N,K]
 hipError_t linear_dgrad(const Ctx& c, const float* dy, long long lddy, int rows, int N, const float* W, int K, float* dx,
@@ -354,7 +366,7 @@ int sg_train_forward(sg_handle_t* h, float* const* params, const sg_inputs_t* in
   {
     TGemm g{s.MD, s.MD + o1 * D, s.COST, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B,
             1.f / 16.f, 0.f, nullptr};
-    ST_HIP(tgemm(g, false, true, nullptr, 0, c.st));
+    ST_HIP(tgemm(g, false, true, nullptr, 0, c.st, fwd_x6()));
   }
   if (out->sinkhorn_cost)
     ST_HIP(hipMemcpyAsync(out->sinkhorn_cost, s.COST, (size_t)B * M * N * 4, hipMemcpyDeviceToDevice, c.st));

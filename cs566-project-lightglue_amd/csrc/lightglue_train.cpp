@@ -35,7 +35,7 @@ static bool head_sim_x6() {
   return v != 0;
 }
 #ifndef LG_HEAD_X6
-#define LG_HEAD_X6 0  // 1: the assignment heads' products may take the bf16x6 GEMM too
+#define LG_HEAD_X6 1  // 1: the assignment heads' products may take the bf16x6 GEMM too
 #endif
 
 namespace {
@@ -195,7 +195,7 @@ struct Ctx {
   float* ws;
   size_t ws_floats;
   float* part;
-  bool x6 = true;  // the trunk's linears may take the bf16x6 GEMM; the heads stay on f32 MFMA
+  bool x6 = true;  // the trunk's linears may take the bf16x6 GEMM; the heads follow LG_HEAD_X6
 };
 
 // y[M,N] = alpha (x[M,K] W[N,K]^T + b) + beta y

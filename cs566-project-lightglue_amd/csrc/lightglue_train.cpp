@@ -615,10 +615,15 @@ int lg_head_forward(lg_handle_t* h, const float* const* params, int32_t layer, c
   const size_t o1 = (size_t)R0 * D;
   float* sim = similarity ? similarity : s.SIM;
   // md = final_proj(desc) / d**0.25, z = matchability(desc), sim = md0 md1^T (:306-315)
-  TR_HIP(hipMemcpyAsync(s.X, desc0, o1 * 4, hipMemcpyDeviceToDevice, c.st));
-  TR_HIP(hipMemcpyAsync(s.X + o1, desc1, (size_t)(R - R0) * D * 4, hipMemcpyDeviceToDevice, c.st));
-  TR_HIP(linear(c, s.X, D, R, D, P.w(a + ".final_proj.weight"), P.w(a + ".final_proj.bias"), D, s.MD, D, 0.f, 0.25f));
-  TR_HIP(gemv256(s.X, R, P.w(a + ".matchability.weight"), P.w(a + ".matchability.bias"), s.Z, c.st));
+  // per image, straight from the inputs (row-wise products: the same values as one call over both)
+  for (int im = 0; im < 2; ++im) {
+    const float* dsc = im ? desc1 : desc0;
+    const int rows = im ? R - R0 : R0;
+    const size_t o = im ? o1 : 0;
+    TR_HIP(linear(c, dsc, D, rows, D, P.w(a + ".final_proj.weight"), P.w(a + ".final_proj.bias"), D, s.MD + o, D, 0.f,
+                  0.25f));
+    TR_HIP(gemv256(dsc, rows, P.w(a + ".matchability.weight"), P.w(a + ".matchability.bias"), s.Z + (im ? R0 : 0), c.st));
+  }
   {
     TGemm g{s.MD, s.MD + o1, sim, D, D, N, (long long)M * D, (long long)N * D, (long long)M * N, M, N, D, B, 1.f, 0.f, nullptr};
     TR_HIP(tgemm(g, false, true, c.ws, c.ws_floats, c.st, head_sim_x6() ? 2 : (int)c.x6));

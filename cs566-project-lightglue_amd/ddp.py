@@ -30,7 +30,12 @@ What it does, and where it differs from torch's DDP:
 * The loss stays the per-rank mean (``train.py:436``); with equal per-rank batches the averaged
   gradient equals the single-process gradient of the concatenated batch (``tests/test_ddp.py``:
   the semantics on the float64 oracle over gloo; ``tools/ddp_check.py``: this module on the GPU,
-  two ranks against one process, report in ``profiles/r05/``).
+  two ranks against one process, run by ``tests/test_gpu_ddp.py``).
+* **A rank failure is fatal to the job**, as under torch's DDP.  A failing rank (a library call
+  that errors mid-backward, a failed collective in a callback) issues fewer collectives than its
+  peers, which would then block forever in their next all-reduce.  ``DataParallel.abort`` waits
+  for the collectives this rank already issued, destroys the process group -- the peers' pending
+  collectives then fail instead of hanging -- and re-raises; the wrapper is unusable afterwards.
 """
 import ctypes
 import re
@@ -92,10 +97,14 @@ class _Buckets:
 
     def finish(self):
         if self.error is not None:
-            raise self.error
-        for w in self.works:
-            w.wait()
+            self.ddp.abort(self.error)
+        try:
+            for w in self.works:
+                w.wait()
+        except Exception as e:  # noqa: BLE001 -- a peer failed or the group is gone
+            self.ddp.abort(e)
         self.works = []
+        self.ddp._active = None
         self.flat.div_(self.ddp.world)
         return self.grads
 
@@ -115,6 +124,8 @@ class DataParallel:
         self._coll_buf = None
         self._coll_cb = None
         self._coll_error = None
+        self._active = None  # the _Buckets of the backward call in progress
+        self.broken = None
         model._ddp = self
         # same initial parameters everywhere (DDP broadcasts rank 0's at construction)
         with torch.no_grad():
@@ -131,25 +142,64 @@ class DataParallel:
         return name.startswith(("log_assignment.", "token_confidence."))
 
     def _param_ready(self, p):
-        self._pending.append((p, dist.all_reduce(p.grad, group=self.group, async_op=True)))
+        self._check_usable()
+        try:
+            self._pending.append((p, dist.all_reduce(p.grad, group=self.group, async_op=True)))
+        except Exception as e:  # noqa: BLE001
+            self.abort(e)
         if not self._queued:
             self._queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finish_pending)
 
     def _finish_pending(self):
-        for p, w in self._pending:
-            w.wait()
+        try:
+            for _, w in self._pending:
+                w.wait()
+        except Exception as e:  # noqa: BLE001
+            self.abort(e)
+        for p, _ in self._pending:
             p.grad.div_(self.world)
         self._pending = []
         self._queued = False
 
+    # ------------------------------------------------------------------ failure: fatal to the job
+    def _check_usable(self):
+        if self.broken is not None:
+            raise RuntimeError("DataParallel: an earlier rank failure destroyed the process group") from self.broken
+
+    def abort(self, exc):
+        """Fail this rank without stranding its peers: wait for every collective this rank issued
+        (the peers issued them too), destroy the process group so that the peers' next collective
+        raises instead of waiting for this rank forever, then re-raise ``exc``."""
+        if self.broken is None:
+            self.broken = exc
+            works = [w for _, w in self._pending]
+            if self._active is not None:
+                works += self._active.works
+                self._active.works = []
+            self._pending, self._active, self._queued = [], None, False
+            for w in works:
+                try:
+                    w.wait()
+                except Exception:  # noqa: BLE001,S110 -- the group may already be broken
+                    pass
+            try:
+                if dist.is_initialized():
+                    dist.destroy_process_group(self.group)
+            except Exception:  # noqa: BLE001,S110
+                pass
+        raise exc
+
     # ------------------------------------------------------------------ trunk calls (library hooks)
     def buckets(self, names, params, wanted, n_layers, sg, device):
-        return _Buckets(self, names, params, wanted, n_layers, sg, device)
+        self._check_usable()
+        self._active = _Buckets(self, names, params, wanted, n_layers, sg, device)
+        return self._active
 
     # ------------------------------------------------------------------ SyncBatchNorm (SuperGlue)
     def attach_collective(self, lib, handle, device):
         """Register the SyncBatchNorm collective on a SuperGlue handle (idempotent)."""
+        self._check_usable()
         if not self.sync_batchnorm:
             _lib.check(lib.sg_set_collective(handle, None, None, None, 0), "sg_set_collective")
             return
@@ -170,6 +220,7 @@ class DataParallel:
                    "sg_set_collective")
 
     def check_collective(self):
+        """After a library call that ran SyncBatchNorm collectives: a failed one is fatal (abort)."""
         if self._coll_error is not None:
             e, self._coll_error = self._coll_error, None
-            raise e
+            self.abort(e)

@@ -190,6 +190,10 @@ class _TrainTrunk(torch.autograd.Function):
                                              _ptr(ctx.saved_buf), ctx.saved_buf.numel(), _ptr(g_rd0), _ptr(g_rd1),
                                              model._param_array(grads), _ptr(gd0), _ptr(gd1), _ptr(scratch), nb.value,
                                              ctypes.c_void_p(stream)), "lg_train_backward")
+        except Exception as e:
+            if ddp is not None:
+                ddp.abort(e)  # fewer bucket collectives than the peers issue: fatal to the job, never a hang
+            raise
         finally:
             if ddp is not None:
                 lib.lg_set_grad_ready_hook(model._handle, None, None)
@@ -340,7 +344,7 @@ class _HeadNLL(torch.autograd.Function):
         data, w, prepared = gt
         d0c, d1c = d0.float().contiguous(), d1.float().contiguous()
         # the scratch keeps md / z / similarity / LSEs for the backward (saved activations, ~1 GB per
-        # head at configs[2]): no recompute of the head there
+        # head at configs[2]): no recompute of the head there (unless conf.checkpointed)
         if _HEAD_FUSED and d1c.shape[1] <= 4096:
             terms, am0, am1, t0, t1, scratch = _head_nll_forward(model, layer, d0c, d1c, params, tokens, prepared, balancing)
         else:
@@ -348,7 +352,10 @@ class _HeadNLL(torch.autograd.Function):
             terms = _nll(la, data, 1, float(balancing), prepared)  # [5, B]: nll, nll_pos, nll_neg, num_pos, num_neg
             am0, am1 = la[:, :-1, :].max(-1).indices, la[:, :, :-1].max(-2).indices
             del la
-        ctx.scratch = scratch if _HEAD_REUSE else None
+        # conf.checkpointed asks for activation memory over speed: the head's backward then
+        # recomputes md / z / similarity / LSEs instead of keeping this ~1 GB scratch (configs[2])
+        ctx.scratch = scratch if (_HEAD_REUSE and not model.conf.checkpointed) else None
+        del scratch
         if not tokens:
             t0, t1 = d0c.new_zeros(0), d0c.new_zeros(0)
         ctx.model, ctx.layer, ctx.tokens, ctx.bal = model, layer, tokens, float(balancing)
@@ -380,7 +387,10 @@ class _HeadNLL(torch.autograd.Function):
         needs = list(ctx.needs_input_grad[7:]) + [ctx.needs_input_grad[5], ctx.needs_input_grad[6]]
         gd0, gd1, grads = _head_backward(ctx.model, ctx.layer, d0, d1, params, needs, w, s_in, s_dust, None, g_t0, g_t1,
                                          fwd_scratch=ctx.scratch, gt=ctx.gt)
-        ctx.scratch = ctx.gt = None
+        # only the forward's scratch is dropped (a second backward through a retained graph then
+        # recomputes the head); the ground truth stays: without the dense weights (w None) it is
+        # what the backward reads its NLL weights from
+        ctx.scratch = None
         return (None, None, None, None, None, gd0, gd1, *grads)
 
 

@@ -342,6 +342,11 @@ class _SGTrain(torch.autograd.Function):
         rc = lib.sg_train_forward(h, ptrs, ctypes.byref(inp), ctypes.byref(out), _ptr(saved), nb.value, stream)
         if ddp is not None:
             ddp.check_collective()
+            if rc != _lib.LG_OK:  # a failure between SyncBatchNorm collectives strands the peers
+                try:
+                    _lib.check(rc, "sg_train_forward")
+                except Exception as e:
+                    ddp.abort(e)
         _lib.check(rc, "sg_train_forward")
         if getattr(model, "keep_relu_masks", False):
             model.last_relu_masks = model._relu_masks(lib, saved, B, M, N)
@@ -386,6 +391,10 @@ class _SGTrain(torch.autograd.Function):
             if ddp is not None:
                 ddp.check_collective()
             _lib.check(rc, "sg_train_backward")
+        except Exception as e:
+            if ddp is not None:
+                ddp.abort(e)  # fewer collectives than the peers issue: fatal to the job, never a hang
+            raise
         finally:
             if ddp is not None:
                 lib.sg_set_grad_ready_hook(model._handle, None, None)

@@ -136,3 +136,63 @@ def test_data_parallel_step_equals_one_step_on_the_concatenated_batch(tmp_path, 
         assert set(got["stats"]) == set(ref_s)
         for k, s in ref_s.items():
             assert float((got["stats"][k] - s).abs().max()) <= 1e-12 * max(float(s.abs().max()), 1.0), (r, k)
+
+
+def _abort_worker(rank, world, port, out_dir):
+    """Rank 1 fails after its first gradient bucket (as a library error mid-backward would); rank 0
+    goes on to its second bucket's all-reduce, which rank 1 never issues."""
+    import time
+
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import lgamd  # noqa: F401
+    from lightglue_amd.ddp import DataParallel
+
+    class Tiny(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.transformers = torch.nn.ModuleList([torch.nn.Linear(4, 4) for _ in range(2)])
+
+    model = Tiny()
+    ddp = DataParallel(model)
+    names = [n for n, _ in model.named_parameters()]
+    params = [p for _, p in model.named_parameters()]
+    b = ddp.buckets(names, params, [True] * len(params), 2, False, torch.device("cpu"))
+    for g in b.grads:
+        g.fill_(rank + 1.0)
+    ready = b.callback(lambda f: f)  # the Python callback itself (the library would call it)
+    ready(None, 1, None)  # layer 1's bucket: both ranks issue it
+    t0 = time.time()
+    try:
+        if rank == 1:
+            ddp.abort(RuntimeError("injected failure"))
+        ready(None, 0, None)  # rank 0 only
+        b.finish()
+        res = "finished"
+    except Exception as e:  # noqa: BLE001
+        res = f"raised {type(e).__name__}"
+    with open(os.path.join(out_dir, f"abort{rank}.txt"), "w") as f:
+        f.write(f"{res} {time.time() - t0:.1f}")
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def test_data_parallel_rank_failure_fails_the_peers_instead_of_hanging(tmp_path):
+    """ddp.DataParallel.abort: a failing rank drains what it issued and destroys the
+    process group, so a peer blocked in a collective the failed rank never issues raises."""
+    import time
+
+    ctx = mp.spawn(_abort_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=False)
+    deadline = time.time() + 120
+    while not ctx.join(timeout=1):
+        if time.time() > deadline:
+            for p in ctx.processes:
+                p.kill()
+            pytest.fail("a rank hung after its peer failed")
+    r0 = open(os.path.join(str(tmp_path), "abort0.txt")).read()
+    print("rank 0:", r0)
+    r1 = open(os.path.join(str(tmp_path), "abort1.txt")).read()
+    assert r1.startswith("raised RuntimeError"), r1
+    assert r0.startswith("raised"), r0
+    assert float(r0.split()[-1]) < 60, r0  # promptly: the closed group, not a collective timeout

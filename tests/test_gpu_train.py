@@ -108,6 +108,9 @@ def test_train_attention_forward_backward_fp64(B, Nq, Nk):
 
 
 # ------------------------------------------------------------------ full backward
+REF_ONLY_CANARY = 2.0  # see test_gpu_sg_train.py
+
+
 def _gpu_grads(conf, sd, pair, gt):
     from lightglue_amd import LightGlue
 
@@ -144,7 +147,7 @@ def test_backward_matches_reference_and_oracle(name):
 
     def spread(ref32, r64, o32):
         return max(float(ref32), float(np.abs(np.asarray(o32) - r64).max()))
-    worst, bad = [], []
+    worst, bad, canary = [], [], []
     for n in meta["names"]:
         assert grads[n] is not None, f"no gradient for {n}"
         tol = 8 * spread(g[f"spread32:{n}"], og[n], og32[n]) + 1e-6 * float(g[f"max64:{n}"]) + 1e-12
@@ -155,6 +158,9 @@ def test_backward_matches_reference_and_oracle(name):
         worst.append((max(e_gold, e_full) / tol, n))
         if e_gold > tol or e_full > tol:
             bad.append((n, float(e_gold), float(e_full), tol, float(g[f"max64:{n}"])))
+        # canary on the bar of the reference's own float32 spread alone (round 5's
+        # default routes reached 1.19 of it, profiles/r05/grad_routes/)
+        canary.append((float(e_gold) / (8 * float(g[f"spread32:{n}"]) + 1e-6 * float(g[f"max64:{n}"]) + 1e-12), n))
     for got, ref, r32, key in ((gd0, ogd0, o32d0, "gdesc0"), (gd1, ogd1, o32d1, "gdesc1")):
         idx, gref, gmax = desc_golden(g, key)
         tol = 8 * spread(g[f"spread_{key}"], ref, r32) + 1e-6 * gmax + 1e-12
@@ -163,8 +169,11 @@ def test_backward_matches_reference_and_oracle(name):
         if e_gold > tol or e_full > tol:
             bad.append((key, float(e_gold), float(e_full), tol, gmax))
     worst.sort(reverse=True)
-    print(name, "loss", loss, "worst err/tol:", [(n, round(r, 3)) for r, n in worst[:6]])
+    canary.sort(reverse=True)
+    print(name, "loss", loss, "worst err/tol:", [(n, round(r, 3)) for r, n in worst[:6]],
+          "reference-spread-only:", [(n, round(r, 3)) for r, n in canary[:3]])
     assert not bad, bad[:12]
+    assert canary[0][0] <= REF_ONLY_CANARY, canary[:4]
 
 
 @pytest.mark.parametrize("name", ["grad_train_b2_n64", "grad_train_l3_b2_n96_proj_ori"])
@@ -489,3 +498,34 @@ def test_trunk_backward_with_one_posenc_parameter_frozen(frozen):
         assert g is not None and torch.isfinite(g).all(), n
         err = float((g - full[n]).abs().max())
         assert err <= 1e-4 * scale, (n, err, scale)
+
+
+def test_loss_heads_backward_twice_through_a_retained_graph():
+    """_HeadNLL's backward drops only the forward's scratch, not the ground truth its NLL
+    weights come from, so a second backward through a retained graph recomputes the head
+    (lg_head_nll_backward, from_forward = 0) and gives the first backward's gradients."""
+    g, meta = load_grad("grad_train_b2_n64")
+    conf, sd, pair, gt = grad_case(meta)
+    from lightglue_amd import LightGlue
+
+    model = LightGlue(conf).to(DEV)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model.train()
+    data = {k: torch.from_numpy(v).to(DEV) for k, v in pair.items() if not k.startswith("image_size")}
+    data["view0"] = {"image_size": torch.from_numpy(pair["image_size0"]).to(DEV)}
+    data["view1"] = {"image_size": torch.from_numpy(pair["image_size1"]).to(DEV)}
+    data.update({k: torch.from_numpy(v).to(DEV) for k, v in gt.items()})
+    pred = model(data)
+    # the trunk's saved activations go with its first backward: differentiate the heads only
+    rd0 = pred["ref_descriptors0"].detach().requires_grad_()
+    rd1 = pred["ref_descriptors1"].detach().requires_grad_()
+    losses, _ = model.loss({**pred, "ref_descriptors0": rd0, "ref_descriptors1": rd1}, data)
+    loss = torch.mean(losses["total"])
+    loss.backward(retain_graph=True)
+    first = (rd0.grad.clone(), rd1.grad.clone())
+    rd0.grad = rd1.grad = None
+    loss.backward()
+    for a, b in zip(first, (rd0.grad, rd1.grad)):
+        scale = float(a.abs().max())
+        assert scale > 0
+        assert float((a - b).abs().max()) <= 1e-6 * scale

@@ -10,6 +10,7 @@
 #include "../cs566-project-lightglue_amd/csrc/elementwise.hip"
 #include "../cs566-project-lightglue_amd/csrc/gemm_h3.hip"
 #include "gemm_persist.hip"
+#include "gemm_defer.hip"
 
 using namespace lg;
 
@@ -58,6 +59,26 @@ double run_h3p(const Shape& s, float* bias, float* Y, int iters, _Float16* Yp, i
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
   for (int i = 0; i < iters; ++i) CK(gemm_h3p(a, 0, grid));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
+template <int NK, int DIAG = 0>
+double run_h3d(const Shape& s, float* bias, float* Y, int iters, int grid) {
+  GemmH3Args a;
+  memset(&a, 0, sizeof(a));
+  a.A0 = {g_aplanes, (long long)s.R * s.K, s.R}; a.K0 = s.K; a.K = s.K;
+  a.W = {g_planes, (long long)s.N * s.K, s.N}; a.R = s.R; a.Nout = s.N;
+  a.acc_scale = g_unscale; a.out_scale = 1.f; a.bias = bias; a.Y = Y; a.ldy = s.N;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK((gemm_h3d<NK, DIAG>(a, 0, grid)));
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK((gemm_h3d<NK, DIAG>(a, 0, grid)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -199,6 +220,21 @@ int main() {
         CK(hipMemset(Y, 0, (size_t)s.R * s.N * 4));
         ms = run_h3p(s, bias, Y, it, Yp, grid); rep(nm, ms, true);
       }
+      continue;
+    }
+    if (getenv("KB_DEFER")) {  // deferred-store persistent prototype (tools/gemm_defer.hip), fp32 out
+      if (s.K < 256) continue;
+      ms = run_h3<256, 2, EPI_PROBE>(s, bias, Y, it, false, Yp); rep("256x256 k-loop only", ms, false);
+      CK(hipMemset(Y, 0, (size_t)s.R * s.N * 4));
+      ms = run_h3<256, 2>(s, bias, Y, it, false, Yp); rep("256x256 + fp32 out", ms, true);
+      CK(hipMemset(Y, 0, (size_t)s.R * s.N * 4));
+      ms = s.K == 256 ? run_h3d<8>(s, bias, Y, it, 256) : run_h3d<16>(s, bias, Y, it, 256);
+      rep("defer 256x128 + fp32 (deferred)", ms, true);
+      ms = s.K == 256 ? run_h3d<8, 1>(s, bias, Y, it, 256) : run_h3d<16, 1>(s, bias, Y, it, 256);
+      rep("defer 256x128 k-loop only", ms, false);
+      CK(hipMemset(Y, 0, (size_t)s.R * s.N * 4));
+      ms = s.K == 256 ? run_h3d<8, 2>(s, bias, Y, it, 256) : run_h3d<16, 2>(s, bias, Y, it, 256);
+      rep("defer 256x128 + fp32 (stores at tile end)", ms, true);
       continue;
     }
     if (getenv("KB_CHAIN")) {

@@ -570,7 +570,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / WN) * 64 * KS) void gemm_h3_kerne
               v1[e] = fmaf(v1[e], accs, b1[e]) * g.out_scale;
             }
             if (g.res) {
-              const float* rp = g.res + (size_t)row * g.ldr + n0 + wn0 + c4;
+              const float* rp = (g.res2 && row >= g.res2_row0 ? g.res2 + (size_t)(row - g.res2_row0) * g.ldr
+                                                              : g.res + (size_t)row * g.ldr) + n0 + wn0 + c4;
               f32x4 r0, r1;
               if (LG_GEMM_A_NT && g.stream) {
                 r0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(rp));
@@ -970,6 +971,45 @@ hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipSt
   if (n == 0) return hipSuccess;
   const size_t blocks = std::min<size_t>((n / 4 + 255) / 256 + 1, 1024);
   hipLaunchKernelGGL(range_absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, tab, slot);
+  return hipGetLastError();
+}
+
+// max |x| over two arrays (both images' descriptors) -> M[slot] in one launch, eight 16-byte loads
+// in flight per thread (the one-array kernel above keeps one: 67 MB in ~30 us, 2.2 TB/s); the
+// maximum is order-independent, so the slot holds the same value as two range_absmax calls
+__global__ __launch_bounds__(256) void range_absmax2_kernel(const float* x0, size_t n0, const float* x1, size_t n1,
+                                                            unsigned* tab, int slot) {
+  float m = 0.f;
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  auto am4 = [](const f32x4& v) { return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))); };
+  auto body = [&](const float* x, size_t n) {
+    if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+      const size_t n4 = n / 4;
+      const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+      size_t i = t0;
+      for (; i + 7 * stride < n4; i += 8 * stride) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = x4[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) m = fmaxf(m, am4(v[u]));
+      }
+      for (; i < n4; i += stride) m = fmaxf(m, am4(x4[i]));
+      for (size_t j = n4 * 4 + t0; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
+    } else {
+      for (size_t j = t0; j < n; j += stride) m = fmaxf(m, fabsf(x[j]));
+    }
+  };
+  body(x0, n0);
+  body(x1, n1);
+  range_commit(RangeOut{tab, -1, -1, 0.f, 0.f, 0.f, slot, 1}, m, 0);
+}
+
+hipError_t range_absmax2(const float* x0, size_t n0, const float* x1, size_t n1, unsigned* tab, int slot,
+                         hipStream_t st) {
+  if (n0 + n1 == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>(((n0 + n1) / 4 + 255) / 256 + 1, 1024);
+  hipLaunchKernelGGL(range_absmax2_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x0, n0, x1, n1, tab, slot);
   return hipGetLastError();
 }
 }  // namespace lg

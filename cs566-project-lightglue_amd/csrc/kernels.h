@@ -139,6 +139,8 @@ struct GemmH3Args {
   const float* bias;  // [Nout] or null
   const float* res;   // EPI_STORE: Y = res + (...) (nullable), row stride ldr
   int ldr;
+  const float* res2;  // EPI_STORE (nullable): rows >= res2_row0 read their residual at res2 + (row - res2_row0) * ldr
+  int res2_row0;
   float* Y;           // EPI_STORE fp32 output (nullable), row stride ldy
   int ldy;
   float* Y2;          // EPI_STORE (nullable): rows >= y2_row0 go to Y2 + (row - y2_row0) * ldy instead
@@ -165,6 +167,9 @@ hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes
                           const RangeOut& ro, hipStream_t st, float* xcopy = nullptr, const RowMask* rm = nullptr);
 // max |x| over n floats, atomicMax'ed into slot `slot` of a range table (M only)
 hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipStream_t st);
+// the same over two arrays in one launch (x1 may be null when n1 == 0)
+hipError_t range_absmax2(const float* x0, size_t n0, const float* x1, size_t n1, unsigned* tab, int slot,
+                         hipStream_t st);
 
 // Attention over head-major Q/K/V ([set][b][h][n][64]); O written row-major into ctx
 // [rows][256] at column h*64 (rows in GEMM order).  Two "sets" per launch (blockIdx.z).

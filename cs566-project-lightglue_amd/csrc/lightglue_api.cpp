@@ -766,6 +766,10 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
   if (prec == PREC_H3) LG_HIP(hipMemsetAsync(w.rtab, 0, (size_t)w.nslots * lg::kRangeStride * sizeof(unsigned), st));
   h->pass_started = true;
   int s_x = -1;  // slot of the current residual-stream plane image Xp
+  // set when w.X was not initialised from the descriptors: layer 0's self-block ffn.3 reads its
+  // residual rows from here (image 0 rows, then image 1 rows)
+  const float* res_in0 = nullptr;
+  const float* res_in1 = nullptr;
   // ---- input projection (lightglue.py:370-373,486-487); H3 also builds x's plane image
   if (c.input_dim != D) {
     if (prec == PREC_H3) {
@@ -780,8 +784,7 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       }
       const int s_in = slot(), s_d = slot();
       s_x = slot();
-      LG_HIP(range_absmax(d0, (size_t)B * M * din, rt, s_in, st));
-      LG_HIP(range_absmax(d1, (size_t)B * N * din, rt, s_in, st));
+      LG_HIP(range_absmax2(d0, (size_t)B * M * din, d1, (size_t)B * N * din, rt, s_in, st));
       LG_HIP(rows_to_planes(d0, B * M, din, din, w.Dp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_d), st));
       LG_HIP(rows_to_planes(d1, B * N, din, din, w.Dp, RP, B * M, ro(s_in, 1.f, -1, 0.f, 0.f, s_d), st));
       GemmH3Args g = gemm_h3_base();
@@ -802,14 +805,16 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     const int s_in = prec == PREC_H3 ? slot() : -1;
     s_x = prec == PREC_H3 ? slot() : -1;
     if (prec == PREC_H3) {
-      LG_HIP(range_absmax(in->descriptors0, (size_t)B * M * D, rt, s_in, st));
-      LG_HIP(range_absmax(in->descriptors1, (size_t)B * N * D, rt, s_in, st));
+      LG_HIP(range_absmax2(in->descriptors0, (size_t)B * M * D, in->descriptors1, (size_t)B * N * D, rt, s_in, st));
     }
-    if (prec == PREC_H3 && din_a16) {
-      // residual stream and its plane image from one read of the descriptors
-      LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st, w.X));
-      LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st,
-                            w.X + (size_t)B * M * D));
+    if (prec == PREC_H3 && din_a16 && L > 0) {
+      // the plane image from one read of the descriptors; the fp32 residual stream w.X is first
+      // written by layer 0's self-block ffn.3, which reads its residual from the descriptors
+      // themselves (res_in) -- no copy; with pruning / early stop every row of layer 0 is live
+      LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st));
+      LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st));
+      res_in0 = in->descriptors0;
+      res_in1 = in->descriptors1;
     } else {
       LG_HIP(hipMemcpyAsync(w.X, in->descriptors0, sizeof(float) * B * M * D, hipMemcpyDeviceToDevice, st));
       LG_HIP(hipMemcpyAsync(w.X + (size_t)B * M * D, in->descriptors1, sizeof(float) * B * N * D, hipMemcpyDeviceToDevice, st));
@@ -944,6 +949,12 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
         g.A0 = image(w.Hp, 2 * D); g.K0 = 2 * D; g.K = 2 * D; wplanes(g, bw.W2); g.bias = Wb + bw.b2;
         g.rtab = rt; g.a0_slot = s_h; g.rm = live;  // frozen / dead rows keep their residual stream
         g.R = R; g.Nout = D; g.Y = w.X; g.ldy = D; g.res = w.X; g.ldr = D;
+        if (res_in0) {  // the first ffn.3: the residual is the input descriptors (never copied into w.X)
+          g.res = res_in0;
+          g.res2 = res_in1;
+          g.res2_row0 = B * M;
+          res_in0 = res_in1 = nullptr;
+        }
         g.reverse = h->ffn3_reverse;  // read the hidden planes the LN GEMM wrote last first
         if (direct_out && i == L - 1 && blk == 1) {  // the final descriptors straight into the outputs
           g.Y = out->ref_descriptors0;

@@ -505,8 +505,7 @@ int sg_forward(sg_handle_t* h, const sg_inputs_t* in, sg_outputs_t* out, void* w
   if (h->enc_gemm) {
     const int s_d = slot(), s_hr = slot(), s_he = slot();
     s_x = slot();
-    SG_HIP(range_absmax(in->descriptors0, (size_t)B * M * D, rt, s_d, st));
-    SG_HIP(range_absmax(in->descriptors1, (size_t)B * N * D, rt, s_d, st));
+    SG_HIP(range_absmax2(in->descriptors0, (size_t)B * M * D, in->descriptors1, (size_t)B * N * D, rt, s_d, st));
     SG_HIP(range_absmax(w.ctx, (size_t)R * kl, rt, s_hr, st));
     SG_HIP(rows_to_planes(w.ctx, R, kl, kl, w.Hp, RP, 0, ro(s_hr, 1.f, -1, 0.f, 0.f, s_he, 1), st));
     GemmH3Args g;

@@ -1,3 +1,4 @@
+#include <algorithm>
 // Bandwidth-bound kernels of the LightGlue hot path (gfx950): positional encoding, fused
 // LayerNorm+GELU, 256-wide GEMVs (matchability / token confidence), weight repacking and the
 // point-pruning compaction.  One wave per row wherever a row reduction is needed.
@@ -70,6 +71,40 @@ hipError_t positional_encoding(const PEArgs& a0, hipStream_t st) {
   if (a0.B * a0.n == 0) return hipSuccess;
   const int threads = a0.B * a0.n * 32;
   hipLaunchKernelGGL(pe_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, a0);
+  return hipGetLastError();
+}
+
+// both images in one launch (blockIdx.y selects the image; the values are pe_kernel's)
+__global__ void pe2_kernel(PEArgs a0, PEArgs a1) {
+  const PEArgs& a = blockIdx.y == 0 ? a0 : a1;
+  if ((int)blockIdx.x * (int)blockDim.x >= a.B * a.n * 32) return;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int f = gid & 31;
+  const int pt = gid >> 5;
+  if (pt >= a.B * a.n) return;
+  const int b = pt / a.n;
+  const float w = a.size[b * 2 + 0], h = a.size[b * 2 + 1];
+  const float scale = div_rn(fmaxf(w, h), 2.f);
+  float x[4];
+  x[0] = div_rn(sub_rn(a.kpts[(size_t)pt * 2 + 0], div_rn(w, 2.f)), scale);
+  x[1] = div_rn(sub_rn(a.kpts[(size_t)pt * 2 + 1], div_rn(h, 2.f)), scale);
+  if (a.m_in == 4) {
+    x[2] = a.scales[pt];
+    x[3] = a.oris[pt];
+  }
+  const float* wr = a.Wr + f * a.m_in;
+  float p = mul_rn(x[0], wr[0]);
+  for (int k = 1; k < a.m_in; ++k) p = __fmaf_rn(x[k], wr[k], p);
+  const float cond = add_rn(mul_rn((float)a.n, a.Wc[f]), a.bc[f]);  // relu(n) = n
+  p = add_rn(p, cond);
+  a.cosb[(size_t)pt * kFreq + f] = cosf(p);
+  a.sinb[(size_t)pt * kFreq + f] = sinf(p);
+}
+
+hipError_t positional_encoding2(const PEArgs& a0, const PEArgs& a1, hipStream_t st) {
+  const int t = std::max(a0.B * a0.n, a1.B * a1.n) * 32;
+  if (t == 0) return hipSuccess;
+  hipLaunchKernelGGL(pe2_kernel, dim3((t + 255) / 256, 2), dim3(256), 0, st, a0, a1);
   return hipGetLastError();
 }
 
@@ -178,6 +213,31 @@ hipError_t gemv_256_masked(const float* x, const float* w, const float* b, float
                            hipStream_t st) {
   if (rows == 0) return hipSuccess;
   hipLaunchKernelGGL(gemv256_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, y, rows, 0, m);
+  return hipGetLastError();
+}
+
+// the same over two row sources in one launch: rows [0, r0) of x0, then rows [0, r1) of x1 into
+// y[0 .. r0 + r1); each source's rows are tested against rm with their own index (as two calls)
+__global__ __launch_bounds__(256) void gemv256_2_kernel(const float* x0, int r0, const float* x1, int r1, const float* w,
+                                                        const float* b, float* y, RowMask rm) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= r0 + r1) return;
+  const bool second = row >= r0;
+  const int sr = second ? row - r0 : row;
+  if (!row_live(rm, sr)) return;
+  const float* x = (second ? x1 : x0) + (size_t)sr * kDim;
+  const f32x4 xv = *reinterpret_cast<const f32x4*>(x + lane * 4);
+  const f32x4 wv = *reinterpret_cast<const f32x4*>(w + lane * 4);
+  float s = xv[0] * wv[0] + xv[1] * wv[1] + xv[2] * wv[2] + xv[3] * wv[3];
+  s = wave_sum(s);
+  if (lane == 0) y[row] = s + b[0];
+}
+
+hipError_t gemv_256_masked2(const float* x0, int r0, const float* x1, int r1, const float* w, const float* b, float* y,
+                            const RowMask& m, hipStream_t st) {
+  if (r0 + r1 == 0) return hipSuccess;
+  hipLaunchKernelGGL(gemv256_2_kernel, dim3((r0 + r1 + 3) / 4), dim3(256), 0, st, x0, r0, x1, r1, w, b, y, m);
   return hipGetLastError();
 }
 

@@ -946,6 +946,46 @@ hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes
   return hipGetLastError();
 }
 
+// rows_to_planes of two row sources in one launch: rows row0 .. row0+r0-1 from x0, then r1 rows
+// from x1 (no fp32 copy, no row mask); element for element the values of two rows_to_planes calls
+__global__ void rows_to_planes2_kernel(const float* x0, int r0, const float* x1, int r1, int K, int ld,
+                                       _Float16* planes, int rows_pad, int row0, RangeOut ro) {
+  const int nch = K / 8;
+  const int eo = range_exponent(ro);
+  const float so = ldexpf(1.f, -eo);
+  float wmax = 0.f;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)(r0 + r1) * nch;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / nch), c = (int)(i % nch);
+    const float* p = (r < r0 ? x0 + (size_t)r * ld : x1 + (size_t)(r - r0) * ld) + c * 8;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(p), v1 = *reinterpret_cast<const f32x4*>(p + 4);
+    f16x8 h, l;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = e < 4 ? v0[e] : v1[e - 4];
+      wmax = fmaxf(wmax, fabsf(v));
+      _Float16 a, b;
+      split2h(v * so, a, b);
+      h[e] = a;
+      l[e] = b;
+    }
+    const size_t off = plane_off(row0 + r, c * 8, rows_pad);
+    *reinterpret_cast<f16x8*>(planes + off) = h;
+    *reinterpret_cast<f16x8*>(planes + (size_t)rows_pad * K + off) = l;
+  }
+  range_commit(ro, wmax, eo);
+}
+
+hipError_t rows_to_planes2(const float* x0, int r0, const float* x1, int r1, int K, int ld, _Float16* planes,
+                           int rows_pad, int row0, const RangeOut& ro, hipStream_t st) {
+  if (r0 + r1 <= 0) return hipSuccess;
+  if (K % kKB || rows_pad < row0 + r0 + r1) return hipErrorInvalidValue;
+  const size_t n = (size_t)(r0 + r1) * (K / 8);
+  hipLaunchKernelGGL(rows_to_planes2_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 2048)), dim3(256), 0, st,
+                     x0, r0, x1, r1, K, ld, planes, rows_pad, row0, ro);
+  return hipGetLastError();
+}
+
 }  // namespace lg
 
 namespace lg {

@@ -165,6 +165,9 @@ hipError_t gemm_h3(const GemmH3Args& a, int epi, hipStream_t st);
 // the fp16-range guard; xcopy (optional) also receives the fp32 rows, row stride K
 hipError_t rows_to_planes(const float* x, int R, int K, int ld, _Float16* planes, int rows_pad, int row0,
                           const RangeOut& ro, hipStream_t st, float* xcopy = nullptr, const RowMask* rm = nullptr);
+// two row sources (r0 rows of x0, then r1 rows of x1) in one launch, no copy / mask
+hipError_t rows_to_planes2(const float* x0, int r0, const float* x1, int r1, int K, int ld, _Float16* planes,
+                           int rows_pad, int row0, const RangeOut& ro, hipStream_t st);
 // max |x| over n floats, atomicMax'ed into slot `slot` of a range table (M only)
 hipError_t range_absmax(const float* x, size_t n, unsigned* tab, int slot, hipStream_t st);
 // the same over two arrays in one launch (x1 may be null when n1 == 0)
@@ -219,6 +222,8 @@ struct PEArgs {
   int B, n, m_in;
 };
 hipError_t positional_encoding(const PEArgs& a, hipStream_t st);
+// both images in one launch
+hipError_t positional_encoding2(const PEArgs& a0, const PEArgs& a1, hipStream_t st);
 // size = 1 + max - min of each pair's keypoints (normalize_keypoints fallback, lightglue.py:25-26)
 hipError_t kpt_extent(const float* kpts, int B, int n, float* size_out, hipStream_t st);
 
@@ -228,6 +233,9 @@ hipError_t layernorm_gelu_512(float* x, const float* g, const float* b, int rows
                               const RangeOut& ro, hipStream_t st);
 // y[r] = dot(x[r,:256], w) + b ; optional sigmoid
 hipError_t gemv_256(const float* x, const float* w, const float* b, float* y, int rows, int sigmoid, hipStream_t st);
+// rows of x0 then rows of x1 into y (no sigmoid), one launch
+hipError_t gemv_256_masked2(const float* x0, int r0, const float* x1, int r1, const float* w, const float* b, float* y,
+                            const RowMask& m, hipStream_t st);
 
 // Dual-softmax assignment + mutual filter (lightglue.py:284-296, 321-337).
 struct AssignArgs {

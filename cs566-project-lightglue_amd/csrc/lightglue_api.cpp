@@ -13,6 +13,17 @@
 
 #include "../../include/lightglue_mi355x.h"
 #include "kernels.h"
+
+// two-image launches of the input preparation / final matchability (round 6 A/B switches)
+#ifndef LG_MERGE_PE
+#define LG_MERGE_PE 1
+#endif
+#ifndef LG_MERGE_R2P
+#define LG_MERGE_R2P 1
+#endif
+#ifndef LG_MERGE_GEMV
+#define LG_MERGE_GEMV 1
+#endif
 #include "common.h"
 
 namespace {
@@ -811,8 +822,13 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       // the plane image from one read of the descriptors; the fp32 residual stream w.X is first
       // written by layer 0's self-block ffn.3, which reads its residual from the descriptors
       // themselves (res_in) -- no copy; with pruning / early stop every row of layer 0 is live
+#if LG_MERGE_R2P
+      LG_HIP(rows_to_planes2(in->descriptors0, B * M, in->descriptors1, B * N, D, D, w.Xp, RP, 0,
+                             ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st));
+#else
       LG_HIP(rows_to_planes(in->descriptors0, B * M, D, D, w.Xp, RP, 0, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st));
       LG_HIP(rows_to_planes(in->descriptors1, B * N, D, D, w.Xp, RP, B * M, ro(s_in, 1.f, -1, 0.f, 0.f, s_x, 1), st));
+#endif
       res_in0 = in->descriptors0;
       res_in1 = in->descriptors1;
     } else {
@@ -832,10 +848,15 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
     p.Wr = Wb + h->Wr; p.Wc = Wb + h->Wc; p.bc = Wb + h->bc; p.m_in = c.add_scale_ori ? 4 : 2; p.B = B;
     p.kpts = in->keypoints0; p.size = s0; p.scales = in->scales0; p.oris = in->oris0; p.n = M;
     p.cosb = w.cosb; p.sinb = w.sinb;
+    PEArgs p1 = p;
+    p1.kpts = in->keypoints1; p1.size = s1; p1.scales = in->scales1; p1.oris = in->oris1; p1.n = N;
+    p1.cosb = w.cosb + (size_t)B * M * 32; p1.sinb = w.sinb + (size_t)B * M * 32;
+#if LG_MERGE_PE
+    LG_HIP(positional_encoding2(p, p1, st));
+#else
     LG_HIP(positional_encoding(p, st));
-    p.kpts = in->keypoints1; p.size = s1; p.scales = in->scales1; p.oris = in->oris1; p.n = N;
-    p.cosb = w.cosb + (size_t)B * M * 32; p.sinb = w.sinb + (size_t)B * M * 32;
-    LG_HIP(positional_encoding(p, st));
+    LG_HIP(positional_encoding(p1, st));
+#endif
   }
 
   // ---- early stop / point pruning for any batch size, counts on the device (kernels.h
@@ -1059,8 +1080,13 @@ static int forward_pass(lg_handle_t* h, const lg_inputs_t* in, lg_outputs_t* out
       LG_HIP(gemm(g, EPI_STORE, 1));
     }
     if (direct_out) {  // the final fp32 descriptors live in the outputs (every row live)
+#if LG_MERGE_GEMV
+      LG_HIP(gemv_256_masked2(out->ref_descriptors0, B * M, out->ref_descriptors1, B * N, Wb + la.wm, Wb + la.bm, w.z, m,
+                              st));
+#else
       LG_HIP(gemv_256_masked(out->ref_descriptors0, Wb + la.wm, Wb + la.bm, w.z, B * M, m, st));
       LG_HIP(gemv_256_masked(out->ref_descriptors1, Wb + la.wm, Wb + la.bm, w.z + (size_t)B * M, B * N, m, st));
+#endif
     } else {
       LG_HIP(gemv_256_masked(w.X, Wb + la.wm, Wb + la.bm, w.z, R, m, st));
     }

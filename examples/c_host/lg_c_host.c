@@ -4,7 +4,7 @@
  * LightGlue.__init__ + forward do (gluefactory/models/matchers/lightglue.py:367-430, 444-579) for
  * one batch: build the matcher from a state dict, match, write matches / scores.
  *
- *   lg_c_host <weights.bin> <inputs.bin> <outputs.bin> [filter_threshold]
+ *   lg_c_host <weights.bin> <inputs.bin> <outputs.bin> [filter_threshold [depth_confidence width_confidence]]
  *
  * weights.bin  "LGW1", u32 count, then per tensor: u32 name length, name bytes, i64 numel,
  *              numel float32 (the state-dict keys and PyTorch layouts, lightglue.py:367-398)
@@ -69,15 +69,17 @@ static float* upload(FILE* f, size_t n, const char* what) {
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    fprintf(stderr, "usage: %s weights.bin inputs.bin outputs.bin [filter_threshold]\n", argv[0]);
+    fprintf(stderr, "usage: %s weights.bin inputs.bin outputs.bin [filter_threshold [depth_conf width_conf]]\n", argv[0]);
     return 1;
   }
   if (lg_abi_version() != LG_ABI_VERSION) {
     fprintf(stderr, "ABI mismatch: library %d, header %d\n", lg_abi_version(), LG_ABI_VERSION);
     return 1;
   }
-  /* LightGlue.default_conf (lightglue.py:341-361) with the caller's filter_threshold */
-  lg_config_t cfg = {256, 256, 9, 4, 0, -1.0, -1.0, argc > 4 ? atof(argv[4]) : 0.0, LG_PREC_AUTO};
+  /* LightGlue.default_conf (lightglue.py:341-361) with the caller's filter_threshold and, optionally,
+   * the adaptive depth / width confidences (early stop and point pruning, lightglue.py:502-540) */
+  lg_config_t cfg = {256, 256, 9, 4, 0, argc > 6 ? atof(argv[5]) : -1.0, argc > 6 ? atof(argv[6]) : -1.0,
+                     argc > 4 ? atof(argv[4]) : 0.0, LG_PREC_AUTO};
   lg_handle_t* h = NULL;
   LG_OK_(lg_create(&cfg, 0, &h));
 

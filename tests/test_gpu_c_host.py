@@ -48,7 +48,11 @@ def _read_outputs(path):
     return out
 
 
-def test_c_host_forward_equals_python_forward(tmp_path):
+@pytest.mark.parametrize("adaptive", [False, True], ids=["fixed_depth", "early_stop_and_pruning"])
+def test_c_host_forward_equals_python_forward(tmp_path, adaptive):
+    """adaptive: depth_confidence 0.95 / width_confidence 0.95 (lightglue.py:502-540) on one pair --
+    the C host against the Python class only (both run the same kernels; the oracle's pruning
+    parity is pinned on the goldens in test_gpu_parity.py)."""
     import lgamd  # noqa: F401
     import oracle
     from lightglue_amd import LightGlue
@@ -56,12 +60,16 @@ def test_c_host_forward_equals_python_forward(tmp_path):
 
     assert os.path.exists(EXE), "examples/c_host/lg_c_host is built by make -C cs566-project-lightglue_amd/csrc"
     conf = {"filter_threshold": 0.1}
+    args = ["0.1"]
+    if adaptive:
+        conf.update(depth_confidence=0.95, width_confidence=0.95)
+        args += ["0.95", "0.95"]
     sd = synthetic_state_dict(conf, seed=0)
-    data = synthetic_pair(B=2, M=300, N=277, seed=9)
+    data = synthetic_pair(B=1 if adaptive else 2, M=300, N=277, seed=9)
     w, i, o = (str(tmp_path / n) for n in ("w.bin", "i.bin", "o.bin"))
     _write_weights(w, sd)
     _write_inputs(i, data)
-    r = subprocess.run([EXE, w, i, o, "0.1"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([EXE, w, i, o] + args, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     got = _read_outputs(o)
 
@@ -75,6 +83,8 @@ def test_c_host_forward_equals_python_forward(tmp_path):
         pred = model(feed)
     for k in ("matches0", "matches1", "matching_scores0", "matching_scores1"):
         np.testing.assert_array_equal(got[k], pred[k].cpu().numpy(), err_msg=k)
+    if adaptive:
+        return
     ref = oracle.lightglue_forward(sd, data, conf)
     np.testing.assert_array_equal(got["matches0"], ref["matches0"].numpy())
     np.testing.assert_allclose(got["matching_scores0"], ref["matching_scores0"].numpy(), atol=1e-4)

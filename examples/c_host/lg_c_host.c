@@ -138,6 +138,10 @@ int main(int argc, char** argv) {
   HIP_OK(hipMalloc((void**)&out.matches1, (size_t)B * N * sizeof(int64_t)));
   HIP_OK(hipMalloc((void**)&out.matching_scores0, (size_t)B * M * sizeof(float)));
   HIP_OK(hipMalloc((void**)&out.matching_scores1, (size_t)B * N * sizeof(float)));
+  if (cfg.width_confidence > 0) { /* point pruning reports each point's layer count */
+    HIP_OK(hipMalloc((void**)&out.prune0, (size_t)B * M * sizeof(int64_t)));
+    HIP_OK(hipMalloc((void**)&out.prune1, (size_t)B * N * sizeof(int64_t)));
+  }
   size_t ws_bytes = 0;
   LG_OK_(lg_workspace_bytes(h, B, M, N, &ws_bytes));
   void* ws = NULL;
@@ -167,12 +171,14 @@ int main(int argc, char** argv) {
 
   long matched = 0;
   for (size_t i = 0; i < (size_t)B * M; ++i) matched += m0[i] > -1;
-  printf("lg_c_host: B %d M %d N %d, %ld matches (precision used %d)\n", B, M, N, matched, out.precision_used);
+  printf("lg_c_host: B %d M %d N %d, %ld matches, stop layer %d (precision used %d)\n", B, M, N, matched,
+         out.stop_layer, out.precision_used);
 
   free(m0); free(m1); free(s0); free(s1);
   HIP_OK(hipFree(ws));
   HIP_OK(hipFree(out.matches0)); HIP_OK(hipFree(out.matches1));
   HIP_OK(hipFree(out.matching_scores0)); HIP_OK(hipFree(out.matching_scores1));
+  if (out.prune0) { HIP_OK(hipFree(out.prune0)); HIP_OK(hipFree(out.prune1)); }
   HIP_OK(hipFree((void*)in.keypoints0)); HIP_OK(hipFree((void*)in.keypoints1));
   HIP_OK(hipFree((void*)in.descriptors0)); HIP_OK(hipFree((void*)in.descriptors1));
   HIP_OK(hipFree((void*)in.image_size0)); HIP_OK(hipFree((void*)in.image_size1));

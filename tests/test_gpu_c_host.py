@@ -50,22 +50,26 @@ def _read_outputs(path):
 
 @pytest.mark.parametrize("adaptive", [False, True], ids=["fixed_depth", "early_stop_and_pruning"])
 def test_c_host_forward_equals_python_forward(tmp_path, adaptive):
-    """adaptive: depth_confidence 0.95 / width_confidence 0.95 (lightglue.py:502-540) on one pair --
-    the C host against the Python class only (both run the same kernels; the oracle's pruning
-    parity is pinned on the goldens in test_gpu_parity.py)."""
+    """adaptive: the golden case prune_depth_width_n2048 (depth / width confidence 0.95, weights that
+    make the reference stop early and prune, lightglue.py:502-540, from tests/golden/make_golden.py):
+    the C host against the Python class bit for bit, and against the reference's own matches and
+    stop layer stored in the golden."""
     import lgamd  # noqa: F401
     import oracle
+    from golden_util import case_inputs, load
     from lightglue_amd import LightGlue
     from lightglue_amd.weights import synthetic_pair, synthetic_state_dict
 
     assert os.path.exists(EXE), "examples/c_host/lg_c_host is built by make -C cs566-project-lightglue_amd/csrc"
-    conf = {"filter_threshold": 0.1}
-    args = ["0.1"]
     if adaptive:
-        conf.update(depth_confidence=0.95, width_confidence=0.95)
-        args += ["0.95", "0.95"]
-    sd = synthetic_state_dict(conf, seed=0)
-    data = synthetic_pair(B=1 if adaptive else 2, M=300, N=277, seed=9)
+        g = load("prune_depth_width_n2048")
+        conf, sd, data = case_inputs(g["meta"])
+        args = [repr(conf["filter_threshold"]), repr(conf["depth_confidence"]), repr(conf["width_confidence"])]
+    else:
+        conf = {"filter_threshold": 0.1}
+        sd = synthetic_state_dict(conf, seed=0)
+        data = synthetic_pair(B=2, M=300, N=277, seed=9)
+        args = ["0.1"]
     w, i, o = (str(tmp_path / n) for n in ("w.bin", "i.bin", "o.bin"))
     _write_weights(w, sd)
     _write_inputs(i, data)
@@ -84,6 +88,11 @@ def test_c_host_forward_equals_python_forward(tmp_path, adaptive):
     for k in ("matches0", "matches1", "matching_scores0", "matching_scores1"):
         np.testing.assert_array_equal(got[k], pred[k].cpu().numpy(), err_msg=k)
     if adaptive:
+        # lg_outputs_t.stop_layer as the C host printed it; the golden's layer count is the reference's
+        stop = int(r.stdout.split("stop layer ")[1].split()[0])
+        assert stop + 1 == int(g["n_layers_run"]) < conf.get("n_layers", 9), (stop, g["n_layers_run"])
+        assert np.asarray(g["prune0"]).min() < np.asarray(g["prune0"]).max()  # the case does prune
+        np.testing.assert_array_equal(got["matches0"], np.asarray(g["matches0"]))
         return
     ref = oracle.lightglue_forward(sd, data, conf)
     np.testing.assert_array_equal(got["matches0"], ref["matches0"].numpy())

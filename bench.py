@@ -363,7 +363,9 @@ def run(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
-    distributed = world > 1
+    # LG_BENCH_DIST=1: the process-group path (RCCL all-gather / DataParallel buckets) at one rank
+    # too -- how tests/test_gpu_bench_dist.py exercises RCCL on a one-GPU box
+    distributed = world > 1 or os.environ.get("LG_BENCH_DIST") == "1"
     selftest = args.selftest_cpu
     if distributed:
         if selftest:

@@ -9,6 +9,6 @@ mkdir -p "$tmp/cs566-project-lightglue_amd"
 cp -r "$root/cs566-project-lightglue_amd/csrc" "$tmp/cs566-project-lightglue_amd/"
 rm -rf "$tmp/cs566-project-lightglue_amd/csrc/build"
 cp -r "$root/include" "$tmp/"
-make -s -C "$tmp/cs566-project-lightglue_amd/csrc" -j8 OUT="$out" EXTRA="$*"
+make -s -C "$tmp/cs566-project-lightglue_amd/csrc" -j8 OUT="$out" EXTRA="$*" "$out"
 rm -rf "$tmp"
 echo "built $out with $*"

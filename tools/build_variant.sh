@@ -6,6 +6,6 @@ rev=$1; out=$(realpath -m "$2")
 root=$(cd "$(dirname "$0")/.." && pwd)
 tmp=$(mktemp -d)
 git -C "$root" archive "$rev" cs566-project-lightglue_amd/csrc include | tar -x -C "$tmp"
-make -s -C "$tmp/cs566-project-lightglue_amd/csrc" -j8 OUT="$out"
+make -s -C "$tmp/cs566-project-lightglue_amd/csrc" -j8 OUT="$out" "$out"
 rm -rf "$tmp"
 echo "built $out from $rev"

@@ -1,8 +1,8 @@
 """The north star's accuracy clause -- HPatches ``H_error_dlt`` AUC within +-0.002 of the reference
 -- on synthetic HPatches-style pairs (HPatches images and trained weights are not available here).
 
-Pairs: 640 x 480 views related by a random homography (corners moved up to 64 px, the HPatches
-viewpoint range), 0.5 px keypoint noise, 20 % of the second view's points replaced by unrelated
+Pairs (16 x 1024 points, and the bench's 32 x 2048): 640 x 480 views related by a random
+homography (corners moved up to 64 px, the HPatches viewpoint range), 0.5 px keypoint noise, 20 % of the second view's points replaced by unrelated
 points and descriptors, the second view shuffled; descriptors unit vectors, the second view's a
 noisy copy.  Weights: the seeded random trunk with each block's ffn.3 scaled by 0.03 (the layers
 move the descriptors a little, so the transformer matters to the result) and assignment heads that
@@ -86,14 +86,15 @@ def dlt_errors(pred, data, Hs):
     return np.asarray(errs)
 
 
-def test_synthetic_hpatches_auc_equals_the_oracle():
+@pytest.mark.parametrize("B,N,seed", [(16, 1024, 2), (32, 2048, 3)], ids=["16x1024", "configs2_32x2048"])
+def test_synthetic_hpatches_auc_equals_the_oracle(B, N, seed):
     import oracle
     from lightglue_amd import LightGlue
     from lightglue_amd import hpatches_metrics as hm
 
     conf = {"filter_threshold": 0.1}
     sd = crafted_state_dict(conf)
-    data, Hs = homography_pairs(16, 1024, seed=2)
+    data, Hs = homography_pairs(B, N, seed=seed)
     dev = torch.device("cuda", 0)
     model = LightGlue(conf).eval().to(dev)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
@@ -106,7 +107,7 @@ def test_synthetic_hpatches_auc_equals_the_oracle():
     e_hip, e_ref = dlt_errors(hip, data, Hs), dlt_errors(ref, data, Hs)
     a_hip, a_ref = hm.summarize_dlt(list(e_hip)), hm.summarize_dlt(list(e_ref))
     print(json.dumps({"auc_hip": a_hip, "auc_oracle": a_ref, "max_pair_error_diff_px": float(np.abs(e_hip - e_ref).max()),
-                      "pairs": len(Hs), "npts": 1024}))
+                      "pairs": len(Hs), "npts": N}))
     for k in a_ref:
         assert abs(a_hip[k] - a_ref[k]) <= AUC_TOL, (k, a_hip[k], a_ref[k])
     # a discriminating case: sub-pixel to pixel errors, so the AUCs move with the matches
